@@ -1,0 +1,211 @@
+"""TEST INFRASTRUCTURE ONLY -- CPU oracle for the NeuMF training hot path.
+
+Only ``tests/``, ``bench.py``'s ``cpu_baseline`` leg and
+``__graft_entry__.smoke()`` may import this module, and only as the checker
+(or the timed CPU baseline) -- never as the thing measured or shipped.  The
+product (``ncf_amd``) never imports it.
+
+What it restates (reference = YonkaMayonkaZ/NCF, paths relative to its root):
+
+* ``OracleNCF``      -- ``src/ncf/models.py:5-46`` (parameters, init RNG order)
+                        and ``:97-118`` (forward), as stock PyTorch CPU ops,
+                        which is what the reference runs on a CPU.
+* ``bce_mean``       -- ``nn.BCEWithLogitsLoss()`` (``scripts/train_neumf.py:86``).
+* ``train_steps``    -- the loop body ``scripts/train_neumf.py:106-118``
+                        (zero_grad / fwd / loss / backward / Adam or SGD step).
+* ``ng_sample``      -- ``src/data/datasets.py:53-69`` via the C restatement
+                        in ``sampler_oracle.c`` (legacy MT19937 + masked
+                        rejection); ``ng_sample_py`` is a pure-Python restatement
+                        for small cases.
+* ``epoch_order``    -- the DataLoader(shuffle=True) protocol
+                        (``scripts/train_neumf.py:55``): per epoch one int64
+                        ``base_seed`` draw, one int64 sampler seed, then
+                        ``randperm`` on a fresh generator; a metrics() pass over
+                        the test loader costs one more draw.
+* ``metrics_np``     -- ``src/training/metrics.py:4-25`` in numpy.
+
+Pinning: every function here is checked against the reference's own outputs
+(``tests/golden/*.npz``, produced by ``tests/golden/make_golden.py`` importing
+the reference in the build container) in ``tests/test_oracle.py``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "_build", "libncf_oracle.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(["make", "-s", "-C", _HERE])
+        lib = ctypes.CDLL(path)
+        lib.oracle_ng_sample.restype = ctypes.c_int64
+        lib.oracle_ng_sample.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32,
+                                         ctypes.c_void_p]
+        lib.oracle_mt_words.restype = None
+        lib.oracle_mt_words.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_void_p]
+        _LIB = lib
+    return _LIB
+
+
+# --------------------------------------------------------------------------- model
+class OracleNCF(nn.Module):
+    """Same parameters, same construction order (hence the same CPU-generator
+    draws) and same forward as the reference NCF (models.py:5-46, 97-118)."""
+
+    def __init__(self, user_num, item_num, factor_num, num_layers, dropout, model_type):
+        super().__init__()
+        self.model_type = model_type
+        self.embed_user_GMF = nn.Embedding(user_num, factor_num)
+        self.embed_item_GMF = nn.Embedding(item_num, factor_num)
+        dm = factor_num * (2 ** (num_layers - 1))
+        self.embed_user_MLP = nn.Embedding(user_num, dm)
+        self.embed_item_MLP = nn.Embedding(item_num, dm)
+        mods = []
+        width = factor_num * (2 ** num_layers)
+        for _ in range(num_layers):
+            mods += [nn.Dropout(p=dropout), nn.Linear(width, width // 2), nn.ReLU()]
+            width //= 2
+        self.MLP_layers = nn.Sequential(*mods)
+        self.predict_layer = nn.Linear(factor_num if model_type in ("GMF", "MLP") else 2 * factor_num, 1)
+        for emb in (self.embed_user_GMF, self.embed_item_GMF, self.embed_user_MLP, self.embed_item_MLP):
+            nn.init.normal_(emb.weight, std=0.01)
+        for m in self.MLP_layers:
+            if isinstance(m, nn.Linear):
+                nn.init.xavier_uniform_(m.weight)
+        nn.init.kaiming_uniform_(self.predict_layer.weight, a=1, nonlinearity="sigmoid")
+
+    def forward(self, user, item):
+        if self.model_type == "GMF":
+            out = self.embed_user_GMF(user) * self.embed_item_GMF(item)
+        elif self.model_type == "MLP":
+            out = self.MLP_layers(torch.cat((self.embed_user_MLP(user), self.embed_item_MLP(item)), -1))
+        else:
+            gmf = self.embed_user_GMF(user) * self.embed_item_GMF(item)
+            mlp = self.MLP_layers(torch.cat((self.embed_user_MLP(user), self.embed_item_MLP(item)), -1))
+            out = torch.cat((gmf, mlp), -1)
+        return self.predict_layer(out).view(-1)
+
+
+def bce_mean(logits, labels):
+    return nn.BCEWithLogitsLoss()(logits, labels.float())
+
+
+def make_optimizer(model, lr, kind="adam"):
+    if kind == "adam":
+        return torch.optim.Adam(model.parameters(), lr=lr)
+    if kind == "sgd":
+        return torch.optim.SGD(model.parameters(), lr=lr)
+    raise ValueError(kind)
+
+
+def train_steps(model, opt, users, items, labels, steps=None):
+    """Reference loop body (train_neumf.py:106-118) over pre-formed batches.
+    users/items/labels: int64 [T, B] (or lists of 1-D arrays).  Returns losses."""
+    losses = []
+    T = len(users) if steps is None else steps
+    for t in range(T):
+        u = torch.as_tensor(np.asarray(users[t]), dtype=torch.int64)
+        i = torch.as_tensor(np.asarray(items[t]), dtype=torch.int64)
+        y = torch.as_tensor(np.asarray(labels[t]), dtype=torch.int64)
+        opt.zero_grad()
+        loss = bce_mean(model(u, i), y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    return losses
+
+
+def forward_backward(model, users, items, labels):
+    """One forward + BCE + backward; returns (logits, loss, {name: grad})."""
+    model.zero_grad(set_to_none=True)
+    u = torch.as_tensor(np.asarray(users), dtype=torch.int64)
+    i = torch.as_tensor(np.asarray(items), dtype=torch.int64)
+    y = torch.as_tensor(np.asarray(labels), dtype=torch.int64)
+    logits = model(u, i)
+    loss = bce_mean(logits, y)
+    loss.backward()
+    grads = {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
+    return logits.detach(), float(loss.item()), grads
+
+
+# --------------------------------------------------------------------------- data stream
+def ng_sample(pos_users, pos_items, num_item, num_ng, seed):
+    """Negatives of datasets.py:53-69 after np.random.seed(seed) (C restatement)."""
+    pu = np.ascontiguousarray(pos_users, dtype=np.int64)
+    pi = np.ascontiguousarray(pos_items, dtype=np.int64)
+    out = np.empty(len(pu) * num_ng, dtype=np.int64)
+    _lib().oracle_ng_sample(pu.ctypes.data, pi.ctypes.data, len(pu), int(num_item), int(num_ng),
+                            int(seed) & 0xFFFFFFFF, out.ctypes.data)
+    return out
+
+
+def mt_words(seed, n):
+    out = np.empty(n, dtype=np.uint32)
+    _lib().oracle_mt_words(int(seed) & 0xFFFFFFFF, int(n), out.ctypes.data)
+    return out
+
+
+def ng_sample_py(pos_users, pos_items, num_item, num_ng, seed):
+    """Pure-Python restatement on numpy's own legacy generator (small cases)."""
+    rs = np.random.RandomState(seed)
+    train = set(zip(np.asarray(pos_users).tolist(), np.asarray(pos_items).tolist()))
+    out = []
+    for u in np.asarray(pos_users).tolist():
+        for _ in range(num_ng):
+            j = rs.randint(num_item)
+            while (u, j) in train:
+                j = rs.randint(num_item)
+            out.append(j)
+    return np.asarray(out, dtype=np.int64)
+
+
+def epoch_order(n, gen: torch.Generator | None = None):
+    """One DataLoader(shuffle=True) epoch on the global (or given) generator:
+    draw base_seed, draw the sampler seed, randperm on a fresh generator."""
+    torch.empty((), dtype=torch.int64).random_(generator=gen)           # _BaseDataLoaderIter base_seed
+    seed = int(torch.empty((), dtype=torch.int64).random_(generator=gen).item())   # RandomSampler
+    g = torch.Generator()
+    g.manual_seed(seed)
+    return torch.randperm(n, generator=g).numpy()
+
+
+def test_pass_draw(gen: torch.Generator | None = None):
+    """metrics() iterating a non-shuffled DataLoader consumes one base_seed draw."""
+    torch.empty((), dtype=torch.int64).random_(generator=gen)
+
+
+# --------------------------------------------------------------------------- metrics
+def metrics_np(logits, items, batch_size, top_k):
+    """metrics.py:4-25 on precomputed logits (ties resolved like a stable argsort of
+    -logits; fixtures are tie-free).  Returns (HR list[int], NDCG list[float])."""
+    logits = np.asarray(logits)
+    items = np.asarray(items)
+    HR, NDCG = [], []
+    for s in range(0, len(items), batch_size):
+        p = logits[s:s + batch_size]
+        it = items[s:s + batch_size]
+        if top_k > len(p):
+            raise RuntimeError("selected index k out of range")
+        idx = np.argsort(-p, kind="stable")[:top_k]
+        rec = it[idx]
+        gt = it[0]
+        hit = gt in rec
+        HR.append(int(hit))
+        NDCG.append(1.0 / np.log2(int(np.where(rec == gt)[0][0]) + 2) if hit else 0.0)
+    return HR, NDCG
+
+
+def flat_state(model):
+    return {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}

@@ -1,0 +1,151 @@
+"""Pin the CPU oracle against the reference's own outputs (tests/golden/*.npz).
+
+No GPU needed.  If these fail, nothing downstream (GPU parity) means anything.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ncf_oracle as O
+
+MODEL_TYPES = ["GMF", "MLP", "NeuMF-end", "NeuMF-pre"]
+SHAPES = [(8, 3), (16, 3), (8, 1)]
+
+
+def _sha(arrs):
+    h = hashlib.sha256()
+    for a in arrs:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+# ---------------------------------------------------------------- G1 negatives
+def test_toy_negatives_kat(golden):
+    g = golden("G1_negatives")
+    toy = g["toy_pos"]
+    neg = O.ng_sample(toy[:, 0], toy[:, 1], int(g["toy_num_item"]), 4, 0)
+    assert neg.tolist() == g["toy_neg_seed0"].tolist() == [4, 0, 3, 3, 3, 3, 4, 0, 4, 2, 1, 1, 1, 0, 1, 4]
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_small_negatives_rejection_heavy(golden, seed):
+    g = golden("G1_negatives")
+    pos = g["small_pos"]
+    neg = O.ng_sample(pos[:, 0], pos[:, 1], int(g["small_num_item"]), 4, seed)
+    assert np.array_equal(neg, g[f"small_neg_seed{seed}"].astype(np.int64))
+    neg_py = O.ng_sample_py(pos[:, 0], pos[:, 1], int(g["small_num_item"]), 4, seed)
+    assert np.array_equal(neg, neg_py)
+
+
+def test_ml100k_shaped_negatives_hash(golden):
+    g = golden("G1_negatives")
+    pos = g["big_pos"].astype(np.int64)
+    neg = O.ng_sample(pos[:, 0], pos[:, 1], int(g["big_num_item"]), 4, 0).astype(np.int32)
+    assert np.array_equal(neg[:4096], g["big_neg_seed0_head"])
+    assert _sha([neg]) == str(g["big_neg_seed0_sha256"])
+
+
+def test_mt_words_match_numpy_legacy():
+    for seed in (0, 1, 12345, 2**32 - 1):
+        rs = np.random.RandomState(seed)
+        ref = rs.randint(0, 2**32, size=5000, dtype=np.uint64).astype(np.uint32)
+        assert np.array_equal(O.mt_words(seed, 5000), ref)
+
+
+# ---------------------------------------------------------------- G2 shuffle
+@pytest.mark.parametrize("seed", [0, 7])
+@pytest.mark.parametrize("n,bs", [(1000, 64), (257, 256)])
+def test_epoch_order_protocol(golden, seed, n, bs):
+    g = golden("G2_shuffle")
+    torch.manual_seed(seed)
+    for ep in range(2):
+        order = O.epoch_order(n)
+        assert np.array_equal(order.astype(np.int32), g[f"s{seed}_n{n}_ep{ep}"])
+        sizes = [min(bs, n - s) for s in range(0, n, bs)]
+        assert sizes == g[f"s{seed}_n{n}_ep{ep}_sizes"].tolist()
+        O.test_pass_draw()
+
+
+# ---------------------------------------------------------------- G3 init
+def test_init_big_sha(golden):
+    g = golden("G3_init")
+    torch.manual_seed(0)
+    m = O.OracleNCF(944, 1683, 8, 3, 0.0, "NeuMF-end")
+    sd = O.flat_state(m)
+    assert list(sd.keys()) == g["big_keys"].tolist()
+    assert _sha(list(sd.values())) == str(g["big_sha256"])
+
+
+@pytest.mark.parametrize("mt", MODEL_TYPES)
+@pytest.mark.parametrize("f,L", SHAPES)
+def test_init_small_exact(golden, mt, f, L):
+    g = golden("G3_init")
+    tag = f"{mt}_f{f}_L{L}"
+    torch.manual_seed(1)
+    m = O.OracleNCF(50, 80, f, L, 0.0, mt)
+    sd = O.flat_state(m)
+    assert list(sd.keys()) == g[f"{tag}_keys"].tolist()
+    for k, v in sd.items():
+        assert np.array_equal(v, g[f"{tag}::{k}"]), k
+    assert sum(p.numel() for p in m.parameters()) == int(g[f"{tag}_nparams"])
+
+
+# ---------------------------------------------------------------- G4 fwd/bwd
+@pytest.mark.parametrize("mt", MODEL_TYPES)
+@pytest.mark.parametrize("f,L", SHAPES)
+def test_forward_backward(golden, mt, f, L):
+    g = golden("G4_fwd_bwd")
+    tag = f"{mt}_f{f}_L{L}"
+    torch.manual_seed(1)
+    m = O.OracleNCF(50, 80, f, L, 0.0, mt)
+    logits, loss, grads = O.forward_backward(m, g["users"], g["items"], g["labels"])
+    np.testing.assert_allclose(logits.numpy(), g[f"{tag}_logits"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(loss, float(g[f"{tag}_loss"]), rtol=1e-6)
+    names = [k.split("::grad::")[1] for k in g.files if k.startswith(tag + "::grad::")]
+    assert sorted(names) == sorted(grads.keys())
+    for k in names:
+        np.testing.assert_allclose(grads[k].numpy(), g[f"{tag}::grad::{k}"], rtol=1e-5, atol=1e-9)
+
+
+def test_spot_values(golden):
+    g = golden("G4_fwd_bwd")
+    torch.manual_seed(0)
+    m = O.OracleNCF(944, 1683, 8, 3, 0.0, "NeuMF-end")
+    p = m(torch.tensor([0, 1, 2, 943]), torch.tensor([0, 1, 2, 1682]))
+    np.testing.assert_array_equal(p.detach().numpy(), g["spot_logits"])
+    loss = O.bce_mean(p, torch.tensor([1, 0, 0, 1]))
+    assert np.float32(loss.item()) == g["spot_loss"]
+
+
+# ---------------------------------------------------------------- G5 trajectories
+@pytest.mark.parametrize("mt,opt", [("NeuMF-end", "adam"), ("GMF", "adam"), ("MLP", "adam"), ("NeuMF-end", "sgd")])
+def test_train_trajectory(golden, mt, opt):
+    g = golden("G5_steps")
+    torch.manual_seed(3)
+    m = O.OracleNCF(50, 80, 8, 3, 0.0, mt)
+    o = O.make_optimizer(m, 1e-3 if opt == "adam" else 1e-2, opt)
+    T = 100 if opt == "adam" else 10
+    losses = O.train_steps(m, o, g["users"], g["items"], g["labels"], steps=T)
+    np.testing.assert_allclose(losses, g[f"{mt}_{opt}_losses"], rtol=1e-6)
+    sd = O.flat_state(m)
+    for k, v in sd.items():
+        np.testing.assert_allclose(v, g[f"{mt}_{opt}_t{T}::{k}"], rtol=1e-5, atol=1e-7)
+
+
+# ---------------------------------------------------------------- G6 metrics
+@pytest.mark.parametrize("bs,k", [(100, 10), (100, 1), (100, 5), (25, 10)])
+def test_metrics(golden, bs, k):
+    g = golden("G6_metrics")
+    test = g["test_pairs"]
+    HR, NDCG = O.metrics_np(g["logits"], test[:, 1], bs, k)
+    assert HR == g[f"bs{bs}_k{k}_HR"].tolist()
+    np.testing.assert_allclose(NDCG, g[f"bs{bs}_k{k}_NDCG"], rtol=0, atol=0)
+
+
+def test_metrics_small_batch_raises(golden):
+    g = golden("G6_metrics")
+    assert bool(g["bs7_k10_raises"])
+    with pytest.raises(RuntimeError):
+        O.metrics_np(g["logits"], g["test_pairs"][:, 1], 7, 10)
