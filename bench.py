@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Headline benchmark: NeuMF training interactions/sec on MI355X.
+
+Workload (BASELINE.json metric "training interactions/sec + HR@10, NeuMF
+factors=64 ml-1m"): NCF(6041, 3707, factor_num=16,
+num_layers=3, 'NeuMF-end') -- 64-wide MLP embeddings, tower [128,64,32,16] --
+on ml-1m-shaped synthetic data (994,169 positives, 4 sampled negatives each,
+bit-exact reference sampler), 65,536 rows per GPU per step, Adam lr 1e-3.
+
+A "step" = fused fwd+loss+bwd kernel, tower-grad reduction, (RCCL all-reduce
+of the gradient bucket when N > 1), dense Adam -- the whole optimizer step of
+scripts/train_neumf.py:111-115, captured once into a hipGraph and replayed.
+The epoch stream (users/items/labels, already shuffled) is resident in HBM
+before the timed region.  Per-GPU work is fixed (65,536 rows/GPU/step), so
+scaling is weak and value = all ranks' rows / max-over-ranks time.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one process per GPU, RCCL).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (dataset shape, factor_num, num_layers, rows per GPU per step)
+    "c3": ("ml-1m", 16, 3, 65536),     # headline: NeuMF-64 (MLP [128,64,32,16])
+    "c2": ("ml-1m", 8, 3, 1024),       # NeuMF [64,32,16,8], bs 1024
+    "c4": ("ml-20m", 16, 3, 65536),    # ml-20m shape
+}
+
+
+def tower_flops_per_row(f, L, model="NeuMF-end"):
+    dm = f * 2 ** (L - 1)
+    s = [(2 * dm) >> k for k in range(L + 1)]
+    fl = 6 * sum(s[k] * s[k + 1] for k in range(L))
+    p = 2 * f if model.startswith("NeuMF") else f
+    return fl + 6 * p
+
+
+def gather_scatter_bytes_per_row(f, L):
+    """Algorithmic HBM bytes per row of the fused kernel: int32 user+item ids,
+    f32 label, the four embedding rows read, and the same four rows' gradient
+    added (f32 atomics: read-modify-write at the memory side)."""
+    dm = f * 2 ** (L - 1)
+    rows = 2 * (f + dm) * 4
+    return 12 + rows + rows
+
+
+def cpu_baseline(f, L, U, I, batch, seconds, threads):
+    """The oracle (oracle/ncf_oracle.py: the reference model restated on stock
+    PyTorch CPU ops + torch.optim.Adam) timed on a bounded sample of the same
+    workload: full 65,536-row steps on random ids of the same id space."""
+    from oracle import ncf_oracle as O
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    m = O.OracleNCF(U, I, f, L, 0.0, "NeuMF-end")
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    rng = np.random.default_rng(0)
+    mk = lambda: (torch.from_numpy(rng.integers(0, U, batch)), torch.from_numpy(rng.integers(0, I, batch)),
+                  torch.from_numpy((rng.random(batch) < 0.2).astype(np.int64)))
+    u, i, y = mk()
+    O.train_steps(m, opt, [u], [i], [y])  # warm-up
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        O.train_steps(m, opt, [u], [i], [y])
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": steps * batch / el, "unit": "interactions/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} x {batch}-row Adam steps of the oracle (reference NCF restated on torch CPU "
+                      f"ops), NCF({U},{I},{f},{L}), {el:.1f} s on {threads} threads "
+                      f"({platform.processor() or platform.machine()})"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--kernel-steps", type=int, default=20, help="eager steps timed per kernel with HIP events")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--skip-cpu-baseline", action="store_true")
+    ap.add_argument("--skip-eval", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run --nproc-per-node N")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+        group = dist.group.WORLD
+
+    from ncf_amd import synthetic
+    from ncf_amd.data import HostSampler, epoch_permutation
+    from ncf_amd.engine import TrainEngine
+    from ncf_amd.models import NCF
+    from ncf_amd import ops
+    import ncf_amd._lib as L
+
+    shape, f, nl, per_gpu = CONFIGS[args.config]
+    global_batch = per_gpu * world
+
+    # ---- data: identical on every rank (seeded) -----------------------------
+    t_data = time.perf_counter()
+    ds = synthetic.make_dataset(shape, seed=0)
+    U, I = ds["user_num"], ds["item_num"]
+    np.random.seed(0)
+    torch.manual_seed(0)
+    sampler = HostSampler(ds["train_users"], ds["train_items"], U, I)
+    t_s = time.perf_counter()
+    neg = sampler.sample(I, 4)
+    t_sample = time.perf_counter() - t_s
+    pu, pi = ds["train_users"], ds["train_items"]
+    users = np.concatenate([pu, np.repeat(pu, 4)]).astype(np.int32)
+    items = np.concatenate([pi, neg]).astype(np.int32)
+    labels = np.concatenate([np.ones(len(pu), np.float32), np.zeros(len(neg), np.float32)])
+    model = NCF(U, I, f, nl, 0.0, "NeuMF-end").to(dev)
+    perm = epoch_permutation(len(users)).to(dev)
+    u_d, i_d, y_d = (torch.from_numpy(users).to(dev), torch.from_numpy(items).to(dev),
+                     torch.from_numpy(labels).to(dev))
+    us, its, ys = torch.empty_like(u_d), torch.empty_like(i_d), torch.empty_like(y_d)
+    L.check(L.hip().ncf_gather_epoch(u_d.data_ptr(), i_d.data_ptr(), y_d.data_ptr(), perm.data_ptr(), len(users),
+                                     us.data_ptr(), its.data_ptr(), ys.data_ptr(), L.stream_ptr(dev)), "gather")
+    eng = TrainEngine(model, lr=1e-3, world_size=world, rank=rank, process_group=group)
+    eng.set_epoch_stream(us, its, ys, global_batch)
+    torch.cuda.synchronize(dev)
+    t_data = time.perf_counter() - t_data
+
+    # ---- warmup (first step eager, then capture) -----------------------------
+    use_graph = not args.no_graph
+    eng.run(max(1, args.warmup), use_graph=use_graph)
+    torch.cuda.synchronize(dev)
+
+    # ---- timed region ----------------------------------------------------------
+    if world > 1:
+        torch.distributed.barrier(group=group, device_ids=[local])
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    eng.run(args.steps, use_graph=use_graph)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    if world > 1:
+        torch.distributed.barrier(group=group, device_ids=[local])
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=group)
+        dt = float(t.item())
+    rows = args.steps * global_batch
+    value = rows / dt
+    losses = eng.epoch_losses()
+    final_loss = float(losses[(eng.state_step() - 1) % eng.num_batches])
+
+    # ---- per-kernel live timing (HIP events on the launch stream) -------------
+    kt = eng.time_kernels(args.kernel_steps)
+    rows_per_launch = per_gpu
+    flops = tower_flops_per_row(f, nl) * rows_per_launch
+    ms = kt["ncf_train_step"]
+    achieved_tf = flops / (ms * 1e-3) / 1e12
+    bytes_launch = gather_scatter_bytes_per_row(f, nl) * rows_per_launch
+    achieved_gbs = bytes_launch / (ms * 1e-3) / 1e9
+    P = sum(p.numel() for p in model.parameters())
+    adam_bytes = 32 * P  # read p,g,m,v; write p,m,v,g(=0)
+    traffic = None
+    tfile = os.environ.get("NCF_PMC_TRAFFIC_JSON")
+    if tfile and os.path.exists(tfile):
+        traffic = json.load(open(tfile)).get("ncf_train_step_bytes_per_launch")
+
+    # ---- quality: HR@10 / NDCG@10 on the leave-one-out test set ---------------
+    hr10 = ndcg10 = None
+    if not args.skip_eval and rank == 0:
+        from ncf_amd.metrics import evaluate_arrays
+        tu = np.repeat(ds["test_users"], 100)
+        ti = np.concatenate([ds["test_items"][:, None], ds["test_negatives"]], 1).reshape(-1)
+        HR, NDCG = evaluate_arrays(model, tu, ti, 100, 10)
+        hr10, ndcg10 = float(np.mean(HR)), float(np.mean(NDCG))
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if not args.skip_cpu_baseline and world == 1:
+            cpu = cpu_baseline(f, nl, U, I, per_gpu, args.cpu_seconds, threads=min(16, os.cpu_count() or 1))
+        out = {
+            "metric": "training interactions/sec (NeuMF factors=64 [MLP 128-64-32-16], ml-1m synthetic)",
+            "value": value,
+            "unit": "interactions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic ml-1m-shaped (6,040 users x 3,706 items, 994,169 train positives, "
+                    "4 bit-exact sampled negatives each; seed 0)",
+            "config": {"workload": f"{args.config.upper()}: NCF(user_num={U}, item_num={I}, factor_num={f}, "
+                                   f"num_layers={nl}, NeuMF-end), Adam lr 1e-3",
+                       "global_batch": global_batch, "per_gpu_batch": per_gpu, "parallelism": f"dp{world}",
+                       "hip_graph": use_graph},
+            "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": 157.3, "unit": "TFLOP/s",
+                         "frac": achieved_tf / 157.3, "traffic": traffic,
+                         "kernel": "ncf_step_kernel<16,3,NeuMF> (fused fwd+bwd)",
+                         "flops_per_launch": flops, "kernel_ms": ms},
+            "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": 8000.0, "unit": "GB/s",
+                             "frac": achieved_gbs / 8000.0, "bytes_per_launch": bytes_launch,
+                             "note": "gather+scatter algorithmic bytes of the same fused kernel"},
+            "kernel_ms": kt,
+            "adam": {"params": P, "bytes": adam_bytes, "ms": kt["optimizer"],
+                     "GB/s": adam_bytes / (kt["optimizer"] * 1e-3) / 1e9},
+            "quality": {"HR@10": hr10, "NDCG@10": ndcg10, "epochs_trained": round(eng.state_step() / eng.num_batches, 2),
+                        "last_batch_loss": final_loss},
+            "cpu_baseline": cpu,
+            "setup_s": {"data+upload": round(t_data, 2), "ng_sample_cpp": round(t_sample, 3)},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.barrier(group=group, device_ids=[local])
+        torch.distributed.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

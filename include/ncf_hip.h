@@ -1,0 +1,139 @@
+/*
+ * ncf_hip.h -- C ABI of libncf_hip.so, the MI355X (gfx950) NeuMF training hot path.
+ *
+ * Plain C: raw device pointers, sizes, and a `void *stream` (a hipStream_t, e.g.
+ * torch.cuda.current_stream().cuda_stream).  No torch or HIP types in any
+ * signature.  Every entry point is asynchronous on `stream`, allocates nothing
+ * (workspaces are passed in) and is therefore capturable into a hipGraph.
+ * Return value: NCF_OK (0) or a negative NCF_E* code; the Python host layer
+ * (ncf_amd/_lib.py) turns a non-zero code into RuntimeError.
+ *
+ * The reference (YonkaMayonkaZ/NCF) has no FFI: its hot path is a set of ATen ops
+ * reached from Python.  Each entry point below replaces the reference code cited
+ * next to it (paths relative to the reference root).
+ */
+#ifndef NCF_HIP_H
+#define NCF_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NCF_ABI_VERSION 1
+
+#define NCF_OK 0
+#define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
+#define NCF_E_ARG (-2)         /* bad pointer / size */
+#define NCF_E_LAUNCH (-3)      /* hipGetLastError() after launch */
+
+/* model_type: src/ncf/models.py:30-33,98-107 */
+#define NCF_MODEL_GMF 0
+#define NCF_MODEL_MLP 1
+#define NCF_MODEL_NEUMF 2 /* "NeuMF-end" and "NeuMF-pre" share the forward */
+
+/* dz_mode of ncf_train_step */
+#define NCF_DZ_BCE 0    /* fused nn.BCEWithLogitsLoss() (mean) from labels (train_neumf.py:86,113) */
+#define NCF_DZ_DLOGIT 1 /* upstream dL/dlogit given per row (autograd backward of NCF.forward) */
+
+/* Flat parameter buffer layout, offsets in floats.  Order and shapes follow the
+ * reference state_dict (models.py:11-34): embed_user_GMF [U,f], embed_item_GMF [I,f],
+ * embed_user_MLP [U,dm], embed_item_MLP [I,dm], MLP_layers.{3k+1}.weight [s_{k+1}, s_k]
+ * and .bias, predict_layer.weight [1,P], .bias [1]; every segment starts 64-float aligned.
+ * [tower_begin, tower_begin + tower_len) covers tower + predict parameters (the part
+ * whose gradient is produced through per-workgroup partial slabs); the float at
+ * tower_begin + tower_len is the loss slot (sum of per-row BCE / global batch). */
+typedef struct ncf_layout {
+    int64_t ug, ig, um, im;
+    int64_t w[4], b[4];
+    int64_t wp, bp;
+    int64_t tower_begin, tower_len;
+    int64_t total; /* floats in the flat buffer, loss slot included */
+    int32_t user_num, item_num, factor_num, num_layers, model_type, pad_;
+} ncf_layout;
+
+/* Device-resident step control block (16-byte aligned, 4 x int64).  Lets a
+ * captured hipGraph replay consecutive batches with no host involvement. */
+typedef struct ncf_step_ctl {
+    int64_t batch;   /* global batch index inside the epoch stream            */
+    int64_t adam_t;  /* optimizer steps completed (torch Adam state['step'])  */
+    int64_t n_total; /* rows in the epoch stream (positives + negatives)      */
+    int64_t done;    /* last-workgroup ticket of ncf_adam_step (keep 0)       */
+} ncf_step_ctl;
+
+int ncf_abi_version(void);
+
+/* 1 if a fused kernel is compiled for this shape, else 0. */
+int ncf_supported(int model_type, int factor_num, int num_layers);
+
+/* Host-only: fill *out for NCF(user_num, item_num, factor_num, num_layers, model_type). */
+int ncf_layout_init(int user_num, int item_num, int factor_num, int num_layers, int model_type,
+                    ncf_layout *out);
+
+/* Workgroups the fused step launches (rows of the partial slab). */
+int ncf_slab_rows(void);
+
+/*
+ * Fused forward + loss + backward for one global batch (replaces, per step,
+ * NCF.forward models.py:97-118, BCEWithLogitsLoss train_neumf.py:113 and
+ * loss.backward() train_neumf.py:114: embedding gathers, GMF product, MLP tower
+ * GEMM+bias+ReLU, predict layer, BCE, tower dgrad/wgrad and embedding_dense_backward).
+ *
+ * Rows: global batch `ctl->batch % ceil(n_total / batch_global)` over the epoch stream
+ * users/items/labels[0 .. ctl->n_total), last batch partial (DataLoader
+ * drop_last=False); this rank takes rows [rank*ceil(gb/world), ...) of it.
+ * grads: dense flat gradient buffer; embedding rows are scatter-added (f32
+ * atomics), the tower/predict part is written per workgroup into
+ * slab[ncf_slab_rows()][tower_len + 1] (reduce with ncf_reduce_slab).
+ * dz_mode NCF_DZ_DLOGIT: `labels` holds dL/dlogit per row instead.
+ * logits_out (optional, may be NULL): per-row logits of this rank's rows.
+ */
+int ncf_train_step(const ncf_layout *lay, const float *params, float *grads,
+                   const int32_t *users, const int32_t *items, const float *labels,
+                   const ncf_step_ctl *ctl, int64_t batch_global, int world, int rank,
+                   int dz_mode, float *slab, float *logits_out, void *stream);
+
+/* Forward only (NCF.forward under no_grad, metrics.py:11-12): logits[n]. */
+int ncf_forward(const ncf_layout *lay, const float *params, const int32_t *users,
+                const int32_t *items, int64_t n, float *logits, void *stream);
+
+/* grads[tower_begin + j] = sum_w slab[w][j] for j <= tower_len (loss slot included). */
+int ncf_reduce_slab(const ncf_layout *lay, const float *slab, float *grads, void *stream);
+
+/*
+ * Dense Adam over the active ranges of the flat buffers (torch.optim.Adam,
+ * _single_tensor_adam arithmetic; train_neumf.py:90,115), grads zeroed after
+ * use (optimizer.zero_grad, train_neumf.py:111).  ranges: host array of
+ * 2*nranges int64 [begin, end) pairs.  t = ctl->adam_t + 1.  The last workgroup
+ * advances ctl->batch and ctl->adam_t and, if loss_hist != NULL, stores
+ * grads[loss_slot] into loss_hist[ctl->batch % hist_len].
+ */
+int ncf_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq,
+                  const int64_t *ranges, int nranges, ncf_step_ctl *ctl, double lr,
+                  double beta1, double beta2, double eps, int64_t loss_slot, float *loss_hist,
+                  int64_t hist_len, void *stream);
+
+/* Plain SGD p -= lr * g (optim.SGD(lr*10) on the --pretraining path, train_neumf.py:87-88). */
+int ncf_sgd_step(float *params, float *grads, const int64_t *ranges, int nranges,
+                 ncf_step_ctl *ctl, double lr, int64_t loss_slot, float *loss_hist, int64_t hist_len,
+                 void *stream);
+
+/* out[k] = src[perm[k]] for the three epoch streams (DataLoader shuffle=True order). */
+int ncf_gather_epoch(const int32_t *users, const int32_t *items, const float *labels,
+                     const int64_t *perm, int64_t n, int32_t *users_out, int32_t *items_out,
+                     float *labels_out, void *stream);
+
+/*
+ * HR@K / NDCG@K per DataLoader batch (metrics.py:4-25): batches of `batch`
+ * consecutive rows (last one partial), ground truth = the batch's first item,
+ * recommends = items of the top_k logits.  hr[b] in {0,1}; ndcg[b] = 1/log2(pos+2).
+ * Returns NCF_E_ARG if a batch is shorter than top_k (torch.topk raises there).
+ */
+int ncf_hr_ndcg(const float *logits, const int32_t *items, int64_t n, int batch, int top_k,
+                int32_t *hr, float *ndcg, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NCF_HIP_H */

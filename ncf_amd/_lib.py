@@ -1,0 +1,142 @@
+"""ctypes bindings of the two in-tree native libraries.
+
+* ``libncf_hip.so``     -- HIP kernels + C ABI, declared in ``include/ncf_hip.h``
+* ``libncf_sampler.so`` -- host C++ negative sampler, ``include/ncf_sampler.h``
+
+There is no fallback: if a library is missing or a call returns an error code,
+this module raises.  ``torch`` is imported first so that the HIP runtime torch
+ships (SONAME ``libamdhip64.so.7``) is the one ``libncf_hip.so`` binds to, and
+streams/pointers from torch are valid in our launches.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede loading libncf_hip.so)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+HIP_LIB_PATH = os.path.join(_HERE, "libncf_hip.so")
+SAMPLER_LIB_PATH = os.path.join(_HERE, "libncf_sampler.so")
+
+NCF_OK = 0
+NCF_E_UNSUPPORTED = -1
+NCF_E_ARG = -2
+NCF_E_LAUNCH = -3
+MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
+DZ_BCE, DZ_DLOGIT = 0, 1
+MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
+
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_vp = ctypes.c_void_p
+
+
+class NcfLayout(ctypes.Structure):
+    _fields_ = [("ug", c_i64), ("ig", c_i64), ("um", c_i64), ("im", c_i64),
+                ("w", c_i64 * 4), ("b", c_i64 * 4), ("wp", c_i64), ("bp", c_i64),
+                ("tower_begin", c_i64), ("tower_len", c_i64), ("total", c_i64),
+                ("user_num", c_i32), ("item_num", c_i32), ("factor_num", c_i32),
+                ("num_layers", c_i32), ("model_type", c_i32), ("pad_", c_i32)]
+
+    @property
+    def loss_slot(self) -> int:
+        return int(self.tower_begin + self.tower_len)
+
+
+class NcfStepCtl(ctypes.Structure):
+    _fields_ = [("batch", c_i64), ("adam_t", c_i64), ("n_total", c_i64), ("done", c_i64)]
+
+
+_HIP_PROTOS = {
+    "ncf_abi_version": (ctypes.c_int, []),
+    "ncf_supported": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "ncf_layout_init": (ctypes.c_int, [ctypes.c_int] * 5 + [ctypes.POINTER(NcfLayout)]),
+    "ncf_slab_rows": (ctypes.c_int, []),
+    "ncf_train_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
+    "ncf_forward": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "ncf_reduce_slab": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp]),
+    "ncf_adam_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.c_int, c_vp,
+                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                     c_i64, c_vp, c_i64, c_vp]),
+    "ncf_sgd_step": (ctypes.c_int, [c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.c_int, c_vp, ctypes.c_double,
+                                    c_i64, c_vp, c_i64, c_vp]),
+    "ncf_gather_epoch": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "ncf_hr_ndcg": (ctypes.c_int, [c_vp, c_vp, c_i64, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
+}
+
+_SAMPLER_PROTOS = {
+    "ncf_sampler_create": (c_vp, [c_vp, c_vp, c_i64, c_i32, c_i32]),
+    "ncf_sampler_destroy": (None, [c_vp]),
+    "ncf_sampler_contains": (ctypes.c_int, [c_vp, c_i32, c_i32]),
+    "ncf_mt_seed": (None, [ctypes.c_uint32, c_vp, c_vp]),
+    "ncf_sampler_sample": (c_i64, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp]),
+}
+
+_lock = threading.Lock()
+_hip = None
+_sampler = None
+
+
+def _load(path, protos, what):
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{what} not found at {path}: build it with `make -C ncf_amd/csrc` "
+            "(or `python -c 'import __graft_entry__ as g; g.build()'`). There is no fallback path.")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in protos.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def hip():
+    """The loaded libncf_hip.so (raises if it is missing)."""
+    global _hip
+    if _hip is None:
+        with _lock:
+            if _hip is None:
+                lib = _load(HIP_LIB_PATH, _HIP_PROTOS, "libncf_hip.so")
+                if lib.ncf_abi_version() != 1:
+                    raise RuntimeError("libncf_hip.so ABI mismatch; rebuild")
+                _hip = lib
+    return _hip
+
+
+def sampler_lib():
+    global _sampler
+    if _sampler is None:
+        with _lock:
+            if _sampler is None:
+                _sampler = _load(SAMPLER_LIB_PATH, _SAMPLER_PROTOS, "libncf_sampler.so")
+    return _sampler
+
+
+def check(code: int, what: str):
+    if code != NCF_OK:
+        names = {NCF_E_UNSUPPORTED: "unsupported shape", NCF_E_ARG: "bad argument", NCF_E_LAUNCH: "HIP launch failed"}
+        raise RuntimeError(f"{what}: {names.get(code, 'error')} (code {code})")
+
+
+def layout(user_num: int, item_num: int, factor_num: int, num_layers: int, model_type) -> NcfLayout:
+    mode = MODEL_CODES[model_type] if isinstance(model_type, str) else int(model_type)
+    lay = NcfLayout()
+    check(hip().ncf_layout_init(int(user_num), int(item_num), int(factor_num), int(num_layers), mode,
+                                ctypes.byref(lay)), "ncf_layout_init")
+    return lay
+
+
+def supported(model_type, factor_num: int, num_layers: int) -> bool:
+    mode = MODEL_CODES[model_type] if isinstance(model_type, str) else int(model_type)
+    return bool(hip().ncf_supported(mode, int(factor_num), int(num_layers)))
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()

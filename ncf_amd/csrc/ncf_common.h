@@ -1,0 +1,30 @@
+// Shared definitions for the NeuMF HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ncf_hip.h"
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// v_mfma_f32_16x16x4_f32: exact f32 FMA chain, 32-cycle issue per SIMD.
+//   A operand: lane l holds A[i = l&15][k = l>>4]
+//   B operand: lane l holds B[k = l>>4][j = l&15]
+//   C/D      : lane l, reg r holds C[i = 4*(l>>4) + r][j = l&15]
+#define MFMA4(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
+
+static constexpr int WAVE = 64;
+
+__device__ __forceinline__ float lane_get(const f4& v, int r) {
+    return r == 0 ? v.x : (r == 1 ? v.y : (r == 2 ? v.z : v.w));
+}
+
+__device__ __forceinline__ float shfl_xor(float v, int m) { return __shfl_xor(v, m, 64); }
+
+// Exact reference-order BCE-with-logits pieces (torch binary_cross_entropy_with_logits):
+//   loss = (1 - y) * x + m + log(exp(-m) + exp(-x - m)),  m = max(-x, 0)
+__device__ __forceinline__ float bce_loss(float x, float y) {
+    float m = fmaxf(-x, 0.0f);
+    return (1.0f - y) * x + m + logf(expf(-m) + expf(-x - m));
+}
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }

@@ -1,0 +1,71 @@
+// Internal (C++) declarations shared by the kernel translation units and the C ABI.
+#pragma once
+#include "ncf_common.h"
+
+namespace ncf {
+
+constexpr int NWAVES = 8;
+constexpr int NTHREADS = NWAVES * WAVE;
+constexpr int TILE_ROWS = NWAVES * 16;
+constexpr int SLAB_ROWS = 256;  // one workgroup per CU on MI355X
+constexpr int LDS_LIMIT_BYTES = 160 * 1024;
+
+template <int F_, int L_, int MODE_>
+struct Shape {
+    static constexpr int F = F_, L = L_, MODE = MODE_;
+    static constexpr bool GMF = MODE != NCF_MODEL_MLP;
+    static constexpr bool MLP = MODE != NCF_MODEL_GMF;
+    static constexpr int DM = F << (L - 1);
+    static constexpr int P = (MODE == NCF_MODEL_NEUMF) ? 2 * F : F;
+    static constexpr int POFF = (MODE == NCF_MODEL_NEUMF) ? F : 0;  // tower output offset in predict input
+    __host__ __device__ static constexpr int S(int k) { return (2 * DM) >> k; }
+    __host__ __device__ static constexpr int MT(int k) { return (S(k + 1) + 15) / 16; }  // output 16-tiles
+    __host__ __device__ static constexpr int KT(int k) { return S(k) / 16; }             // input 16-tiles
+    __host__ __device__ static constexpr int SW(int k) { return S(k) + 4; }              // LDS stride of W_k
+    __host__ __device__ static constexpr int SD(int k) { return 16 * MT(k) + 4; }        // staged dpre_k
+    __host__ __device__ static constexpr int SH(int k) { return S(k) + 4; }              // staged H_k
+    __host__ __device__ static constexpr int wsize(int k) { return MLP ? 16 * MT(k) * SW(k) : 0; }
+    __host__ __device__ static constexpr int woff(int k) { return k == 0 ? 0 : woff(k - 1) + wsize(k - 1); }
+    static constexpr int W_TOTAL = woff(L);
+    __host__ __device__ static constexpr int stsize(int k) {
+        return MLP ? 16 * SD(k) + (k >= 1 ? 16 * SH(k) : 0) : 0;
+    }
+    __host__ __device__ static constexpr int rmax(int par, int k) {
+        return k >= L ? 0
+                      : ((k & 1) == par ? (stsize(k) > rmax(par, k + 1) ? stsize(k) : rmax(par, k + 1))
+                                        : rmax(par, k + 1));
+    }
+    static constexpr int R0 = rmax(0, 0), R1 = rmax(1, 0);
+    static constexpr int WAVE_STAGE = R0 + R1;
+    static constexpr int MISC = 5 * TILE_ROWS;  // su, si, labels, zgmf, dz
+    __host__ __device__ static constexpr int TPW(int k) { return (MT(k) * KT(k) + NWAVES - 1) / NWAVES; }
+    static constexpr int KT0 = MLP ? KT(0) : 1;
+    static_assert(F >= 8 && F <= 64 && (F & (F - 1)) == 0, "factor_num must be 8..64, a power of 2");
+    static_assert(L >= 1 && L <= 4, "num_layers must be 1..4");
+};
+
+struct TrainArgs {
+    ncf_layout lay;
+    const float* params;
+    float* grads;
+    const int32_t* users;
+    const int32_t* items;
+    const float* labels;
+    const ncf_step_ctl* ctl;
+    int64_t batch_global;
+    int world, rank, dz_mode;
+    float* slab;
+    float* logits_out;
+    int64_t fwd_n;  // FWD_ONLY: number of rows
+};
+
+struct KernelEntry {
+    int mode, F, L;
+    const void* train;
+    const void* fwd;
+    int w_total, misc, stage8;  // LDS floats
+};
+
+const KernelEntry* kernel_table(int* n);
+
+}  // namespace ncf

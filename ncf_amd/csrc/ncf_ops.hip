@@ -1,0 +1,405 @@
+// Optimizer, reduction, epoch-shuffle and evaluation kernels + the C ABI
+// (include/ncf_hip.h) of libncf_hip.so.  gfx950 only.
+#include <math.h>
+#include <string.h>
+
+#include "ncf_kernels.h"
+
+namespace ncf {
+
+static inline int64_t rup64(int64_t x) { return (x + 63) / 64 * 64; }
+
+// ---------------------------------------------------------------------------
+// Slab reduction: grads[tb + j] = sum_w slab[w][j], fixed order (bitwise
+// reproducible).  Block = 256 threads = 64 columns x 4 row-quarters.
+__global__ __launch_bounds__(256) void reduce_slab_kernel(const float* __restrict__ slab, float* __restrict__ out,
+                                                          int lo, int len, int rows) {
+    __shared__ float part[4][64];
+    const int jj = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int j = lo + blockIdx.x * 64 + jj;
+    const int per = rows / 4;
+    float s = 0.f;
+    if (j < len) {
+        const float* p = slab + (int64_t)(q * per) * len + j;
+        for (int r = 0; r < per; ++r) s += p[(int64_t)r * len];
+    }
+    part[q][jj] = s;
+    __syncthreads();
+    if (q == 0 && j < len) out[j] = ((part[0][jj] + part[1][jj]) + part[2][jj]) + part[3][jj];
+}
+
+// ---------------------------------------------------------------------------
+// Dense Adam (torch.optim.Adam, single-tensor path) + fused grad zeroing.
+struct Ranges {
+    int64_t begin[8];
+    int64_t prefix[9];  // prefix sums of float4 counts
+    int n;
+};
+
+__device__ __forceinline__ int64_t range_locate(const Ranges& R, int64_t q, int* which) {
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < 8; ++i)
+        if (i < R.n && q >= R.prefix[i]) k = i;
+    *which = k;
+    return R.begin[k] + (q - R.prefix[k]) * 4;
+}
+
+__device__ void step_epilogue(ncf_step_ctl* ctl, float* grads, int64_t loss_slot, float* loss_hist,
+                              int64_t hist_len) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const unsigned long long prev = atomicAdd(reinterpret_cast<unsigned long long*>(&ctl->done), 1ull);
+        if (prev == (unsigned long long)(gridDim.x - 1)) {
+            __threadfence();
+            const int64_t b = ctl->batch;
+            if (loss_hist != nullptr && loss_slot >= 0 && hist_len > 0) loss_hist[b % hist_len] = grads[loss_slot];
+            ctl->batch = b + 1;
+            ctl->adam_t = ctl->adam_t + 1;
+            ctl->done = 0;
+            __threadfence();
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                                   float* __restrict__ v, Ranges R, ncf_step_ctl* ctl, double lr,
+                                                   double beta1, double beta2, float eps, int64_t loss_slot,
+                                                   float* loss_hist, int64_t hist_len) {
+#pragma clang fp contract(off)
+    const double t = (double)(ctl->adam_t + 1);
+    const double bc1 = 1.0 - pow(beta1, t);
+    const double bc2 = 1.0 - pow(beta2, t);
+    const float neg_step = (float)(-(lr / bc1));
+    const float bc2s = (float)sqrt(bc2);
+    const float w1 = (float)(1.0 - beta1);
+    const float b2 = (float)beta2;
+    const float omb2 = (float)(1.0 - beta2);
+    const int64_t total = R.prefix[R.n];
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
+        int which;
+        const int64_t i = range_locate(R, q, &which);
+        f4 gg = *reinterpret_cast<const f4*>(g + i);
+        f4 mm = *reinterpret_cast<const f4*>(m + i);
+        f4 vv = *reinterpret_cast<const f4*>(v + i);
+        f4 pp = *reinterpret_cast<const f4*>(p + i);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float gr = lane_get(gg, r);
+            const float mr = fmaf(w1, gr - lane_get(mm, r), lane_get(mm, r));  // lerp_(g, 1-b1): fmadd form
+            const float vr = lane_get(vv, r) * b2 + omb2 * gr * gr;            // mul_(b2).addcmul_(g, g, 1-b2)
+            const float den = sqrtf(vr) / bc2s + eps;                           // (sqrt(v) / bc2_sqrt).add_(eps)
+            const float pr = lane_get(pp, r) + neg_step * mr / den;             // addcdiv_(m, den, -step_size)
+            if (r == 0) { mm.x = mr; vv.x = vr; pp.x = pr; }
+            else if (r == 1) { mm.y = mr; vv.y = vr; pp.y = pr; }
+            else if (r == 2) { mm.z = mr; vv.z = vr; pp.z = pr; }
+            else { mm.w = mr; vv.w = vr; pp.w = pr; }
+        }
+        *reinterpret_cast<f4*>(m + i) = mm;
+        *reinterpret_cast<f4*>(v + i) = vv;
+        *reinterpret_cast<f4*>(p + i) = pp;
+        *reinterpret_cast<f4*>(g + i) = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    step_epilogue(ctl, g, loss_slot, loss_hist, hist_len);
+}
+
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* __restrict__ g, Ranges R,
+                                                  ncf_step_ctl* ctl, float lr, int64_t loss_slot, float* loss_hist,
+                                                  int64_t hist_len) {
+#pragma clang fp contract(off)
+    const int64_t total = R.prefix[R.n];
+    const float nlr = -lr;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
+        int which;
+        const int64_t i = range_locate(R, q, &which);
+        f4 gg = *reinterpret_cast<const f4*>(g + i);
+        f4 pp = *reinterpret_cast<const f4*>(p + i);
+        pp.x = pp.x + nlr * gg.x;  // param.add_(grad, alpha=-lr)
+        pp.y = pp.y + nlr * gg.y;
+        pp.z = pp.z + nlr * gg.z;
+        pp.w = pp.w + nlr * gg.w;
+        *reinterpret_cast<f4*>(p + i) = pp;
+        *reinterpret_cast<f4*>(g + i) = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    step_epilogue(ctl, g, loss_slot, loss_hist, hist_len);
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gather_epoch_kernel(const int32_t* __restrict__ u, const int32_t* __restrict__ it,
+                                                           const float* __restrict__ y, const int64_t* __restrict__ perm,
+                                                           int64_t n, int32_t* uo, int32_t* io, float* yo) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = perm[k];
+        uo[k] = u[s];
+        io[k] = it[s];
+        yo[k] = y[s];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// HR / NDCG per batch.  One wave per batch; the batch's logits staged in LDS.
+// rank(e) = #{e' : x[e'] > x[e] or (x[e'] == x[e] and e' < e)}  (stable order)
+constexpr int HR_MAXB = 1024;
+__global__ __launch_bounds__(256) void hr_ndcg_kernel(const float* __restrict__ logits, const int32_t* __restrict__ items,
+                                                      int64_t n, int bs, int k, int64_t nb, int32_t* hr, float* ndcg) {
+    __shared__ float sx[4][HR_MAXB];
+    __shared__ int si[4][HR_MAXB];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + w;
+    if (b >= nb) return;  // wave-uniform; no workgroup barrier below
+    const int64_t r0 = b * bs;
+    const int cnt = (int)((n - r0) < bs ? (n - r0) : bs);
+    for (int e = l; e < cnt; e += 64) {
+        sx[w][e] = logits[r0 + e];
+        si[w][e] = items[r0 + e];
+    }
+    __builtin_amdgcn_wave_barrier();  // LDS is in-order per wave: the writes above are seen below
+    const int gt = si[w][0];
+    int best = 0x7fffffff;
+    for (int e = l; e < cnt; e += 64) {
+        if (si[w][e] != gt) continue;
+        const float x = sx[w][e];
+        int rank = 0;
+        for (int e2 = 0; e2 < cnt; ++e2) {
+            const float y = sx[w][e2];
+            rank += (y > x) || (y == x && e2 < e);
+        }
+        if (rank < k && rank < best) best = rank;
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const int o = __shfl_xor(best, m, 64);
+        best = o < best ? o : best;
+    }
+    if (l == 0) {
+        const bool hit = best < k;
+        hr[b] = hit ? 1 : 0;
+        ndcg[b] = hit ? (float)(1.0 / log2((double)best + 2.0)) : 0.0f;
+    }
+}
+
+static const KernelEntry* find_entry(int mode, int F, int L) {
+    int n = 0;
+    const KernelEntry* t = kernel_table(&n);
+    const int Lk = (mode == NCF_MODEL_GMF) ? 1 : L;
+    for (int i = 0; i < n; ++i)
+        if (t[i].mode == mode && t[i].F == F && t[i].L == Lk) return &t[i];
+    return nullptr;
+}
+
+static int64_t train_lds_floats(const KernelEntry* e, const ncf_layout* lay) {
+    const int64_t img = lay->tower_len + 1;
+    return e->w_total + e->misc + (e->stage8 > img ? e->stage8 : img);
+}
+
+static Ranges make_ranges(const int64_t* ranges, int nranges, int* err) {
+    Ranges R;
+    memset(&R, 0, sizeof(R));
+    *err = 0;
+    if (nranges < 1 || nranges > 8) {
+        *err = 1;
+        return R;
+    }
+    R.n = nranges;
+    R.prefix[0] = 0;
+    for (int i = 0; i < nranges; ++i) {
+        const int64_t b = ranges[2 * i], e = ranges[2 * i + 1];
+        if (b < 0 || e < b || (b & 3) || ((e - b) & 3)) *err = 1;
+        R.begin[i] = b;
+        R.prefix[i + 1] = R.prefix[i] + (e - b) / 4;
+    }
+    for (int i = nranges + 1; i < 9; ++i) R.prefix[i] = R.prefix[nranges];
+    return R;
+}
+
+static int launch_status() { return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH; }
+
+// hipFuncSetAttribute once per (kernel, size): nothing but launches happen on
+// the hot path, so a step can be captured into a hipGraph.
+static int ensure_lds(const void* fn, int64_t bytes) {
+    struct Slot { const void* fn; int64_t bytes; };
+    static Slot slots[128];
+    static int nslots = 0;
+    for (int i = 0; i < nslots; ++i)
+        if (slots[i].fn == fn && slots[i].bytes >= bytes) return NCF_OK;
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
+        return NCF_E_LAUNCH;
+    for (int i = 0; i < nslots; ++i)
+        if (slots[i].fn == fn) { slots[i].bytes = bytes; return NCF_OK; }
+    if (nslots < 128) slots[nslots++] = Slot{fn, bytes};
+    return NCF_OK;
+}
+
+}  // namespace ncf
+
+using namespace ncf;
+
+extern "C" {
+
+int ncf_abi_version(void) { return NCF_ABI_VERSION; }
+
+int ncf_slab_rows(void) { return SLAB_ROWS; }
+
+int ncf_layout_init(int U, int I, int F, int L, int mode, ncf_layout* o) {
+    if (!o || U <= 0 || I <= 0 || F <= 0 || L < 1 || L > 4 || mode < 0 || mode > 2) return NCF_E_ARG;
+    memset(o, 0, sizeof(*o));
+    const int64_t DM = (int64_t)F << (L - 1);
+    const int64_t P = mode == NCF_MODEL_NEUMF ? 2 * F : F;
+    int64_t off = 0;
+    o->ug = off; off += rup64((int64_t)U * F);
+    o->ig = off; off += rup64((int64_t)I * F);
+    o->um = off; off += rup64((int64_t)U * DM);
+    o->im = off; off += rup64((int64_t)I * DM);
+    o->tower_begin = off;
+    for (int k = 0; k < 4; ++k) {
+        if (k < L) {
+            const int64_t si = (2 * DM) >> k, so = si / 2;
+            o->w[k] = off; off += rup64(so * si);
+            o->b[k] = off; off += rup64(so);
+        } else {
+            o->w[k] = -1;
+            o->b[k] = -1;
+        }
+    }
+    o->wp = off; off += rup64(P);
+    o->bp = off; off += 64;
+    o->tower_len = off - o->tower_begin;
+    off += 64;  // loss slot + pad
+    o->total = off;
+    o->user_num = U; o->item_num = I; o->factor_num = F; o->num_layers = L; o->model_type = mode;
+    return NCF_OK;
+}
+
+int ncf_supported(int mode, int F, int L) {
+    const KernelEntry* e = find_entry(mode, F, L);
+    if (!e) return 0;
+    ncf_layout lay;
+    if (ncf_layout_init(1, 1, F, L, mode, &lay) != NCF_OK) return 0;
+    return train_lds_floats(e, &lay) * 4 <= LDS_LIMIT_BYTES ? 1 : 0;
+}
+
+int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, const int32_t* users,
+                   const int32_t* items, const float* labels, const ncf_step_ctl* ctl, int64_t batch_global,
+                   int world, int rank, int dz_mode, float* slab, float* logits_out, void* stream) {
+    if (!lay || !params || !grads || !users || !items || !labels || !ctl || !slab) return NCF_E_ARG;
+    if (batch_global <= 0 || world < 1 || rank < 0 || rank >= world) return NCF_E_ARG;
+    if (dz_mode != NCF_DZ_BCE && dz_mode != NCF_DZ_DLOGIT) return NCF_E_ARG;
+    const KernelEntry* e = find_entry(lay->model_type, lay->factor_num, lay->num_layers);
+    if (!e) return NCF_E_UNSUPPORTED;
+    const int64_t lds = train_lds_floats(e, lay) * 4;
+    if (lds > LDS_LIMIT_BYTES) return NCF_E_UNSUPPORTED;
+    if (ensure_lds(e->train, lds) != NCF_OK) return NCF_E_LAUNCH;
+    TrainArgs a;
+    memset(&a, 0, sizeof(a));
+    a.lay = *lay;
+    a.params = params;
+    a.grads = grads;
+    a.users = users;
+    a.items = items;
+    a.labels = labels;
+    a.ctl = ctl;
+    a.batch_global = batch_global;
+    a.world = world;
+    a.rank = rank;
+    a.dz_mode = dz_mode;
+    a.slab = slab;
+    a.logits_out = logits_out;
+    void* args[] = {&a};
+    if (hipLaunchKernel(e->train, dim3(SLAB_ROWS), dim3(NTHREADS), args, (size_t)lds, (hipStream_t)stream) !=
+        hipSuccess)
+        return NCF_E_LAUNCH;
+    return launch_status();
+}
+
+int ncf_forward(const ncf_layout* lay, const float* params, const int32_t* users, const int32_t* items, int64_t n,
+                float* logits, void* stream) {
+    if (!lay || !params || !users || !items || !logits || n < 0) return NCF_E_ARG;
+    if (n == 0) return NCF_OK;
+    const KernelEntry* e = find_entry(lay->model_type, lay->factor_num, lay->num_layers);
+    if (!e) return NCF_E_UNSUPPORTED;
+    const int64_t lds = (int64_t)(e->w_total + e->misc) * 4;
+    if (lds > LDS_LIMIT_BYTES) return NCF_E_UNSUPPORTED;
+    if (ensure_lds(e->fwd, lds) != NCF_OK) return NCF_E_LAUNCH;
+    TrainArgs a;
+    memset(&a, 0, sizeof(a));
+    a.lay = *lay;
+    a.params = params;
+    a.users = users;
+    a.items = items;
+    a.logits_out = logits;
+    a.fwd_n = n;
+    a.world = 1;
+    const int64_t ntiles = (n + TILE_ROWS - 1) / TILE_ROWS;
+    const int grid = (int)(ntiles < 2 * SLAB_ROWS ? ntiles : 2 * SLAB_ROWS);
+    void* args[] = {&a};
+    if (hipLaunchKernel(e->fwd, dim3(grid), dim3(NTHREADS), args, (size_t)lds, (hipStream_t)stream) != hipSuccess)
+        return NCF_E_LAUNCH;
+    return launch_status();
+}
+
+int ncf_reduce_slab(const ncf_layout* lay, const float* slab, float* grads, void* stream) {
+    if (!lay || !slab || !grads) return NCF_E_ARG;
+    const int len = (int)lay->tower_len + 1;
+    const int lo = lay->model_type == NCF_MODEL_GMF ? (int)(lay->wp - lay->tower_begin) : 0;
+    const int blocks = (len - lo + 63) / 64;
+    hipLaunchKernelGGL(reduce_slab_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab,
+                       grads + lay->tower_begin, lo, len, SLAB_ROWS);
+    return launch_status();
+}
+
+int ncf_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, const int64_t* ranges,
+                  int nranges, ncf_step_ctl* ctl, double lr, double beta1, double beta2, double eps,
+                  int64_t loss_slot, float* loss_hist, int64_t hist_len, void* stream) {
+    if (!params || !grads || !exp_avg || !exp_avg_sq || !ranges || !ctl) return NCF_E_ARG;
+    int err = 0;
+    Ranges R = make_ranges(ranges, nranges, &err);
+    if (err) return NCF_E_ARG;
+    const int64_t total = R.prefix[R.n];
+    int64_t grid = (total + 255) / 256;
+    if (grid > 2048) grid = 2048;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(adam_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
+                       exp_avg_sq, R, ctl, lr, beta1, beta2, (float)eps, loss_slot, loss_hist, hist_len);
+    return launch_status();
+}
+
+int ncf_sgd_step(float* params, float* grads, const int64_t* ranges, int nranges, ncf_step_ctl* ctl, double lr,
+                 int64_t loss_slot, float* loss_hist, int64_t hist_len, void* stream) {
+    if (!params || !grads || !ranges || !ctl) return NCF_E_ARG;
+    int err = 0;
+    Ranges R = make_ranges(ranges, nranges, &err);
+    if (err) return NCF_E_ARG;
+    const int64_t total = R.prefix[R.n];
+    int64_t grid = (total + 255) / 256;
+    if (grid > 2048) grid = 2048;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(sgd_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, params, grads, R, ctl, (float)lr,
+                       loss_slot, loss_hist, hist_len);
+    return launch_status();
+}
+
+int ncf_gather_epoch(const int32_t* users, const int32_t* items, const float* labels, const int64_t* perm, int64_t n,
+                     int32_t* users_out, int32_t* items_out, float* labels_out, void* stream) {
+    if (!users || !items || !labels || !perm || !users_out || !items_out || !labels_out || n < 0) return NCF_E_ARG;
+    if (n == 0) return NCF_OK;
+    int64_t grid = (n + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(gather_epoch_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, users, items, labels,
+                       perm, n, users_out, items_out, labels_out);
+    return launch_status();
+}
+
+int ncf_hr_ndcg(const float* logits, const int32_t* items, int64_t n, int batch, int top_k, int32_t* hr, float* ndcg,
+                void* stream) {
+    if (!logits || !items || !hr || !ndcg || n <= 0 || batch <= 0 || batch > HR_MAXB || top_k <= 0) return NCF_E_ARG;
+    const int64_t nb = (n + batch - 1) / batch;
+    const int64_t last = n - (nb - 1) * batch;
+    if (top_k > batch || top_k > last) return NCF_E_ARG;  // torch.topk: "selected index k out of range"
+    const int64_t grid = (nb + 3) / 4;
+    hipLaunchKernelGGL(hr_ndcg_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, logits, items, n, batch,
+                       top_k, nb, hr, ndcg);
+    return launch_status();
+}
+
+}  // extern "C"

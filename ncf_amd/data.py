@@ -1,0 +1,228 @@
+"""Data path of the NeuMF hot loop: ``load_all`` / ``NCFData`` (reference
+src/data/datasets.py:9-83) with the same signatures and semantics, backed by
+numpy arrays and the C++ negative sampler (libncf_sampler.so).
+
+* ``NCFData.ng_sample`` consumes NumPy's *global* legacy RandomState exactly
+  like the reference's Python loop (datasets.py:57-63): the sampler reads the
+  state with ``np.random.get_state()``, draws in C++, and writes it back with
+  ``np.random.set_state()``.  Negatives are bit-identical.
+* ``__getitem__`` returns python ints like the reference; ``__getitems__``
+  (torch >= 2 batched fetch) returns ``[users, items, labels]`` int64 tensors,
+  which the default collate stacks to ``[3, B]`` so ``for user, item, label in
+  loader`` still unpacks correctly while avoiding per-sample Python.
+* ``load_all`` parses the reference file formats literally (no ``eval``).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.utils.data as data
+
+from . import _lib as L
+
+
+def _state_arrays():
+    st = np.random.get_state(legacy=True)
+    if st[0] != "MT19937":
+        raise RuntimeError("numpy global generator is not MT19937")
+    key = np.ascontiguousarray(st[1], dtype=np.uint32).copy()
+    pos = np.array([st[2]], dtype=np.int32)
+    return st, key, pos
+
+
+class HostSampler:
+    """Membership index over the training positives + bit-exact legacy-MT19937
+    negative draws (C++, libncf_sampler.so)."""
+
+    def __init__(self, pos_users, pos_items, num_users, num_items):
+        self.pos_users = np.ascontiguousarray(pos_users, dtype=np.int32)
+        self.pos_items = np.ascontiguousarray(pos_items, dtype=np.int32)
+        self._h = L.sampler_lib().ncf_sampler_create(self.pos_users.ctypes.data, self.pos_items.ctypes.data,
+                                                     len(self.pos_users), int(num_users), int(num_items))
+        if not self._h:
+            raise RuntimeError("ncf_sampler_create failed")
+        self.num_users, self.num_items = int(num_users), int(num_items)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                L.sampler_lib().ncf_sampler_destroy(h)
+            except Exception:
+                pass
+
+    def contains(self, u, i):
+        return bool(L.sampler_lib().ncf_sampler_contains(self._h, int(u), int(i)))
+
+    def sample(self, num_item, num_ng, key=None, pos=None):
+        """Negatives for every positive (file order) x num_ng.  With key/pos None
+        NumPy's global stream is used and advanced (the np.random.seed protocol)."""
+        use_global = key is None
+        if use_global:
+            st, key, pos = _state_arrays()
+        out = np.empty(len(self.pos_users) * int(num_ng), dtype=np.int32)
+        words = L.sampler_lib().ncf_sampler_sample(self._h, int(num_item), int(num_ng), key.ctypes.data,
+                                                   pos.ctypes.data, out.ctypes.data)
+        if words < 0:
+            raise RuntimeError("ncf_sampler_sample: bad arguments")
+        if use_global:
+            np.random.set_state((st[0], key, int(pos[0]), 0, 0.0))
+        return out
+
+
+def _membership_from(train_mat, features):
+    if train_mat is not None and hasattr(train_mat, "keys") and hasattr(train_mat, "shape"):
+        ks = np.array(list(train_mat.keys()), dtype=np.int64).reshape(-1, 2)
+        return ks[:, 0].astype(np.int32), ks[:, 1].astype(np.int32), train_mat.shape
+    return None
+
+
+class NCFData(data.Dataset):
+    """Reference ``NCFData`` (datasets.py:39-83), array-backed."""
+
+    def __init__(self, features, num_item, train_mat=None, num_ng=0, is_training=None):
+        super().__init__()
+        f = np.asarray(features, dtype=np.int64).reshape(-1, 2)
+        self._ps_u = np.ascontiguousarray(f[:, 0], dtype=np.int32)
+        self._ps_i = np.ascontiguousarray(f[:, 1], dtype=np.int32)
+        self.num_item = num_item
+        self.train_mat = train_mat
+        self.num_ng = num_ng
+        self.is_training = is_training
+        self.labels = np.zeros(len(f), dtype=np.int64)
+        self._fill_u = self._fill_i = self._fill_y = None
+        self._ng_u = self._ng_i = None
+        self._sampler = None
+
+    # -- compatibility views (lists, like the reference) ---------------------
+    @property
+    def features_ps(self):
+        return np.stack([self._ps_u, self._ps_i], 1).astype(np.int64).tolist()
+
+    @property
+    def features_ng(self):
+        return np.stack([self._ng_u, self._ng_i], 1).astype(np.int64).tolist()
+
+    @property
+    def features_fill(self):
+        return np.stack([self._fill_u, self._fill_i], 1).astype(np.int64).tolist()
+
+    @property
+    def labels_fill(self):
+        return self._fill_y.astype(np.int64).tolist()
+
+    # -- arrays for the device engine ----------------------------------------
+    def arrays(self):
+        """(users int32, items int32, labels float32) in reference fill order."""
+        if self.is_training:
+            return self._fill_u, self._fill_i, self._fill_y.astype(np.float32)
+        return self._ps_u, self._ps_i, self.labels.astype(np.float32)
+
+    def _get_sampler(self):
+        if self._sampler is None:
+            mem = _membership_from(self.train_mat, None)
+            n_users = int(max(self._ps_u.max(initial=0) + 1, mem[2][0] if mem else 0))
+            n_items = int(max(self.num_item, mem[2][1] if mem else 0))
+            if mem is None or (len(mem[0]) == len(self._ps_u)):
+                # train_mat == the training positives (every reference call site)
+                self._sampler = HostSampler(self._ps_u, self._ps_i, n_users, n_items)
+                if mem is not None and len(mem[0]):
+                    # guard: same set of pairs
+                    a = np.sort(self._ps_u.astype(np.int64) * n_items + self._ps_i)
+                    b = np.sort(mem[0].astype(np.int64) * n_items + mem[1])
+                    if not np.array_equal(np.unique(a), np.unique(b)):
+                        raise NotImplementedError("train_mat differs from the training positives")
+            else:
+                raise NotImplementedError("train_mat differs from the training positives")
+        return self._sampler
+
+    def ng_sample(self):
+        assert self.is_training, "no need to sampling when testing"
+        neg = self._get_sampler().sample(self.num_item, self.num_ng)
+        self._ng_u = np.repeat(self._ps_u, self.num_ng)
+        self._ng_i = neg
+        self._fill_u = np.concatenate([self._ps_u, self._ng_u])
+        self._fill_i = np.concatenate([self._ps_i, self._ng_i])
+        self._fill_y = np.concatenate([np.ones(len(self._ps_u), dtype=np.int64),
+                                       np.zeros(len(self._ng_u), dtype=np.int64)])
+
+    def __len__(self):
+        return (self.num_ng + 1) * len(self.labels)
+
+    def __getitem__(self, idx):
+        if self.is_training:
+            return int(self._fill_u[idx]), int(self._fill_i[idx]), int(self._fill_y[idx])
+        return int(self._ps_u[idx]), int(self._ps_i[idx]), int(self.labels[idx])
+
+    def __getitems__(self, indices):
+        idx = np.asarray(indices, dtype=np.int64)
+        if self.is_training:
+            u, i, y = self._fill_u[idx], self._fill_i[idx], self._fill_y[idx]
+        else:
+            u, i, y = self._ps_u[idx], self._ps_i[idx], self.labels[idx]
+        return [torch.from_numpy(u.astype(np.int64)), torch.from_numpy(i.astype(np.int64)),
+                torch.from_numpy(np.asarray(y, dtype=np.int64))]
+
+
+def parse_train_rating(path):
+    import pandas as pd
+    df = pd.read_csv(path, sep="\t", header=None, names=["user", "item"], usecols=[0, 1],
+                     dtype={0: np.int32, 1: np.int32})
+    return df["user"].to_numpy(np.int32), df["item"].to_numpy(np.int32)
+
+
+def parse_test_negative(path):
+    """'(u,pos)\\tn1\\t...' lines -> (users, items) int32 in file order, pos first."""
+    us, its = [], []
+    with open(path, "r") as fd:
+        for line in fd:
+            line = line.rstrip("\n")
+            if not line:
+                continue
+            arr = line.split("\t")
+            head = arr[0].strip()
+            if not (head.startswith("(") and head.endswith(")")):
+                raise ValueError(f"bad test-negative line head: {head!r}")
+            u_s, p_s = head[1:-1].split(",")
+            u = int(u_s)
+            us.append(u)
+            its.append(int(p_s))
+            for x in arr[1:]:
+                us.append(u)
+                its.append(int(x))
+    return np.asarray(us, dtype=np.int32), np.asarray(its, dtype=np.int32)
+
+
+def load_all(test_num=100):
+    """Reference ``load_all`` (datasets.py:9-36): same return tuple."""
+    import scipy.sparse as sp
+
+    from .config import config
+    tu, ti = parse_train_rating(config.train_rating)
+    user_num = int(tu.max()) + 1
+    item_num = int(ti.max()) + 1
+    train_data = np.stack([tu, ti], 1).astype(np.int64).tolist()
+    coo = sp.coo_matrix((np.ones(len(tu), dtype=np.float32), (tu, ti)), shape=(user_num, item_num))
+    coo.sum_duplicates()
+    coo.data[:] = 1.0
+    train_mat = coo.todok()
+    eu, ei = parse_test_negative(config.test_negative)
+    test_data = np.stack([eu, ei], 1).astype(np.int64).tolist()
+    return train_data, test_data, user_num, item_num, train_mat
+
+
+def epoch_permutation(n, generator=None):
+    """DataLoader(shuffle=True) epoch order on the torch global (or given)
+    generator: one int64 base_seed draw by the loader iterator, one int64 draw
+    seeding RandomSampler's private generator, then randperm(n) -- the exact
+    consumption of scripts/train_neumf.py:55,106 (torch/utils/data)."""
+    torch.empty((), dtype=torch.int64).random_(generator=generator)
+    seed = int(torch.empty((), dtype=torch.int64).random_(generator=generator).item())
+    g = torch.Generator()
+    g.manual_seed(seed)
+    return torch.randperm(n, generator=g)
+
+
+def consume_test_pass(generator=None):
+    """A metrics() pass over the (unshuffled) test DataLoader draws one base_seed."""
+    torch.empty((), dtype=torch.int64).random_(generator=generator)

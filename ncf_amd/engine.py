@@ -1,0 +1,218 @@
+"""Device-resident NeuMF training engine (the fast path behind ``Trainer.fit``).
+
+One optimizer step over one global batch is four launches on the current
+stream, with no host synchronisation and no per-step allocation, so the whole
+step is captured once into a hipGraph and replayed:
+
+  1. ``ncf_train_step``  fused gather / GMF / MFMA tower fwd / BCE / MFMA tower
+                         bwd / embedding scatter-add   (models.py:97-118,
+                         train_neumf.py:111-114)
+  2. ``ncf_reduce_slab`` per-workgroup tower grads -> flat grad buffer
+  3. RCCL all-reduce of the flat grad buffer (world > 1 only; one bucket)
+  4. ``ncf_adam_step``   dense Adam over every active parameter + grad zeroing +
+                         loss bookkeeping + batch/step counters
+                         (train_neumf.py:90,115)
+
+Data parallelism: every rank holds the same epoch stream (same seeds, same
+sampler, same permutation); rank r processes rows [r*ceil(gb/W), ...) of each
+global batch, with dlogit scaled by 1/global_batch, so the summed gradient is
+the single-device mean gradient of ``BCEWithLogitsLoss``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib as L
+from . import ops
+
+
+def _active_ranges(model, lay):
+    """Merged [begin, end) float ranges of the parameters that get gradients."""
+    segs = []
+    sizes = [p.numel() for p in model.ordered_params()]
+    offs = [lay.ug, lay.ig, lay.um, lay.im]
+    for k in range(model.num_layers):
+        offs += [lay.w[k], lay.b[k]]
+    offs += [lay.wp, lay.bp]
+    for off, n, act in zip(offs, sizes, ops.active_mask(model)):
+        if act:
+            segs.append([int(off), int(off + (n + 63) // 64 * 64)])
+    merged = []
+    for b, e in sorted(segs):
+        if merged and merged[-1][1] == b:
+            merged[-1][1] = e
+        else:
+            merged.append([b, e])
+    return merged
+
+
+class TrainEngine:
+    def __init__(self, model, lr=1e-3, optimizer="adam", betas=(0.9, 0.999), eps=1e-8,
+                 world_size=1, rank=0, process_group=None, max_batches=1 << 16):
+        self.model = model
+        self.flat, self.lay = ops.ensure_flat(model)
+        dev = self.flat.device
+        self.device = dev
+        n = int(self.lay.total)
+        self.grads = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.optimizer = optimizer
+        if optimizer == "adam":
+            self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
+            self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        elif optimizer != "sgd":
+            raise ValueError(optimizer)
+        self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
+        self.slab = ops.new_slab(self.lay, dev)
+        self.ctl = ops.new_ctl(0, dev)
+        self.world_size, self.rank, self.group = int(world_size), int(rank), process_group
+        rng = _active_ranges(model, self.lay)
+        self._ranges = (ctypes.c_int64 * (2 * len(rng)))(*[x for r in rng for x in r])
+        self._nranges = len(rng)
+        self.loss_hist = torch.zeros(max_batches, dtype=torch.float32, device=dev)
+        self.users = self.items = self.labels = None
+        self.n_total = 0
+        self.batch_size = None
+        self._graph = None
+        self._graph_key = None
+
+    # ------------------------------------------------------------------ data
+    def set_epoch_stream(self, users_i32, items_i32, labels_f32, batch_size):
+        """Device tensors already in training (shuffled) order."""
+        assert users_i32.dtype == torch.int32 and items_i32.dtype == torch.int32
+        assert labels_f32.dtype == torch.float32
+        assert users_i32.is_contiguous() and items_i32.is_contiguous() and labels_f32.is_contiguous()
+        n = users_i32.numel()
+        if items_i32.numel() != n or labels_f32.numel() != n:
+            raise ValueError("epoch stream arrays must have equal length")
+        self.users, self.items, self.labels = users_i32, items_i32, labels_f32
+        self.n_total = n
+        if self.batch_size != batch_size:
+            self._graph = None
+        self.batch_size = int(batch_size)
+        self.ctl[0] = 0
+        self.ctl[2] = n
+        self.ctl[3] = 0
+
+    @property
+    def num_batches(self):
+        return (self.n_total + self.batch_size - 1) // self.batch_size
+
+    # ------------------------------------------------------------------ step
+    def _step_body(self):
+        st = L.stream_ptr(self.device)
+        lib = L.hip()
+        lay = ctypes.byref(self.lay)
+        L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.users.data_ptr(),
+                                   self.items.data_ptr(), self.labels.data_ptr(), self.ctl.data_ptr(),
+                                   self.batch_size, self.world_size, self.rank, L.DZ_BCE,
+                                   self.slab.data_ptr(), None, st), "ncf_train_step")
+        L.check(lib.ncf_reduce_slab(lay, self.slab.data_ptr(), self.grads.data_ptr(), st), "ncf_reduce_slab")
+        if self.world_size > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.grads, group=self.group)
+        hist_len = self.num_batches
+        if self.optimizer == "adam":
+            L.check(lib.ncf_adam_step(self.flat.data_ptr(), self.grads.data_ptr(), self.exp_avg.data_ptr(),
+                                      self.exp_avg_sq.data_ptr(), self._ranges, self._nranges,
+                                      self.ctl.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps,
+                                      self.lay.loss_slot, self.loss_hist.data_ptr(), hist_len, st),
+                    "ncf_adam_step")
+        else:
+            L.check(lib.ncf_sgd_step(self.flat.data_ptr(), self.grads.data_ptr(), self._ranges, self._nranges,
+                                     self.ctl.data_ptr(), self.lr, self.lay.loss_slot,
+                                     self.loss_hist.data_ptr(), hist_len, st), "ncf_sgd_step")
+
+    def time_kernels(self, n_steps):
+        """Run n_steps eager steps with HIP events around each launch (on the
+        stream the kernels run on) and return mean milliseconds per kernel."""
+        st = torch.cuda.current_stream(self.device)
+        names = ["ncf_train_step", "ncf_reduce_slab", "allreduce", "optimizer"]
+        acc = {k: 0.0 for k in names}
+        lib = L.hip()
+        lay = ctypes.byref(self.lay)
+        sp = L.stream_ptr(self.device)
+        evs = []
+        for _ in range(n_steps):
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+            e[0].record(st)
+            L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.users.data_ptr(),
+                                       self.items.data_ptr(), self.labels.data_ptr(), self.ctl.data_ptr(),
+                                       self.batch_size, self.world_size, self.rank, L.DZ_BCE,
+                                       self.slab.data_ptr(), None, sp), "ncf_train_step")
+            e[1].record(st)
+            L.check(lib.ncf_reduce_slab(lay, self.slab.data_ptr(), self.grads.data_ptr(), sp), "ncf_reduce_slab")
+            e[2].record(st)
+            if self.world_size > 1:
+                import torch.distributed as dist
+                dist.all_reduce(self.grads, group=self.group)
+            e[3].record(st)
+            if self.optimizer == "adam":
+                L.check(lib.ncf_adam_step(self.flat.data_ptr(), self.grads.data_ptr(), self.exp_avg.data_ptr(),
+                                          self.exp_avg_sq.data_ptr(), self._ranges, self._nranges,
+                                          self.ctl.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps,
+                                          self.lay.loss_slot, self.loss_hist.data_ptr(), self.num_batches, sp),
+                        "ncf_adam_step")
+            else:
+                L.check(lib.ncf_sgd_step(self.flat.data_ptr(), self.grads.data_ptr(), self._ranges, self._nranges,
+                                         self.ctl.data_ptr(), self.lr, self.lay.loss_slot,
+                                         self.loss_hist.data_ptr(), self.num_batches, sp), "ncf_sgd_step")
+            e[4].record(st)
+            evs.append(e)
+        torch.cuda.synchronize(self.device)
+        for e in evs:
+            for k, name in enumerate(names):
+                acc[name] += e[k].elapsed_time(e[k + 1])
+        return {k: v / max(1, n_steps) for k, v in acc.items()}
+
+    def step(self):
+        """One optimizer step on global batch ctl.batch (eager launches)."""
+        self._step_body()
+
+    def capture(self):
+        """Capture one step into a hipGraph (after at least one eager step)."""
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self._step_body()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self._graph = g
+        self._graph_key = (self.batch_size, self.n_total, self.users.data_ptr())
+        return g
+
+    def run(self, n_steps, use_graph=True):
+        """n_steps consecutive optimizer steps (batches advance on device)."""
+        if not use_graph:
+            for _ in range(n_steps):
+                self._step_body()
+            return
+        key = (self.batch_size, self.n_total, self.users.data_ptr())
+        done = 0
+        if self._graph is None or self._graph_key != key:
+            # eager first step also sets kernel attributes outside the capture
+            self._step_body()
+            done = 1
+            if n_steps <= 1:
+                return
+            # capture replays the *current* batch: rewind the counters it advanced
+            self.capture()
+            # the captured body was not executed during capture
+        for _ in range(n_steps - done):
+            self._graph.replay()
+
+    def epoch_losses(self):
+        """Per-batch mean BCE of the last epoch (host copy)."""
+        return self.loss_hist[: self.num_batches].double().cpu().numpy()
+
+    def state_step(self):
+        return int(self.ctl[1].item())
+
+    def zero_state(self):
+        self.grads.zero_()
+        if self.optimizer == "adam":
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+        self.ctl[1] = 0

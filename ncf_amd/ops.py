@@ -1,0 +1,138 @@
+"""Device-side operators of the NeuMF hot path (torch tensors -> C ABI pointers).
+
+``ensure_flat`` packs a HIP-resident NCF's parameters into one flat fp32 buffer
+laid out by ``ncf_layout_init`` (include/ncf_hip.h) and rebinds every
+``nn.Parameter`` to a view of it, so the kernels read the live weights and the
+module's ``state_dict`` / stock optimizers keep working.
+
+``ncf_forward`` is the autograd-visible forward of ``NCF`` on a HIP device
+(reference models.py:97-118); its backward is the same fused kernel in
+``NCF_DZ_DLOGIT`` mode (replacing the ATen autograd graph that
+``loss.backward()`` walks in train_neumf.py:114).  Everything runs on
+``torch.cuda.current_stream()``.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+
+
+def _segments(model, lay):
+    """(param, flat offset) in model.ordered_params() order."""
+    offs = [lay.ug, lay.ig, lay.um, lay.im]
+    for k in range(model.num_layers):
+        offs += [lay.w[k], lay.b[k]]
+    offs += [lay.wp, lay.bp]
+    return list(zip(model.ordered_params(), offs))
+
+
+def active_mask(model):
+    """Which ordered params receive gradients (reference: unused tables keep
+    .grad None in GMF / MLP mode, so torch Adam skips them)."""
+    n_tower = 2 * model.num_layers
+    if model.model_type == "GMF":
+        return [True, True, False, False] + [False] * n_tower + [True, True]
+    if model.model_type == "MLP":
+        return [False, False, True, True] + [True] * n_tower + [True, True]
+    return [True] * (4 + n_tower + 2)
+
+
+def ensure_flat(model):
+    """Return (flat, layout) for a HIP-resident NCF, (re)packing if needed."""
+    lay = getattr(model, "_ncf_layout", None)
+    flat = getattr(model, "_ncf_flat", None)
+    dev = model.embed_user_GMF.weight.device
+    if lay is None:
+        lay = L.layout(model.user_num, model.item_num, model.factor_num, model.num_layers, model.model_type)
+        model._ncf_layout = lay
+    if flat is not None and flat.device == dev:
+        ok = all(p.data_ptr() == flat.data_ptr() + 4 * off for p, off in _segments(model, lay))
+        if ok:
+            return flat, lay
+    if not L.supported(model.model_type, model.factor_num, model.num_layers):
+        raise NotImplementedError(
+            f"no fused HIP kernel for model_type={model.model_type} factor_num={model.factor_num} "
+            f"num_layers={model.num_layers}")
+    flat = torch.zeros(int(lay.total), dtype=torch.float32, device=dev)
+    with torch.no_grad():
+        for p, off in _segments(model, lay):
+            n = p.numel()
+            view = flat[off:off + n].view_as(p)
+            view.copy_(p.data)
+            p.data = view
+    model._ncf_flat = flat
+    return flat, lay
+
+
+def _as_i32(x, dev):
+    x = torch.as_tensor(x, device=dev)
+    if x.dtype != torch.int32:
+        x = x.to(torch.int32)
+    return x.contiguous()
+
+
+def forward_logits(flat, lay, users_i32, items_i32, out=None):
+    n = users_i32.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=flat.device)
+    L.check(L.hip().ncf_forward(L.ctypes.byref(lay), flat.data_ptr(), users_i32.data_ptr(),
+                                items_i32.data_ptr(), n, out.data_ptr(), L.stream_ptr(flat.device)),
+            "ncf_forward")
+    return out
+
+
+def fused_backward(flat, lay, users_i32, items_i32, dlogit, gflat, slab, ctl):
+    """grads of sum_i dlogit[i] * logit[i] into gflat (zero-initialised)."""
+    n = users_i32.numel()
+    dev = flat.device
+    st = L.stream_ptr(dev)
+    L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), users_i32.data_ptr(),
+                                   items_i32.data_ptr(), dlogit.data_ptr(), ctl.data_ptr(), int(n), 1, 0,
+                                   L.DZ_DLOGIT, slab.data_ptr(), None, st), "ncf_train_step")
+    L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), st),
+            "ncf_reduce_slab")
+
+
+def new_slab(lay, dev):
+    return torch.empty((L.hip().ncf_slab_rows(), int(lay.tower_len) + 1), dtype=torch.float32, device=dev)
+
+
+def new_ctl(n_total, dev, batch=0, adam_t=0):
+    return torch.tensor([batch, adam_t, n_total, 0], dtype=torch.int64, device=dev)
+
+
+class _NCFFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, users, items, model, *params):
+        flat, lay = model._ncf_flat, model._ncf_layout
+        logits = forward_logits(flat, lay, users, items)
+        ctx.model = model
+        ctx.save_for_backward(users, items)
+        return logits
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        users, items = ctx.saved_tensors
+        model = ctx.model
+        flat, lay = model._ncf_flat, model._ncf_layout
+        dev = flat.device
+        gflat = torch.zeros(int(lay.total), dtype=torch.float32, device=dev)
+        slab = new_slab(lay, dev)
+        ctl = new_ctl(users.numel(), dev)
+        dlogit = grad_out.contiguous().to(torch.float32)
+        fused_backward(flat, lay, users, items, dlogit, gflat, slab, ctl)
+        grads = []
+        for (p, off), act in zip(_segments(model, lay), active_mask(model)):
+            grads.append(gflat[off:off + p.numel()].view_as(p) if act and p.requires_grad else None)
+        return (None, None, None, *grads)
+
+
+def ncf_forward(model, user, item):
+    flat, lay = ensure_flat(model)
+    dev = flat.device
+    u = _as_i32(user, dev).view(-1)
+    i = _as_i32(item, dev).view(-1)
+    if torch.is_grad_enabled() and any(p.requires_grad for p in model.ordered_params()):
+        return _NCFFunction.apply(u, i, model, *model.ordered_params())
+    return forward_logits(flat, lay, u, i)

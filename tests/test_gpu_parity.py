@@ -1,0 +1,210 @@
+"""GPU parity: the HIP path (libncf_hip.so through its C ABI) against the CPU
+oracle (oracle/ncf_oracle.py, itself pinned to the reference in test_oracle.py)
+and the reference's golden vectors.
+
+Tolerances (north star: "within 1e-5 relative for fp32 loss/logits"):
+  * logits / loss: rtol 1e-5 (atol 1e-7 for near-zero logits)
+  * one-step gradients: rtol 1e-4 + atol 1e-6*max|g| (summation order differs:
+    atomics and MFMA K-order vs ATen's CPU kernels)
+  * Adam trajectories: per-step loss rtol 1e-5 over 100 steps; parameters
+    rtol 1e-4, atol 1e-6 after 100 steps.
+  * HR / NDCG: exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ncf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+MODEL_TYPES = ["GMF", "MLP", "NeuMF-end", "NeuMF-pre"]
+SHAPES = [(8, 3), (16, 3), (8, 1)]
+DEV = "cuda:0"
+
+
+def _models(mt, f, L, U=50, I=80, seed=1):
+    from ncf_amd.models import NCF
+    torch.manual_seed(seed)
+    ref = O.OracleNCF(U, I, f, L, 0.0, mt)
+    torch.manual_seed(seed)
+    m = NCF(U, I, f, L, 0.0, mt)
+    for (k1, v1), (k2, v2) in zip(ref.state_dict().items(), m.state_dict().items()):
+        assert k1 == k2 and torch.equal(v1, v2)
+    return ref, m.to(DEV)
+
+
+def _close_grad(got, exp, name):
+    scale = max(float(np.abs(exp).max()), 1e-30)
+    np.testing.assert_allclose(got, exp, rtol=1e-4, atol=1e-6 * scale, err_msg=name)
+
+
+@pytest.mark.parametrize("mt", MODEL_TYPES)
+@pytest.mark.parametrize("f,L", SHAPES)
+def test_module_forward_backward_vs_golden(golden, mt, f, L):
+    g = golden("G4_fwd_bwd")
+    tag = f"{mt}_f{f}_L{L}"
+    _, m = _models(mt, f, L)
+    u = torch.from_numpy(g["users"]).to(DEV)
+    i = torch.from_numpy(g["items"]).to(DEV)
+    y = torch.from_numpy(g["labels"]).float().to(DEV)
+    pred = m(u, i)
+    np.testing.assert_allclose(pred.detach().cpu().numpy(), g[f"{tag}_logits"], rtol=1e-5, atol=1e-7)
+    loss = torch.nn.BCEWithLogitsLoss()(pred, y)
+    np.testing.assert_allclose(loss.item(), float(g[f"{tag}_loss"]), rtol=1e-5)
+    loss.backward()
+    for k, p in m.named_parameters():
+        key = f"{tag}::grad::{k}"
+        if key in g.files:
+            assert p.grad is not None, k
+            _close_grad(p.grad.cpu().numpy(), g[key], k)
+        else:
+            assert p.grad is None, f"{k} must keep grad None in {mt} mode"
+
+
+def test_forward_edge_sizes():
+    ref, m = _models("NeuMF-end", 16, 3, U=300, I=500, seed=4)
+    for n in (1, 15, 127, 128, 129, 1000, 4097):
+        rng = np.random.default_rng(n)
+        u = rng.integers(0, 300, n)
+        i = rng.integers(0, 500, n)
+        with torch.no_grad():
+            exp = ref(torch.from_numpy(u), torch.from_numpy(i)).numpy()
+            got = m(torch.from_numpy(u).to(DEV), torch.from_numpy(i).to(DEV)).cpu().numpy()
+        np.testing.assert_allclose(got, exp, rtol=1e-5, atol=1e-7)
+
+
+def _engine_for(mt, f, L, U, I, seed, optimizer="adam", lr=1e-3):
+    from ncf_amd.engine import TrainEngine
+    ref, m = _models(mt, f, L, U=U, I=I, seed=seed)
+    eng = TrainEngine(m, lr=lr, optimizer=optimizer)
+    return ref, m, eng
+
+
+def _stream(eng, users, items, labels, bs):
+    u = torch.as_tensor(np.asarray(users).reshape(-1), dtype=torch.int32, device=DEV).contiguous()
+    i = torch.as_tensor(np.asarray(items).reshape(-1), dtype=torch.int32, device=DEV).contiguous()
+    y = torch.as_tensor(np.asarray(labels).reshape(-1), dtype=torch.float32, device=DEV).contiguous()
+    eng.set_epoch_stream(u, i, y, bs)
+
+
+@pytest.mark.parametrize("mt,opt", [("NeuMF-end", "adam"), ("GMF", "adam"), ("MLP", "adam"), ("NeuMF-end", "sgd")])
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_engine_trajectory_vs_golden(golden, mt, opt, use_graph):
+    g = golden("G5_steps")
+    T = 100 if opt == "adam" else 10
+    ref, m, eng = _engine_for(mt, 8, 3, 50, 80, 3, optimizer=opt, lr=1e-3 if opt == "adam" else 1e-2)
+    _stream(eng, g["users"][:T], g["items"][:T], g["labels"][:T], 256)
+    eng.run(T, use_graph=use_graph)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(eng.epoch_losses()[:T], g[f"{mt}_{opt}_losses"][:T], rtol=1e-5)
+    sd = m.state_dict()
+    for k, v in sd.items():
+        np.testing.assert_allclose(v.cpu().numpy(), g[f"{mt}_{opt}_t{T}::{k}"], rtol=1e-4, atol=1e-6, err_msg=k)
+    assert eng.state_step() == T
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3", "default"])
+def test_one_step_grads_vs_oracle(cfg):
+    """Full-size shapes (ml-1m ids): logits, loss and every gradient of one step."""
+    import ncf_amd._lib as L
+    from ncf_amd import ops
+    f, Lyr, B = {"C2": (8, 3, 1024), "C3": (16, 3, 8192), "default": (32, 2, 4096)}[cfg]
+    U, I = 6041, 3707
+    ref, m = _models("NeuMF-end", f, Lyr, U=U, I=I, seed=11)
+    rng = np.random.default_rng(3)
+    users = rng.integers(0, U, B)
+    items = np.minimum(rng.zipf(1.3, B) - 1, I - 1)  # hot items: heavy atomic contention
+    labels = (rng.random(B) < 0.2).astype(np.int64)
+    logits_ref, loss_ref, grads_ref = O.forward_backward(ref, users, items, labels)
+    flat, lay = ops.ensure_flat(m)
+    gflat = torch.zeros(int(lay.total), device=DEV)
+    slab = ops.new_slab(lay, DEV)
+    ctl = ops.new_ctl(B, DEV)
+    u = torch.as_tensor(users, dtype=torch.int32, device=DEV)
+    it = torch.as_tensor(items, dtype=torch.int32, device=DEV)
+    y = torch.as_tensor(labels, dtype=torch.float32, device=DEV)
+    logits = torch.empty(B, device=DEV)
+    st = L.stream_ptr()
+    L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), u.data_ptr(),
+                                   it.data_ptr(), y.data_ptr(), ctl.data_ptr(), B, 1, 0, L.DZ_BCE,
+                                   slab.data_ptr(), logits.data_ptr(), st), "train")
+    L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), st), "reduce")
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(logits.cpu().numpy(), logits_ref.numpy(), rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(gflat[lay.loss_slot].item(), loss_ref, rtol=1e-5)
+    for (p, off), (name, _) in zip(ops._segments(m, lay), m.named_parameters()):
+        got = gflat[off:off + p.numel()].view_as(p).cpu().numpy()
+        _close_grad(got, grads_ref[name].numpy(), name)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rank_shards_sum_to_full_batch(world):
+    """DP decomposition: sum over ranks of shard grads == single-device grads."""
+    import ncf_amd._lib as L
+    from ncf_amd import ops
+    U, I, B = 6041, 3707, 3000
+    _, m = _models("NeuMF-end", 16, 3, U=U, I=I, seed=5)
+    flat, lay = ops.ensure_flat(m)
+    rng = np.random.default_rng(9)
+    u = torch.as_tensor(rng.integers(0, U, B), dtype=torch.int32, device=DEV)
+    it = torch.as_tensor(rng.integers(0, I, B), dtype=torch.int32, device=DEV)
+    y = torch.as_tensor((rng.random(B) < 0.2), dtype=torch.float32, device=DEV)
+    st = L.stream_ptr()
+
+    def run(world, rank):
+        gflat = torch.zeros(int(lay.total), device=DEV)
+        slab = ops.new_slab(lay, DEV)
+        ctl = ops.new_ctl(B, DEV)
+        L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), u.data_ptr(),
+                                       it.data_ptr(), y.data_ptr(), ctl.data_ptr(), B, world, rank, L.DZ_BCE,
+                                       slab.data_ptr(), None, st), "train")
+        L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), st), "reduce")
+        return gflat
+    full = run(1, 0)
+    parts = sum(run(world, r) for r in range(world))
+    torch.cuda.synchronize()
+    d = (parts - full).abs().max().item()
+    assert d <= 1e-6 * full.abs().max().item() + 1e-9, d
+
+
+@pytest.mark.parametrize("bs,k", [(100, 10), (100, 1), (100, 5), (25, 10)])
+def test_hr_ndcg_vs_golden(golden, bs, k):
+    import ncf_amd._lib as L
+    g = golden("G6_metrics")
+    logits = torch.as_tensor(g["logits"], device=DEV)
+    items = torch.as_tensor(g["test_pairs"][:, 1], dtype=torch.int32, device=DEV)
+    n = items.numel()
+    nb = (n + bs - 1) // bs
+    hr = torch.empty(nb, dtype=torch.int32, device=DEV)
+    nd = torch.empty(nb, dtype=torch.float32, device=DEV)
+    L.check(L.hip().ncf_hr_ndcg(logits.data_ptr(), items.data_ptr(), n, bs, k, hr.data_ptr(), nd.data_ptr(),
+                                L.stream_ptr()), "hr")
+    torch.cuda.synchronize()
+    assert hr.cpu().tolist() == g[f"bs{bs}_k{k}_HR"].tolist()
+    np.testing.assert_allclose(nd.cpu().numpy(), g[f"bs{bs}_k{k}_NDCG"], rtol=1e-6)
+
+
+def test_hr_ndcg_short_batch_raises(golden):
+    import ncf_amd._lib as L
+    g = golden("G6_metrics")
+    logits = torch.as_tensor(g["logits"], device=DEV)
+    items = torch.as_tensor(g["test_pairs"][:, 1], dtype=torch.int32, device=DEV)
+    hr = torch.empty(10000, dtype=torch.int32, device=DEV)
+    nd = torch.empty(10000, dtype=torch.float32, device=DEV)
+    assert L.hip().ncf_hr_ndcg(logits.data_ptr(), items.data_ptr(), items.numel(), 7, 10, hr.data_ptr(),
+                               nd.data_ptr(), L.stream_ptr()) == L.NCF_E_ARG
+
+
+def test_gather_epoch():
+    import ncf_amd._lib as L
+    n = 10007
+    rng = np.random.default_rng(0)
+    u = torch.as_tensor(rng.integers(0, 100, n), dtype=torch.int32, device=DEV)
+    i = torch.as_tensor(rng.integers(0, 100, n), dtype=torch.int32, device=DEV)
+    y = torch.as_tensor(rng.random(n), dtype=torch.float32, device=DEV)
+    perm = torch.randperm(n, device=DEV)
+    uo, io, yo = torch.empty_like(u), torch.empty_like(i), torch.empty_like(y)
+    L.check(L.hip().ncf_gather_epoch(u.data_ptr(), i.data_ptr(), y.data_ptr(), perm.data_ptr(), n, uo.data_ptr(),
+                                     io.data_ptr(), yo.data_ptr(), L.stream_ptr()), "gather")
+    assert torch.equal(uo, u[perm]) and torch.equal(io, i[perm]) and torch.equal(yo, y[perm])
