@@ -84,6 +84,39 @@ def cpu_baseline(f, L, U, I, batch, seconds, threads):
                       f"({platform.processor() or platform.machine()})"}
 
 
+def setup_engine(config, world, rank, dev, group, global_batch, seed=0):
+    """Synthetic dataset -> bit-exact negatives -> shuffled epoch stream in HBM
+    -> NCF + TrainEngine.  Identical on every rank (seeded)."""
+    from ncf_amd import synthetic
+    from ncf_amd.data import HostSampler, epoch_permutation
+    from ncf_amd.engine import TrainEngine
+    from ncf_amd.models import NCF
+    import ncf_amd._lib as L
+    shape, f, nl, _ = CONFIGS[config]
+    ds = synthetic.make_dataset(shape, seed=seed)
+    U, I = ds["user_num"], ds["item_num"]
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    sampler = HostSampler(ds["train_users"], ds["train_items"], U, I)
+    t_s = time.perf_counter()
+    neg = sampler.sample(I, 4)
+    t_sample = time.perf_counter() - t_s
+    pu, pi = ds["train_users"], ds["train_items"]
+    users = np.concatenate([pu, np.repeat(pu, 4)]).astype(np.int32)
+    items = np.concatenate([pi, neg]).astype(np.int32)
+    labels = np.concatenate([np.ones(len(pu), np.float32), np.zeros(len(neg), np.float32)])
+    model = NCF(U, I, f, nl, 0.0, "NeuMF-end").to(dev)
+    perm = epoch_permutation(len(users)).to(dev)
+    u_d, i_d, y_d = (torch.from_numpy(users).to(dev), torch.from_numpy(items).to(dev),
+                     torch.from_numpy(labels).to(dev))
+    us, its, ys = torch.empty_like(u_d), torch.empty_like(i_d), torch.empty_like(y_d)
+    L.check(L.hip().ncf_gather_epoch(u_d.data_ptr(), i_d.data_ptr(), y_d.data_ptr(), perm.data_ptr(), len(users),
+                                     us.data_ptr(), its.data_ptr(), ys.data_ptr(), L.stream_ptr(dev)), "gather")
+    eng = TrainEngine(model, lr=1e-3, world_size=world, rank=rank, process_group=group)
+    eng.set_epoch_stream(us, its, ys, global_batch)
+    return eng, model, ds, t_sample
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -112,39 +145,11 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
         group = dist.group.WORLD
 
-    from ncf_amd import synthetic
-    from ncf_amd.data import HostSampler, epoch_permutation
-    from ncf_amd.engine import TrainEngine
-    from ncf_amd.models import NCF
-    from ncf_amd import ops
-    import ncf_amd._lib as L
-
     shape, f, nl, per_gpu = CONFIGS[args.config]
     global_batch = per_gpu * world
-
-    # ---- data: identical on every rank (seeded) -----------------------------
     t_data = time.perf_counter()
-    ds = synthetic.make_dataset(shape, seed=0)
+    eng, model, ds, t_sample = setup_engine(args.config, world, rank, dev, group, global_batch)
     U, I = ds["user_num"], ds["item_num"]
-    np.random.seed(0)
-    torch.manual_seed(0)
-    sampler = HostSampler(ds["train_users"], ds["train_items"], U, I)
-    t_s = time.perf_counter()
-    neg = sampler.sample(I, 4)
-    t_sample = time.perf_counter() - t_s
-    pu, pi = ds["train_users"], ds["train_items"]
-    users = np.concatenate([pu, np.repeat(pu, 4)]).astype(np.int32)
-    items = np.concatenate([pi, neg]).astype(np.int32)
-    labels = np.concatenate([np.ones(len(pu), np.float32), np.zeros(len(neg), np.float32)])
-    model = NCF(U, I, f, nl, 0.0, "NeuMF-end").to(dev)
-    perm = epoch_permutation(len(users)).to(dev)
-    u_d, i_d, y_d = (torch.from_numpy(users).to(dev), torch.from_numpy(items).to(dev),
-                     torch.from_numpy(labels).to(dev))
-    us, its, ys = torch.empty_like(u_d), torch.empty_like(i_d), torch.empty_like(y_d)
-    L.check(L.hip().ncf_gather_epoch(u_d.data_ptr(), i_d.data_ptr(), y_d.data_ptr(), perm.data_ptr(), len(users),
-                                     us.data_ptr(), its.data_ptr(), ys.data_ptr(), L.stream_ptr(dev)), "gather")
-    eng = TrainEngine(model, lr=1e-3, world_size=world, rank=rank, process_group=group)
-    eng.set_epoch_stream(us, its, ys, global_batch)
     torch.cuda.synchronize(dev)
     t_data = time.perf_counter() - t_data
 

@@ -59,7 +59,7 @@ typedef struct ncf_step_ctl {
     int64_t batch;   /* global batch index inside the epoch stream            */
     int64_t adam_t;  /* optimizer steps completed (torch Adam state['step'])  */
     int64_t n_total; /* rows in the epoch stream (positives + negatives)      */
-    int64_t done;    /* last-workgroup ticket of ncf_adam_step (keep 0)       */
+    int64_t reserved; /* keep 0                                               */
 } ncf_step_ctl;
 
 int ncf_abi_version(void);
@@ -74,6 +74,9 @@ int ncf_layout_init(int user_num, int item_num, int factor_num, int num_layers, 
 /* Workgroups the fused step launches (rows of the partial slab). */
 int ncf_slab_rows(void);
 
+/* Floats per slab row: tower_len + 64 (16-byte aligned rows; loss at index tower_len). */
+int64_t ncf_slab_stride(const ncf_layout *lay);
+
 /*
  * Fused forward + loss + backward for one global batch (replaces, per step,
  * NCF.forward models.py:97-118, BCEWithLogitsLoss train_neumf.py:113 and
@@ -85,7 +88,7 @@ int ncf_slab_rows(void);
  * drop_last=False); this rank takes rows [rank*ceil(gb/world), ...) of it.
  * grads: dense flat gradient buffer; embedding rows are scatter-added (f32
  * atomics), the tower/predict part is written per workgroup into
- * slab[ncf_slab_rows()][tower_len + 1] (reduce with ncf_reduce_slab).
+ * slab[ncf_slab_rows()][ncf_slab_stride()] (reduce with ncf_reduce_slab).
  * dz_mode NCF_DZ_DLOGIT: `labels` holds dL/dlogit per row instead.
  * logits_out (optional, may be NULL): per-row logits of this rank's rows.
  */
@@ -98,16 +101,18 @@ int ncf_train_step(const ncf_layout *lay, const float *params, float *grads,
 int ncf_forward(const ncf_layout *lay, const float *params, const int32_t *users,
                 const int32_t *items, int64_t n, float *logits, void *stream);
 
-/* grads[tower_begin + j] = sum_w slab[w][j] for j <= tower_len (loss slot included). */
-int ncf_reduce_slab(const ncf_layout *lay, const float *slab, float *grads, void *stream);
+/* grads[tower_begin + j] = sum_w slab[w][j] over a slab row (loss slot included), in a
+ * fixed order (bitwise reproducible).  If ctl != NULL, also advances ctl->batch and
+ * ctl->adam_t by one: the step's optimizer then runs as step t = ctl->adam_t. */
+int ncf_reduce_slab(const ncf_layout *lay, const float *slab, float *grads, ncf_step_ctl *ctl, void *stream);
 
 /*
  * Dense Adam over the active ranges of the flat buffers (torch.optim.Adam,
  * _single_tensor_adam arithmetic; train_neumf.py:90,115), grads zeroed after
  * use (optimizer.zero_grad, train_neumf.py:111).  ranges: host array of
- * 2*nranges int64 [begin, end) pairs.  t = ctl->adam_t + 1.  The last workgroup
- * advances ctl->batch and ctl->adam_t and, if loss_hist != NULL, stores
- * grads[loss_slot] into loss_hist[ctl->batch % hist_len].
+ * 2*nranges int64 [begin, end) pairs (16-byte aligned).  t = ctl->adam_t (already
+ * advanced by ncf_reduce_slab).  If loss_hist != NULL, one thread stores
+ * grads[loss_slot] into loss_hist[(ctl->batch - 1) % hist_len].
  */
 int ncf_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq,
                   const int64_t *ranges, int nranges, ncf_step_ctl *ctl, double lr,
@@ -132,6 +137,11 @@ int ncf_gather_epoch(const int32_t *users, const int32_t *items, const float *la
  */
 int ncf_hr_ndcg(const float *logits, const int32_t *items, int64_t n, int batch, int top_k,
                 int32_t *hr, float *ndcg, void *stream);
+
+/* Diagnostics only: ablation switches for the next ncf_train_step launches
+ * (1 = skip embedding scatter-add, 2 = skip weight-gradient MFMAs).  Results are
+ * wrong while any switch is set; 0 restores the production kernel. */
+int ncf_debug_set_diag(int flags);
 
 #ifdef __cplusplus
 }

@@ -46,7 +46,7 @@ class NcfLayout(ctypes.Structure):
 
 
 class NcfStepCtl(ctypes.Structure):
-    _fields_ = [("batch", c_i64), ("adam_t", c_i64), ("n_total", c_i64), ("done", c_i64)]
+    _fields_ = [("batch", c_i64), ("adam_t", c_i64), ("n_total", c_i64), ("reserved", c_i64)]
 
 
 _HIP_PROTOS = {
@@ -57,7 +57,9 @@ _HIP_PROTOS = {
     "ncf_train_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
     "ncf_forward": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
-    "ncf_reduce_slab": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp]),
+    "ncf_reduce_slab": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp]),
+    "ncf_slab_stride": (c_i64, [ctypes.POINTER(NcfLayout)]),
+    "ncf_debug_set_diag": (ctypes.c_int, [ctypes.c_int]),
     "ncf_adam_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.c_int, c_vp,
                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                      c_i64, c_vp, c_i64, c_vp]),

@@ -57,7 +57,13 @@ struct TrainArgs {
     float* slab;
     float* logits_out;
     int64_t fwd_n;  // FWD_ONLY: number of rows
+    int diag;       // DIAG_* ablation switches (0 in production)
 };
+
+// Ablation switches for performance diagnosis (ncf_debug_set_diag); results are
+// wrong when any is set.
+constexpr int DIAG_NO_ATOMICS = 1;  // skip the embedding scatter-add
+constexpr int DIAG_NO_WGRAD = 2;    // skip the weight-gradient MFMAs
 
 struct KernelEntry {
     int mode, F, L;

@@ -11,21 +11,41 @@ static inline int64_t rup64(int64_t x) { return (x + 63) / 64 * 64; }
 
 // ---------------------------------------------------------------------------
 // Slab reduction: grads[tb + j] = sum_w slab[w][j], fixed order (bitwise
-// reproducible).  Block = 256 threads = 64 columns x 4 row-quarters.
+// reproducible).  Block = 256 threads = 16 float4 columns x 16 row groups, each
+// thread 16 independent 16-byte loads; the 16 row-group partials are combined
+// in LDS in a fixed order.  Thread 0 of block 0 also advances the step control
+// block (batch, adam_t): the fused step before it has read `batch`, the
+// optimizer after it reads the advanced `adam_t` (kernel boundaries order it).
 __global__ __launch_bounds__(256) void reduce_slab_kernel(const float* __restrict__ slab, float* __restrict__ out,
-                                                          int lo, int len, int rows) {
-    __shared__ float part[4][64];
-    const int jj = threadIdx.x & 63, q = threadIdx.x >> 6;
-    const int j = lo + blockIdx.x * 64 + jj;
-    const int per = rows / 4;
-    float s = 0.f;
-    if (j < len) {
-        const float* p = slab + (int64_t)(q * per) * len + j;
-        for (int r = 0; r < per; ++r) s += p[(int64_t)r * len];
+                                                          int lo, int stride, int rows, ncf_step_ctl* ctl) {
+    __shared__ f4 part[16][16];
+    const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
+    const int j = lo + (blockIdx.x * 16 + c4) * 4;
+    f4 s = f4{0.f, 0.f, 0.f, 0.f};
+    if (j < stride) {
+        const float* p = slab + (int64_t)rg * stride + j;
+        const int per = rows / 16;
+#pragma unroll 16
+        for (int r = 0; r < per; ++r) {
+            const f4 v = *reinterpret_cast<const f4*>(p + (int64_t)r * 16 * stride);
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
     }
-    part[q][jj] = s;
+    part[rg][c4] = s;
     __syncthreads();
-    if (q == 0 && j < len) out[j] = ((part[0][jj] + part[1][jj]) + part[2][jj]) + part[3][jj];
+    if (rg == 0 && j < stride) {
+        f4 t = part[0][c4];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) {
+            const f4 v = part[q][c4];
+            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+        }
+        *reinterpret_cast<f4*>(out + j) = t;
+    }
+    if (ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+        ctl->batch = ctl->batch + 1;
+        ctl->adam_t = ctl->adam_t + 1;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -45,30 +65,21 @@ __device__ __forceinline__ int64_t range_locate(const Ranges& R, int64_t q, int*
     return R.begin[k] + (q - R.prefix[k]) * 4;
 }
 
-__device__ void step_epilogue(ncf_step_ctl* ctl, float* grads, int64_t loss_slot, float* loss_hist,
-                              int64_t hist_len) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        const unsigned long long prev = atomicAdd(reinterpret_cast<unsigned long long*>(&ctl->done), 1ull);
-        if (prev == (unsigned long long)(gridDim.x - 1)) {
-            __threadfence();
-            const int64_t b = ctl->batch;
-            if (loss_hist != nullptr && loss_slot >= 0 && hist_len > 0) loss_hist[b % hist_len] = grads[loss_slot];
-            ctl->batch = b + 1;
-            ctl->adam_t = ctl->adam_t + 1;
-            ctl->done = 0;
-            __threadfence();
-        }
+// Loss bookkeeping of the step: done by one thread, no cross-block protocol.
+__device__ __forceinline__ void record_loss(const ncf_step_ctl* ctl, const float* grads, int64_t loss_slot,
+                                            float* loss_hist, int64_t hist_len) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && loss_hist != nullptr && loss_slot >= 0 && hist_len > 0) {
+        const int64_t b = ctl->batch - 1;  // ncf_reduce_slab advanced it
+        loss_hist[((b % hist_len) + hist_len) % hist_len] = grads[loss_slot];
     }
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
-                                                   float* __restrict__ v, Ranges R, ncf_step_ctl* ctl, double lr,
+                                                   float* __restrict__ v, Ranges R, const ncf_step_ctl* ctl, double lr,
                                                    double beta1, double beta2, float eps, int64_t loss_slot,
                                                    float* loss_hist, int64_t hist_len) {
 #pragma clang fp contract(off)
-    const double t = (double)(ctl->adam_t + 1);
+    const double t = (double)ctl->adam_t;  // advanced by ncf_reduce_slab
     const double bc1 = 1.0 - pow(beta1, t);
     const double bc2 = 1.0 - pow(beta2, t);
     const float neg_step = (float)(-(lr / bc1));
@@ -101,11 +112,11 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
         *reinterpret_cast<f4*>(p + i) = pp;
         *reinterpret_cast<f4*>(g + i) = f4{0.f, 0.f, 0.f, 0.f};
     }
-    step_epilogue(ctl, g, loss_slot, loss_hist, hist_len);
+    record_loss(ctl, g, loss_slot, loss_hist, hist_len);
 }
 
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* __restrict__ g, Ranges R,
-                                                  ncf_step_ctl* ctl, float lr, int64_t loss_slot, float* loss_hist,
+                                                  const ncf_step_ctl* ctl, float lr, int64_t loss_slot, float* loss_hist,
                                                   int64_t hist_len) {
 #pragma clang fp contract(off)
     const int64_t total = R.prefix[R.n];
@@ -122,7 +133,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* 
         *reinterpret_cast<f4*>(p + i) = pp;
         *reinterpret_cast<f4*>(g + i) = f4{0.f, 0.f, 0.f, 0.f};
     }
-    step_epilogue(ctl, g, loss_slot, loss_hist, hist_len);
+    record_loss(ctl, g, loss_slot, loss_hist, hist_len);
 }
 
 // ---------------------------------------------------------------------------
@@ -213,6 +224,8 @@ static Ranges make_ranges(const int64_t* ranges, int nranges, int* err) {
     return R;
 }
 
+static int g_diag = 0;
+
 static int launch_status() { return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH; }
 
 // hipFuncSetAttribute once per (kernel, size): nothing but launches happen on
@@ -238,6 +251,11 @@ using namespace ncf;
 extern "C" {
 
 int ncf_abi_version(void) { return NCF_ABI_VERSION; }
+
+int ncf_debug_set_diag(int flags) {
+    g_diag = flags;
+    return NCF_OK;
+}
 
 int ncf_slab_rows(void) { return SLAB_ROWS; }
 
@@ -303,6 +321,7 @@ int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, con
     a.world = world;
     a.rank = rank;
     a.dz_mode = dz_mode;
+    a.diag = g_diag;
     a.slab = slab;
     a.logits_out = logits_out;
     void* args[] = {&a};
@@ -338,13 +357,15 @@ int ncf_forward(const ncf_layout* lay, const float* params, const int32_t* users
     return launch_status();
 }
 
-int ncf_reduce_slab(const ncf_layout* lay, const float* slab, float* grads, void* stream) {
+int64_t ncf_slab_stride(const ncf_layout* lay) { return lay ? lay->tower_len + 64 : -1; }
+
+int ncf_reduce_slab(const ncf_layout* lay, const float* slab, float* grads, ncf_step_ctl* ctl, void* stream) {
     if (!lay || !slab || !grads) return NCF_E_ARG;
-    const int len = (int)lay->tower_len + 1;
+    const int stride = (int)ncf_slab_stride(lay);
     const int lo = lay->model_type == NCF_MODEL_GMF ? (int)(lay->wp - lay->tower_begin) : 0;
-    const int blocks = (len - lo + 63) / 64;
+    const int blocks = (stride - lo + 63) / 64;
     hipLaunchKernelGGL(reduce_slab_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab,
-                       grads + lay->tower_begin, lo, len, SLAB_ROWS);
+                       grads + lay->tower_begin, lo, stride, SLAB_ROWS, ctl);
     return launch_status();
 }
 

@@ -265,7 +265,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                     const int q = wr + j * RPI + gq0;
                     const float dzq = sdz[q];
                     dWpG += dzq * (ugv[j] * igv[j]);
-                    if (su[q] >= 0) {
+                    if (su[q] >= 0 && !(a.diag & DIAG_NO_ATOMICS)) {
                         const float dgm = dzq * wpf;
                         atomicAdd(a.grads + lay.ug + (int64_t)su[q] * F + gf, dgm * igv[j]);
                         atomicAdd(a.grads + lay.ig + (int64_t)si[q] * F + gf, dgm * ugv[j]);
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
                     for (int jl = 0; jl < tpw; ++jl) {
                         const int j = w * tpw + jl;
-                        if (j < T) {
+                        if (j < T && !(a.diag & DIAG_NO_WGRAD)) {
                             const int mt = j % S_::MT(k);
                             const int nt = j / S_::MT(k);
                             if constexpr (k == 0) {
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                             const int q = wr + 4 * g + r;
                             const int uu = su[q];
                             const int iq = si[q];
-                            if (uu >= 0) {
+                            if (uu >= 0 && !(a.diag & DIAG_NO_ATOMICS)) {
 #pragma unroll
                                 for (int nt = 0; nt < S_::KT(0); ++nt) {
                                     const int fj = 16 * nt + c;
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         // ---- this workgroup's tower/predict partial: assemble in LDS, store once
         const int64_t tb = lay.tower_begin;
         const int lo = S_::MLP ? 0 : (int)(lay.wp - tb);
-        const int len = (int)lay.tower_len + 1;
+        const int len = (int)lay.tower_len + 64;  // slab stride (ncf_slab_stride); loss at tower_len
         float* img = sstage;
         const int l = l0, c = c0, g = g0, gf = l0 % F;
         __syncthreads();
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         if constexpr (S_::GMF) atomicAdd(img + (lay.wp - tb) + gf, dWpG);
         if (g == 0) {
             atomicAdd(img + (lay.bp - tb), dbpAcc);
-            atomicAdd(img + (len - 1), lossAcc / gb_f);
+            atomicAdd(img + lay.tower_len, lossAcc / gb_f);
         }
         __syncthreads();
         float* out = a.slab + (int64_t)blockIdx.x * len;

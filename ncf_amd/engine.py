@@ -108,7 +108,7 @@ class TrainEngine:
                                    self.items.data_ptr(), self.labels.data_ptr(), self.ctl.data_ptr(),
                                    self.batch_size, self.world_size, self.rank, L.DZ_BCE,
                                    self.slab.data_ptr(), None, st), "ncf_train_step")
-        L.check(lib.ncf_reduce_slab(lay, self.slab.data_ptr(), self.grads.data_ptr(), st), "ncf_reduce_slab")
+        L.check(lib.ncf_reduce_slab(lay, self.slab.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(), st), "ncf_reduce_slab")
         if self.world_size > 1:
             import torch.distributed as dist
             dist.all_reduce(self.grads, group=self.group)
@@ -142,7 +142,7 @@ class TrainEngine:
                                        self.batch_size, self.world_size, self.rank, L.DZ_BCE,
                                        self.slab.data_ptr(), None, sp), "ncf_train_step")
             e[1].record(st)
-            L.check(lib.ncf_reduce_slab(lay, self.slab.data_ptr(), self.grads.data_ptr(), sp), "ncf_reduce_slab")
+            L.check(lib.ncf_reduce_slab(lay, self.slab.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(), sp), "ncf_reduce_slab")
             e[2].record(st)
             if self.world_size > 1:
                 import torch.distributed as dist

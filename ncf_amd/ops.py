@@ -90,12 +90,13 @@ def fused_backward(flat, lay, users_i32, items_i32, dlogit, gflat, slab, ctl):
     L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), users_i32.data_ptr(),
                                    items_i32.data_ptr(), dlogit.data_ptr(), ctl.data_ptr(), int(n), 1, 0,
                                    L.DZ_DLOGIT, slab.data_ptr(), None, st), "ncf_train_step")
-    L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), st),
+    L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st),
             "ncf_reduce_slab")
 
 
 def new_slab(lay, dev):
-    return torch.empty((L.hip().ncf_slab_rows(), int(lay.tower_len) + 1), dtype=torch.float32, device=dev)
+    stride = int(L.hip().ncf_slab_stride(L.ctypes.byref(lay)))
+    return torch.empty((L.hip().ncf_slab_rows(), stride), dtype=torch.float32, device=dev)
 
 
 def new_ctl(n_total, dev, batch=0, adam_t=0):

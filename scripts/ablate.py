@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Ablation of the fused step kernel (diagnosis only): time ncf_train_step with
+HIP events under the DIAG switches, interleaved rounds in one process.
+Prints one JSON line with median ms per variant and per rows-per-launch."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import bench
+    import ncf_amd._lib as L
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    res = {}
+    for rows in (65536, 16384):
+        eng, model, ds, _ = bench.setup_engine(cfg, 1, 0, dev, None, rows)
+        eng.run(3, use_graph=False)
+        torch.cuda.synchronize()
+        variants = {"full": 0, "no_atomics": 1, "no_wgrad": 2, "no_atomics_no_wgrad": 3}
+        times = {k: [] for k in variants}
+        for _ in range(5):
+            for name, d in variants.items():
+                L.hip().ncf_debug_set_diag(d)
+                kt = eng.time_kernels(10)
+                times[name].append(kt["ncf_train_step"])
+        L.hip().ncf_debug_set_diag(0)
+        res[str(rows)] = {k: float(np.median(v)) for k, v in times.items()}
+        res[str(rows) + "_other"] = eng.time_kernels(10)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -28,8 +28,11 @@ rocm-smi --showproductname > gpurun_out/rocm_smi.log 2>&1 || true
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider
 run bench 600 python bench.py --steps "$STEPS" --warmup "$WARMUP"
+if [ "${ABLATE:-0}" = "1" ]; then
+    run ablate 600 python scripts/ablate.py
+fi
 if [ "${PROFILE:-1}" = "1" ]; then
-    run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- \
+    run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
         python3 bench.py --steps 100 --warmup 10 --skip-cpu-baseline --skip-eval
 fi
 echo ALL-DONE

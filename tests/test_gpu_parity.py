@@ -129,7 +129,7 @@ def test_one_step_grads_vs_oracle(cfg):
     L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), u.data_ptr(),
                                    it.data_ptr(), y.data_ptr(), ctl.data_ptr(), B, 1, 0, L.DZ_BCE,
                                    slab.data_ptr(), logits.data_ptr(), st), "train")
-    L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), st), "reduce")
+    L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st), "reduce")
     torch.cuda.synchronize()
     np.testing.assert_allclose(logits.cpu().numpy(), logits_ref.numpy(), rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(gflat[lay.loss_slot].item(), loss_ref, rtol=1e-5)
@@ -159,7 +159,7 @@ def test_rank_shards_sum_to_full_batch(world):
         L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), u.data_ptr(),
                                        it.data_ptr(), y.data_ptr(), ctl.data_ptr(), B, world, rank, L.DZ_BCE,
                                        slab.data_ptr(), None, st), "train")
-        L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), st), "reduce")
+        L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st), "reduce")
         return gflat
     full = run(1, 0)
     parts = sum(run(world, r) for r in range(world))
