@@ -110,11 +110,32 @@ def setup_engine(config, world, rank, dev, group, global_batch, seed=0):
     u_d, i_d, y_d = (torch.from_numpy(users).to(dev), torch.from_numpy(items).to(dev),
                      torch.from_numpy(labels).to(dev))
     us, its, ys = torch.empty_like(u_d), torch.empty_like(i_d), torch.empty_like(y_d)
-    L.check(L.hip().ncf_gather_epoch(u_d.data_ptr(), i_d.data_ptr(), y_d.data_ptr(), perm.data_ptr(), len(users),
-                                     us.data_ptr(), its.data_ptr(), ys.data_ptr(), L.stream_ptr(dev)), "gather")
+    L.check(L.hip().ncf_prepare_epoch(u_d.data_ptr(), i_d.data_ptr(), y_d.data_ptr(), perm.data_ptr(), len(users),
+                                      global_batch, I, us.data_ptr(), its.data_ptr(), ys.data_ptr(),
+                                      L.stream_ptr(dev)), "prepare_epoch")
     eng = TrainEngine(model, lr=1e-3, world_size=world, rank=rank, process_group=group)
     eng.set_epoch_stream(us, its, ys, global_batch)
+
+    def prepare():  # per-epoch device work: shuffle + group each batch by item
+        L.check(L.hip().ncf_prepare_epoch(u_d.data_ptr(), i_d.data_ptr(), y_d.data_ptr(), perm.data_ptr(),
+                                          len(users), global_batch, I, us.data_ptr(), its.data_ptr(),
+                                          ys.data_ptr(), L.stream_ptr(dev)), "prepare_epoch")
+    eng.prepare_epoch = prepare
     return eng, model, ds, t_sample
+
+
+def run_steps(eng, n_steps, use_graph):
+    """n_steps optimizer steps; the per-epoch device preparation (ncf_prepare_epoch)
+    runs at every epoch boundary inside the timed region."""
+    done = 0
+    while done < n_steps:
+        pos = eng.batches_done % eng.num_batches
+        if pos == 0 and eng.batches_done > 0:
+            eng.prepare_epoch()
+        k = min(n_steps - done, eng.num_batches - pos)
+        eng.run(k, use_graph=use_graph)
+        eng.batches_done += k
+        done += k
 
 
 def main():
@@ -155,7 +176,8 @@ def main():
 
     # ---- warmup (first step eager, then capture) -----------------------------
     use_graph = not args.no_graph
-    eng.run(max(1, args.warmup), use_graph=use_graph)
+    eng.batches_done = 0
+    run_steps(eng, max(1, args.warmup), use_graph)
     torch.cuda.synchronize(dev)
 
     # ---- timed region ----------------------------------------------------------
@@ -163,7 +185,7 @@ def main():
         torch.distributed.barrier(group=group, device_ids=[local])
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    eng.run(args.steps, use_graph=use_graph)
+    run_steps(eng, args.steps, use_graph)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     if world > 1:
@@ -178,6 +200,13 @@ def main():
 
     # ---- per-kernel live timing (HIP events on the launch stream) -------------
     kt = eng.time_kernels(args.kernel_steps)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        eng.prepare_epoch()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    kt["prepare_epoch_per_epoch"] = e0.elapsed_time(e1) / 5
     rows_per_launch = per_gpu
     flops = tower_flops_per_row(f, nl) * rows_per_launch
     ms = kt["ncf_train_step"]

@@ -130,6 +130,18 @@ int ncf_gather_epoch(const int32_t *users, const int32_t *items, const float *la
                      float *labels_out, void *stream);
 
 /*
+ * Epoch stream for the fused step: global batch b holds rows perm[b*B .. b*B+cnt)
+ * of the unshuffled stream (the DataLoader(shuffle=True) batch membership,
+ * train_neumf.py:55,106), written back grouped by item id (counting sort per batch).
+ * Order inside a batch does not change the batch gradient; grouping lets the fused
+ * step reduce item-side gradients per item before its atomics.  item_num <= ~40k
+ * (LDS histogram), else NCF_E_UNSUPPORTED.
+ */
+int ncf_prepare_epoch(const int32_t *users, const int32_t *items, const float *labels,
+                      const int64_t *perm, int64_t n, int64_t batch_global, int item_num,
+                      int32_t *users_out, int32_t *items_out, float *labels_out, void *stream);
+
+/*
  * HR@K / NDCG@K per DataLoader batch (metrics.py:4-25): batches of `batch`
  * consecutive rows (last one partial), ground truth = the batch's first item,
  * recommends = items of the top_k logits.  hr[b] in {0,1}; ndcg[b] = 1/log2(pos+2).
@@ -142,6 +154,11 @@ int ncf_hr_ndcg(const float *logits, const int32_t *items, int64_t n, int batch,
  * (1 = skip embedding scatter-add, 2 = skip weight-gradient MFMAs).  Results are
  * wrong while any switch is set; 0 restores the production kernel. */
 int ncf_debug_set_diag(int flags);
+
+/* Diagnostics only: device buffer of ncf_slab_rows() x 64 uint64 that the next
+ * ncf_train_step launches fill with per-workgroup s_memtime phase stamps
+ * (NULL = off, the production setting). */
+int ncf_debug_set_stamps(unsigned long long *dev_buf);
 
 #ifdef __cplusplus
 }

@@ -17,7 +17,9 @@ import threading
 import torch  # noqa: F401  (must precede loading libncf_hip.so)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-HIP_LIB_PATH = os.path.join(_HERE, "libncf_hip.so")
+# NCF_HIP_LIB=diag selects the diagnostics build (phase stamps compiled in)
+HIP_LIB_PATH = os.path.join(_HERE, "libncf_hip_diag.so" if os.environ.get("NCF_HIP_LIB") == "diag"
+                            else "libncf_hip.so")
 SAMPLER_LIB_PATH = os.path.join(_HERE, "libncf_sampler.so")
 
 NCF_OK = 0
@@ -60,12 +62,15 @@ _HIP_PROTOS = {
     "ncf_reduce_slab": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp]),
     "ncf_slab_stride": (c_i64, [ctypes.POINTER(NcfLayout)]),
     "ncf_debug_set_diag": (ctypes.c_int, [ctypes.c_int]),
+    "ncf_debug_set_stamps": (ctypes.c_int, [c_vp]),
     "ncf_adam_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.c_int, c_vp,
                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                      c_i64, c_vp, c_i64, c_vp]),
     "ncf_sgd_step": (ctypes.c_int, [c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.c_int, c_vp, ctypes.c_double,
                                     c_i64, c_vp, c_i64, c_vp]),
     "ncf_gather_epoch": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "ncf_prepare_epoch": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, ctypes.c_int, c_vp, c_vp, c_vp,
+                                         c_vp]),
     "ncf_hr_ndcg": (ctypes.c_int, [c_vp, c_vp, c_i64, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
 }
 

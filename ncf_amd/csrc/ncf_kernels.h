@@ -36,8 +36,19 @@ struct Shape {
                                         : rmax(par, k + 1));
     }
     static constexpr int R0 = rmax(0, 0), R1 = rmax(1, 0);
-    static constexpr int WAVE_STAGE = R0 + R1;
-    static constexpr int MISC = 5 * TILE_ROWS;  // su, si, labels, zgmf, dz
+    // Per-wave scratch of the layer-0 phase (item-side gradient rows before the
+    // per-item segment reduction): [16][DM + 4] MLP part, [16][F + 4] GMF part.
+    // It lives in the R1 staging region, free once every wave is past layer 1.
+    static constexpr int SCM = MLP ? DM + 4 : 0;
+    static constexpr int SCG = GMF ? F + 4 : 0;
+    static constexpr int SCR = 16 * (SCM + SCG);
+    static constexpr int WAVE_STAGE = R0 + (R1 > SCR ? R1 : SCR);
+    // su[2], si[2], labels[2] (double-buffered tile indices), zgmf, dz, then
+    // 128 floats of biases (each layer's padded to 16*MT) and 128 of predict weights
+    static constexpr int MISC = 10 * TILE_ROWS;
+    __host__ __device__ static constexpr int boff(int k) { return k == 0 ? 0 : boff(k - 1) + 16 * MT(k - 1); }
+    static_assert(!MLP || boff(L) <= 128, "bias LDS region");
+    static_assert(P <= 128, "predict LDS region");
     __host__ __device__ static constexpr int TPW(int k) { return (MT(k) * KT(k) + NWAVES - 1) / NWAVES; }
     static constexpr int KT0 = MLP ? KT(0) : 1;
     static_assert(F >= 8 && F <= 64 && (F & (F - 1)) == 0, "factor_num must be 8..64, a power of 2");
@@ -58,12 +69,14 @@ struct TrainArgs {
     float* logits_out;
     int64_t fwd_n;  // FWD_ONLY: number of rows
     int diag;       // DIAG_* ablation switches (0 in production)
+    unsigned long long* stamps;  // diagnostics: per-workgroup s_memtime stamps (nullptr in production)
 };
+
+constexpr int NSTAMP = 64;  // stamps per workgroup
 
 // Ablation switches for performance diagnosis (ncf_debug_set_diag); results are
 // wrong when any is set.
-constexpr int DIAG_NO_ATOMICS = 1;  // skip the embedding scatter-add
-constexpr int DIAG_NO_WGRAD = 2;    // skip the weight-gradient MFMAs
+constexpr int DIAG_NO_WGRAD = 2;  // skip the weight-gradient MFMAs
 
 struct KernelEntry {
     int mode, F, L;

@@ -74,43 +74,66 @@ __device__ __forceinline__ void record_loss(const ncf_step_ctl* ctl, const float
     }
 }
 
+__device__ __forceinline__ void adam_f4(f4& p, f4& m, f4& v, const f4& g, float w1, float b2, float omb2,
+                                        float bc2s, float eps, float neg_step) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float gr = lane_get(g, r);
+        float mr = lane_get(m, r), vr = lane_get(v, r), pr = lane_get(p, r);
+        mr = fmaf(w1, gr - mr, mr);          // exp_avg.lerp_(grad, 1 - beta1)   (fmadd form)
+        vr = vr * b2 + omb2 * gr * gr;       // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+        const float den = sqrtf(vr) / bc2s + eps;  // (exp_avg_sq.sqrt() / bias_correction2_sqrt).add_(eps)
+        pr = pr + neg_step * mr / den;       // param.addcdiv_(exp_avg, denom, value=-step_size)
+        if (r == 0) { m.x = mr; v.x = vr; p.x = pr; }
+        else if (r == 1) { m.y = mr; v.y = vr; p.y = pr; }
+        else if (r == 2) { m.z = mr; v.z = vr; p.z = pr; }
+        else { m.w = mr; v.w = vr; p.w = pr; }
+    }
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                    float* __restrict__ v, Ranges R, const ncf_step_ctl* ctl, double lr,
                                                    double beta1, double beta2, float eps, int64_t loss_slot,
                                                    float* loss_hist, int64_t hist_len) {
 #pragma clang fp contract(off)
-    const double t = (double)ctl->adam_t;  // advanced by ncf_reduce_slab
-    const double bc1 = 1.0 - pow(beta1, t);
-    const double bc2 = 1.0 - pow(beta2, t);
-    const float neg_step = (float)(-(lr / bc1));
-    const float bc2s = (float)sqrt(bc2);
+    __shared__ float sc[2];
+    if (threadIdx.x == 0) {  // bias corrections once per block, in double like torch's Python scalars
+        const double t = (double)ctl->adam_t;  // advanced by ncf_reduce_slab
+        const double bc1 = 1.0 - pow(beta1, t);
+        const double bc2 = 1.0 - pow(beta2, t);
+        sc[0] = (float)(-(lr / bc1));
+        sc[1] = (float)sqrt(bc2);
+    }
+    __syncthreads();
+    const float neg_step = sc[0], bc2s = sc[1];
     const float w1 = (float)(1.0 - beta1);
     const float b2 = (float)beta2;
     const float omb2 = (float)(1.0 - beta2);
     const int64_t total = R.prefix[R.n];
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q0 < total; q0 += 2 * stride) {
+        const int64_t q1 = q0 + stride;
+        const bool has1 = q1 < total;
         int which;
-        const int64_t i = range_locate(R, q, &which);
-        f4 gg = *reinterpret_cast<const f4*>(g + i);
-        f4 mm = *reinterpret_cast<const f4*>(m + i);
-        f4 vv = *reinterpret_cast<const f4*>(v + i);
-        f4 pp = *reinterpret_cast<const f4*>(p + i);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float gr = lane_get(gg, r);
-            const float mr = fmaf(w1, gr - lane_get(mm, r), lane_get(mm, r));  // lerp_(g, 1-b1): fmadd form
-            const float vr = lane_get(vv, r) * b2 + omb2 * gr * gr;            // mul_(b2).addcmul_(g, g, 1-b2)
-            const float den = sqrtf(vr) / bc2s + eps;                           // (sqrt(v) / bc2_sqrt).add_(eps)
-            const float pr = lane_get(pp, r) + neg_step * mr / den;             // addcdiv_(m, den, -step_size)
-            if (r == 0) { mm.x = mr; vv.x = vr; pp.x = pr; }
-            else if (r == 1) { mm.y = mr; vv.y = vr; pp.y = pr; }
-            else if (r == 2) { mm.z = mr; vv.z = vr; pp.z = pr; }
-            else { mm.w = mr; vv.w = vr; pp.w = pr; }
+        const int64_t i0 = range_locate(R, q0, &which);
+        const int64_t i1 = has1 ? range_locate(R, q1, &which) : i0;
+        f4 g0 = *reinterpret_cast<const f4*>(g + i0), g1 = *reinterpret_cast<const f4*>(g + i1);
+        f4 m0 = *reinterpret_cast<const f4*>(m + i0), m1 = *reinterpret_cast<const f4*>(m + i1);
+        f4 v0 = *reinterpret_cast<const f4*>(v + i0), v1 = *reinterpret_cast<const f4*>(v + i1);
+        f4 p0 = *reinterpret_cast<const f4*>(p + i0), p1 = *reinterpret_cast<const f4*>(p + i1);
+        adam_f4(p0, m0, v0, g0, w1, b2, omb2, bc2s, eps, neg_step);
+        *reinterpret_cast<f4*>(m + i0) = m0;
+        *reinterpret_cast<f4*>(v + i0) = v0;
+        *reinterpret_cast<f4*>(p + i0) = p0;
+        *reinterpret_cast<f4*>(g + i0) = f4{0.f, 0.f, 0.f, 0.f};
+        if (has1) {
+            adam_f4(p1, m1, v1, g1, w1, b2, omb2, bc2s, eps, neg_step);
+            *reinterpret_cast<f4*>(m + i1) = m1;
+            *reinterpret_cast<f4*>(v + i1) = v1;
+            *reinterpret_cast<f4*>(p + i1) = p1;
+            *reinterpret_cast<f4*>(g + i1) = f4{0.f, 0.f, 0.f, 0.f};
         }
-        *reinterpret_cast<f4*>(m + i) = mm;
-        *reinterpret_cast<f4*>(v + i) = vv;
-        *reinterpret_cast<f4*>(p + i) = pp;
-        *reinterpret_cast<f4*>(g + i) = f4{0.f, 0.f, 0.f, 0.f};
     }
     record_loss(ctl, g, loss_slot, loss_hist, hist_len);
 }
@@ -145,6 +168,98 @@ __global__ __launch_bounds__(256) void gather_epoch_kernel(const int32_t* __rest
         uo[k] = u[s];
         io[k] = it[s];
         yo[k] = y[s];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Epoch preparation: one workgroup per global batch.  Rows perm[b*B .. b*B+cnt)
+// of the unshuffled stream are the batch (DataLoader shuffle=True membership);
+// they are written back grouped by item (counting sort in LDS).  Row order
+// inside a batch does not change the batch's gradient, it only lets the fused
+// step reduce item-side gradients per item segment before its atomics.
+constexpr int PREP_THREADS = 1024;
+__global__ __launch_bounds__(PREP_THREADS) void prepare_epoch_kernel(
+    const int32_t* __restrict__ users, const int32_t* __restrict__ items, const float* __restrict__ labels,
+    const int64_t* __restrict__ perm, int64_t n, int64_t B, int item_num, int32_t* __restrict__ uo,
+    int32_t* __restrict__ io, float* __restrict__ yo) {
+    extern __shared__ int hist[];  // [item_num] counts -> offsets, then [32] wave partials
+    int* part = hist + ((item_num + 3) & ~3);
+    const int tid = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * B;
+    const int cnt = (int)((n - b0) < B ? (n - b0) : B);
+    for (int i = tid; i < item_num; i += PREP_THREADS) hist[i] = 0;
+    __syncthreads();
+    constexpr int U16 = 16;
+    for (int j0 = 0; j0 < cnt; j0 += U16 * PREP_THREADS) {
+        int64_t src[U16];
+        int it[U16];
+#pragma unroll
+        for (int k = 0; k < U16; ++k) {
+            const int j = j0 + k * PREP_THREADS + tid;
+            src[k] = j < cnt ? perm[b0 + j] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < U16; ++k) it[k] = items[src[k] < 0 ? 0 : src[k]];
+#pragma unroll
+        for (int k = 0; k < U16; ++k)
+            if (src[k] >= 0) atomicAdd(&hist[min(max(it[k], 0), item_num - 1)], 1);
+    }
+    __syncthreads();
+    // exclusive scan: contiguous chunk per thread, wave scan, then across waves
+    const int per = (item_num + PREP_THREADS - 1) / PREP_THREADS;
+    const int i0 = tid * per, i1 = min(item_num, i0 + per);
+    int tot = 0;
+    for (int i = i0; i < i1; ++i) tot += hist[i];
+    const int lane = tid & 63, wv = tid >> 6;
+    int incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) part[wv] = incl;
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int q = 0; q < PREP_THREADS / 64; ++q) {
+            const int v = part[q];
+            part[q] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    int run = part[wv] + incl - tot;
+    for (int i = i0; i < i1; ++i) {
+        const int v = hist[i];
+        hist[i] = run;
+        run += v;
+    }
+    __syncthreads();
+    for (int j0 = 0; j0 < cnt; j0 += U16 * PREP_THREADS) {
+        int64_t src[U16];
+        int it[U16], us[U16];
+        float ys[U16];
+#pragma unroll
+        for (int k = 0; k < U16; ++k) {
+            const int j = j0 + k * PREP_THREADS + tid;
+            src[k] = j < cnt ? perm[b0 + j] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < U16; ++k) {
+            const int64_t sk = src[k] < 0 ? 0 : src[k];
+            it[k] = items[sk];
+            us[k] = users[sk];
+            ys[k] = labels[sk];
+        }
+#pragma unroll
+        for (int k = 0; k < U16; ++k) {
+            if (src[k] >= 0) {
+                const int pos = atomicAdd(&hist[min(max(it[k], 0), item_num - 1)], 1);
+                uo[b0 + pos] = us[k];
+                io[b0 + pos] = it[k];
+                yo[b0 + pos] = ys[k];
+            }
+        }
     }
 }
 
@@ -225,6 +340,7 @@ static Ranges make_ranges(const int64_t* ranges, int nranges, int* err) {
 }
 
 static int g_diag = 0;
+static unsigned long long* g_stamps = nullptr;
 
 static int launch_status() { return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH; }
 
@@ -254,6 +370,11 @@ int ncf_abi_version(void) { return NCF_ABI_VERSION; }
 
 int ncf_debug_set_diag(int flags) {
     g_diag = flags;
+    return NCF_OK;
+}
+
+int ncf_debug_set_stamps(unsigned long long* dev_buf) {
+    g_stamps = dev_buf;
     return NCF_OK;
 }
 
@@ -322,6 +443,7 @@ int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, con
     a.rank = rank;
     a.dz_mode = dz_mode;
     a.diag = g_diag;
+    a.stamps = g_stamps;
     a.slab = slab;
     a.logits_out = logits_out;
     void* args[] = {&a};
@@ -377,8 +499,8 @@ int ncf_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
     Ranges R = make_ranges(ranges, nranges, &err);
     if (err) return NCF_E_ARG;
     const int64_t total = R.prefix[R.n];
-    int64_t grid = (total + 255) / 256;
-    if (grid > 2048) grid = 2048;
+    int64_t grid = (total + 511) / 512;  // two float4 per thread
+    if (grid > 4096) grid = 4096;
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(adam_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
                        exp_avg_sq, R, ctl, lr, beta1, beta2, (float)eps, loss_slot, loss_hist, hist_len);
@@ -408,6 +530,23 @@ int ncf_gather_epoch(const int32_t* users, const int32_t* items, const float* la
     if (grid > 4096) grid = 4096;
     hipLaunchKernelGGL(gather_epoch_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, users, items, labels,
                        perm, n, users_out, items_out, labels_out);
+    return launch_status();
+}
+
+int ncf_prepare_epoch(const int32_t* users, const int32_t* items, const float* labels, const int64_t* perm,
+                      int64_t n, int64_t batch_global, int item_num, int32_t* users_out, int32_t* items_out,
+                      float* labels_out, void* stream) {
+    if (!users || !items || !labels || !perm || !users_out || !items_out || !labels_out || n < 0 ||
+        batch_global <= 0 || item_num <= 0)
+        return NCF_E_ARG;
+    if (n == 0) return NCF_OK;
+    const int64_t lds = (int64_t)(((item_num + 3) & ~3) + 32) * 4;
+    if (lds > LDS_LIMIT_BYTES) return NCF_E_UNSUPPORTED;
+    if (ensure_lds(reinterpret_cast<const void*>(&prepare_epoch_kernel), lds) != NCF_OK) return NCF_E_LAUNCH;
+    const int64_t nb = (n + batch_global - 1) / batch_global;
+    hipLaunchKernelGGL(prepare_epoch_kernel, dim3((unsigned)nb), dim3(PREP_THREADS), (size_t)lds,
+                       (hipStream_t)stream, users, items, labels, perm, n, batch_global, item_num, users_out,
+                       items_out, labels_out);
     return launch_status();
 }
 

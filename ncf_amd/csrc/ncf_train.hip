@@ -41,6 +41,31 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
     sf_impl(fn, std::make_integer_sequence<int, N>{});
 }
 
+// Diagnostics: wave 0 / lane 0 of each workgroup records the shader clock at
+// phase boundaries (one asm statement incl. its lgkmcnt wait, fenced by
+// sched_barriers).  Never on in production (a.stamps == nullptr).
+__device__ __forceinline__ void stamp(const TrainArgs& a, int idx) {
+#ifndef NCF_STAMPS
+    (void)a;
+    (void)idx;
+#else
+    if (a.stamps != nullptr && threadIdx.x == 0 && idx < NSTAMP) {
+        __builtin_amdgcn_sched_barrier(0);
+        unsigned long long t;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        a.stamps[(size_t)blockIdx.x * NSTAMP + idx] = t;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#endif
+}
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for
+// every outstanding global op of the wave (vmcnt(0)) -- i.e. for all in-flight
+// embedding-gradient atomics -- at every barrier; nothing here needs that, so
+// only the wave's LDS ops are drained.  The "memory" clobber keeps the compiler
+// from moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ void set_r(f4& v, int r, float x) {
     if (r == 0) v.x = x;
     else if (r == 1) v.y = x;
@@ -51,14 +76,17 @@ __device__ __forceinline__ void set_r(f4& v, int r, float x) {
 template <int F, int L, int MODE, bool FWD_ONLY>
 __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     using S_ = Shape<F, L, MODE>;
+    static_assert(!S_::MLP || S_::KT(0) <= NWAVES, "layer-0 wgrad: one 16-column block per wave");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* sW = smem;
-    int* su = reinterpret_cast<int*>(smem + S_::W_TOTAL);
-    int* si = su + TILE_ROWS;
-    float* slab_ = reinterpret_cast<float*>(si + TILE_ROWS);
-    float* szg = slab_ + TILE_ROWS;
-    float* sdz = szg + TILE_ROWS;
-    float* sstage = sdz + TILE_ROWS;  // union: per-wave staging | slab image
+    int* su2 = reinterpret_cast<int*>(smem + S_::W_TOTAL);  // [2][TILE_ROWS] user ids (-1 = padding row)
+    int* si2 = su2 + 2 * TILE_ROWS;                         // [2][TILE_ROWS] item ids
+    float* slab2 = reinterpret_cast<float*>(si2 + 2 * TILE_ROWS);  // [2][TILE_ROWS] labels / dlogits
+    float* szg = slab2 + 2 * TILE_ROWS;  // GMF part of the logit, per tile row
+    float* sdz = szg + TILE_ROWS;        // dlogit, per tile row
+    float* sB = sdz + TILE_ROWS;         // biases, layer k at boff(k), zero-padded
+    float* sWP = sB + 128;               // predict weights, zero-padded
+    float* sstage = sWP + 128;           // union: per-wave staging | slab image
 
     const int tid = threadIdx.x;
     const int w = tid >> 6;
@@ -92,25 +120,49 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         gb_f = (float)gb;
     }
     const int64_t ntiles = (nloc + TILE_ROWS - 1) / TILE_ROWS;
+    stamp(a, 0);
 
-    // ---- tower weights -> LDS (rows padded to 16*MT with zeros) -------------
+    // Index prefetch: every thread issues the same three loads (clamped row), so
+    // the vector-memory stream is straight-line and hipcc can count vmcnt waits
+    // exactly instead of draining everything at a branch merge.
+    auto load_idx = [&](int64_t row0, int& u, int& it, float& y) {
+        const int64_t r = row0 + (tid & (TILE_ROWS - 1));
+        const bool ok = r < nloc;
+        const int64_t rc = base + (ok ? r : 0);
+        u = a.users[rc];
+        it = a.items[rc];
+        if constexpr (!FWD_ONLY) y = a.labels[rc];  // forward launches carry no labels
+        if (!ok) u = it = -1;
+    };
+    int nu = -1, ni = -1;
+    float nlab = 0.f;
+    if ((int64_t)blockIdx.x < ntiles) load_idx((int64_t)blockIdx.x * TILE_ROWS, nu, ni, nlab);
+
+    // ---- tower weights, biases, predict weights -> LDS (zero-padded) ---------
     if constexpr (S_::MLP) {
         static_for<L>([&](auto kk) {
             constexpr int k = decltype(kk)::value;
-            constexpr int rows = 16 * S_::MT(k), cols = S_::S(k), outs = S_::S(k + 1);
-            const float* Wg = prm + lay.w[k];
+            constexpr int rows = 16 * S_::MT(k), cols4 = S_::S(k) / 4, outs = S_::S(k + 1);
+            const f4* Wg = reinterpret_cast<const f4*>(prm + lay.w[k]);
             float* Ws = sW + S_::woff(k);
-            for (int e = tid; e < rows * cols; e += NTHREADS) {
-                const int o = e / cols, i = e - o * cols;
-                Ws[o * S_::SW(k) + i] = o < outs ? Wg[e] : 0.0f;
+            for (int e = tid; e < rows * cols4; e += NTHREADS) {
+                const int o = e / cols4, i4 = e - o * cols4;
+                const f4 v = o < outs ? Wg[e] : f4{0.f, 0.f, 0.f, 0.f};
+                *reinterpret_cast<f4*>(Ws + o * S_::SW(k) + 4 * i4) = v;
             }
+            for (int e = tid; e < 16 * S_::MT(k); e += NTHREADS)
+                sB[S_::boff(k) + e] = e < outs ? prm[lay.b[k] + e] : 0.f;
         });
     }
+    for (int e = tid; e < 128; e += NTHREADS) sWP[e] = e < S_::P ? prm[lay.wp + e] : 0.f;
 
     // ---- per-lane persistent accumulators ----------------------------------
-    constexpr int TPW0 = S_::TPW(0) > 0 ? S_::TPW(0) : 1;
+    constexpr int MT0 = S_::MLP ? S_::MT(0) : 1;
+    constexpr int KT0 = S_::KT0;
     constexpr int MTL = S_::MLP ? S_::MT(L - 1) : 1;
-    f4 accW[L][TPW0];
+    constexpr int TPWK = (L > 1 && S_::MLP) ? S_::TPW(1) : 1;  // layers k >= 1 (TPW(k) <= TPW(1))
+    f4 accW0[MT0];          // dW_0 tiles (mt, nt = w)
+    f4 accWk[L][TPWK];      // dW_k tiles, k >= 1 (round-robin blocks)
     float dbAcc[L];
     f4 dWpT[MTL];
     float dWpG = 0.f, dbpAcc = 0.f, lossAcc = 0.f;
@@ -118,8 +170,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     for (int k = 0; k < L; ++k) {
         dbAcc[k] = 0.f;
 #pragma unroll
-        for (int j = 0; j < TPW0; ++j) accW[k][j] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < TPWK; ++j) accWk[k][j] = f4{0.f, 0.f, 0.f, 0.f};
     }
+#pragma unroll
+    for (int t = 0; t < MT0; ++t) accW0[t] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < MTL; ++t) dWpT[t] = f4{0.f, 0.f, 0.f, 0.f};
 
@@ -127,38 +181,128 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     constexpr int NI = S_::GMF ? 16 / RPI : 1;
     const float bpv = prm[lay.bp];
     const float wpf = S_::GMF ? prm[lay.wp + l0 % F] : 0.f;
+    if (tid < TILE_ROWS) {
+        su2[tid] = nu;
+        si2[tid] = ni;
+        slab2[tid] = nlab;
+    }
     __syncthreads();
+
+    // Embedding fragments of the current tile, loaded one tile ahead:
+    //   X0[t]  : MLP input, orientation A: row c, features 16t + 4g .. +3
+    //   ugv/igv: GMF rows, row-major lanes (feature l % F, rows j*RPI + l / F)
+    f4 X0[KT0];
+    float ugv[NI], igv[NI];
+    auto load_emb = [&](const int* su, const int* si, int c, int g, int l) {
+        const int wr = w * 16;
+        if constexpr (S_::MLP) {
+            constexpr int DM = S_::DM;
+            const int uc = max(su[wr + c], 0);
+            const int ic = max(si[wr + c], 0);
+#pragma unroll
+            for (int t = 0; t < KT0; ++t) {
+                const int j0 = 16 * t + 4 * g;
+                const bool isu = j0 < DM;
+                const int64_t off = isu ? lay.um + (int64_t)uc * DM + j0 : lay.im + (int64_t)ic * DM + (j0 - DM);
+                X0[t] = *reinterpret_cast<const f4*>(prm + off);
+            }
+        }
+        if constexpr (S_::GMF) {
+            const int gf = l % F, gq0 = l / F;
+#pragma unroll
+            for (int j = 0; j < NI; ++j) {
+                const int q = wr + j * RPI + gq0;
+                ugv[j] = prm[lay.ug + (int64_t)max(su[q], 0) * F + gf];
+                igv[j] = prm[lay.ig + (int64_t)max(si[q], 0) * F + gf];
+            }
+        }
+    };
+    // Item-side embedding gradients of a wave's 16 rows: rows of a tile are
+    // grouped by item (ncf_prepare_epoch counting-sorts each batch by item), so
+    // consecutive equal items are summed in LDS and each item segment issues one
+    // atomic per feature -- 256 contiguous bytes per wave-instruction for the MLP
+    // table -- instead of one per row.  Correct for any row order (unsorted
+    // input just yields shorter segments).  scr holds the MLP item rows
+    // [16][SCM] (written by the caller); the GMF item rows go to [16][SCG] after it.
+    auto item_segments = [&](float* scr, const TrainArgs& a, const int* su, const int* si, int wr, int l,
+                             const float* gIg, int gf, int gq0) {
+        (void)su;
+        if constexpr (S_::GMF) {
+            float* sg = scr + 16 * S_::SCM;
+#pragma unroll
+            for (int j = 0; j < NI; ++j) sg[(j * RPI + gq0) * S_::SCG + gf] = gIg[j];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // same-wave LDS hand-off
+        if constexpr (S_::MLP) {
+            constexpr int DM = S_::DM;
+#pragma unroll
+            for (int f0 = 0; f0 < DM; f0 += 64) {
+                const int f = f0 + l;
+                float sum = 0.f;
+                for (int row = 0; row < 16; ++row) {
+                    const int it = si[wr + row];
+                    if (f < DM) sum += scr[row * S_::SCM + f];
+                    const bool last = row == 15 || si[wr + row + 1] != it;
+                    if (last) {
+                        if (it >= 0 && f < DM) atomicAdd(a.grads + lay.im + (int64_t)it * DM + f, sum);
+                        sum = 0.f;
+                    }
+                }
+            }
+        }
+        if constexpr (S_::GMF) {
+            const float* sg = scr + 16 * S_::SCM;
+            float sum = 0.f;
+            for (int row = 0; row < 16; ++row) {
+                const int it = si[wr + row];
+                if (l < F) sum += sg[row * S_::SCG + l];
+                const bool last = row == 15 || si[wr + row + 1] != it;
+                if (last) {
+                    if (it >= 0 && l < F) atomicAdd(a.grads + lay.ig + (int64_t)it * F + l, sum);
+                    sum = 0.f;
+                }
+            }
+        }
+    };
+    load_emb(su2, si2, c0, g0, l0);
+    // Consume the first tile's fragments here: the loop header then sees them
+    // as complete on entry, and hipcc's counted wait at their first use inside
+    // the loop is set by the steady state (older than this tile's scatter
+    // atomics: vmcnt(#atomics + 3)), not drained to the index loads.
+    if constexpr (S_::MLP) {
+#pragma unroll
+        for (int t = 0; t < KT0; ++t) asm volatile("" ::"v"(X0[t]));
+    }
+    if constexpr (S_::GMF) {
+#pragma unroll
+        for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(ugv[j]), "v"(igv[j]));
+    }
+    stamp(a, 1);
+    int titer = 0;
 
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = tile * TILE_ROWS;
-        if (tid < TILE_ROWS) {
-            const int64_t r = row0 + tid;
-            const bool ok = r < nloc;
-            su[tid] = ok ? a.users[base + r] : -1;
-            si[tid] = ok ? a.items[base + r] : -1;
-            if constexpr (!FWD_ONLY) slab_[tid] = ok ? a.labels[base + r] : 0.f;
-        }
-        __syncthreads();
-        const int wr = w * 16;  // first WG-tile row of this wave
-        // Opaque per-tile copies of the lane coordinates: every address below is
-        // recomputed inside the tile loop instead of being hoisted out of it and
-        // held in (spilled) VGPRs for the whole launch.
+        const int buf = titer & 1;
+        const int* su = su2 + buf * TILE_ROWS;
+        const int* si = si2 + buf * TILE_ROWS;
+        const float* slab_ = slab2 + buf * TILE_ROWS;
+        const bool has_next = tile + gridDim.x < ntiles;
+        const int sb = 2 + 14 * titer;  // stamp base of this tile
+        stamp(a, sb + 0);
+        const int wr = w * 16;  // first tile row of this wave
+        // Opaque per-tile copies of the lane coordinates: addresses are recomputed
+        // inside the loop instead of being hoisted out of it (and spilled).
         int c = c0, g = g0, l = l0;
         asm volatile("" : "+v"(c), "+v"(g), "+v"(l));
         const int gf = l % F;
         const int gq0 = l / F;
 
-        // ================= GMF forward (row-major lanes: f = l % F) ==========
-        float ugv[NI], igv[NI];
+        // (a) next tile's indices
+        load_idx(row0 + (int64_t)gridDim.x * TILE_ROWS, nu, ni, nlab);
+        if (!has_next) nu = ni = -1;
+
+        // (b) GMF forward
         if constexpr (S_::GMF) {
-#pragma unroll
-            for (int j = 0; j < NI; ++j) {
-                const int q = wr + j * RPI + gq0;
-                const int u = su[q] < 0 ? 0 : su[q];
-                const int it = si[q] < 0 ? 0 : si[q];
-                ugv[j] = prm[lay.ug + (int64_t)u * F + gf];
-                igv[j] = prm[lay.ig + (int64_t)it * F + gf];
-            }
 #pragma unroll
             for (int j = 0; j < NI; ++j) {
                 float v = wpf * (ugv[j] * igv[j]);
@@ -168,32 +312,18 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
             }
         }
 
-        // ================= MLP forward (orientation A) =======================
+        // (c) MLP forward (orientation A)
         const int myq = wr + c;
-        f4 H[L + 1][S_::KT0];
+        f4 H[L + 1][KT0];
         if constexpr (S_::MLP) {
-            constexpr int DM = S_::DM;
-            const int uc = su[myq] < 0 ? 0 : su[myq];
-            const int ic = si[myq] < 0 ? 0 : si[myq];
 #pragma unroll
-            for (int t = 0; t < S_::KT(0); ++t) {
-                const int j0 = 16 * t + 4 * g;
-                const bool isu = j0 < DM;
-                const int64_t off = isu ? lay.um + (int64_t)uc * DM + j0 : lay.im + (int64_t)ic * DM + (j0 - DM);
-                H[0][t] = *reinterpret_cast<const f4*>(prm + off);
-            }
+            for (int t = 0; t < KT0; ++t) H[0][t] = X0[t];
             static_for<L>([&](auto kk) {
                 constexpr int k = decltype(kk)::value;
                 f4 acc[S_::MT(k)];
-                const float* bk = prm + lay.b[k];
 #pragma unroll
-                for (int mt = 0; mt < S_::MT(k); ++mt) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int o = 16 * mt + 4 * g + r;
-                        set_r(acc[mt], r, o < S_::S(k + 1) ? bk[o] : 0.f);
-                    }
-                }
+                for (int mt = 0; mt < S_::MT(k); ++mt)
+                    acc[mt] = *reinterpret_cast<const f4*>(sB + S_::boff(k) + 16 * mt + 4 * g);
                 const float* Ws = sW + S_::woff(k);
 #pragma unroll
                 for (int t = 0; t < S_::KT(k); ++t) {
@@ -219,8 +349,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                 }
             });
         }
+        stamp(a, sb + 1);
 
-        // ================= predict + loss + dlogit ===========================
+        // predict
         float zt = 0.f;
         if constexpr (S_::MLP) {
 #pragma unroll
@@ -228,7 +359,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int o = 16 * mt + 4 * g + r;
-                    if (o < F) zt += prm[lay.wp + S_::POFF + o] * lane_get(H[L][mt], r);
+                    if (o < F) zt += sWP[S_::POFF + o] * lane_get(H[L][mt], r);
                 }
             }
             zt += shfl_xor(zt, 16);
@@ -237,11 +368,38 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         if constexpr (S_::GMF) zt += szg[myq];
         const float z = zt + bpv;
         const bool valid = su[myq] >= 0;
+
         if constexpr (FWD_ONLY) {
             if (g == 0 && valid) a.logits_out[base + row0 + myq] = z;
-            __syncthreads();
+            if (tid < TILE_ROWS) {
+                su2[(buf ^ 1) * TILE_ROWS + tid] = nu;
+                si2[(buf ^ 1) * TILE_ROWS + tid] = ni;
+            }
+            lds_barrier();
+            load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
+            ++titer;
             continue;
         } else {
+            // (d) layer-0 wgrad operand: X0 rows of the whole tile, columns 16*nt + c
+            constexpr int DM = S_::DM;
+            float bx[S_::MLP ? NWAVES * 4 : 1];
+            const int nt0 = w < KT0 ? w : KT0 - 1;
+            if constexpr (S_::MLP) {
+                const int fj = 16 * nt0 + c;
+                const bool isu = fj < DM;
+                const int64_t tab = isu ? lay.um + fj : lay.im + (fj - DM);
+                const int* ids = isu ? su : si;
+#pragma unroll
+                for (int ws = 0; ws < NWAVES; ++ws) {
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        const int id = max(ids[ws * 16 + 4 * g + s], 0);
+                        bx[ws * 4 + s] = prm[tab + (int64_t)id * DM];
+                    }
+                }
+            }
+
+            // (e) loss + dlogit
             if (a.logits_out != nullptr && g == 0 && valid) a.logits_out[row0 + myq] = z;
             float dz = 0.f;
             if (valid) {
@@ -257,25 +415,24 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                 sdz[myq] = dz;
                 dbpAcc += dz;
             }
-
-            // ============= GMF backward (row-major lanes) =====================
+            // GMF backward.  User side: unconditional atomics (padding rows add 0
+            // to row 0).  Item side: kept for the per-item segment reduction.
+            float gIg[NI];
             if constexpr (S_::GMF) {
 #pragma unroll
                 for (int j = 0; j < NI; ++j) {
                     const int q = wr + j * RPI + gq0;
                     const float dzq = sdz[q];
                     dWpG += dzq * (ugv[j] * igv[j]);
-                    if (su[q] >= 0 && !(a.diag & DIAG_NO_ATOMICS)) {
-                        const float dgm = dzq * wpf;
-                        atomicAdd(a.grads + lay.ug + (int64_t)su[q] * F + gf, dgm * igv[j]);
-                        atomicAdd(a.grads + lay.ig + (int64_t)si[q] * F + gf, dgm * ugv[j]);
-                    }
+                    const float dgm = dzq * wpf;
+                    atomicAdd(a.grads + lay.ug + (int64_t)max(su[q], 0) * F + gf, dgm * igv[j]);
+                    gIg[j] = dgm * ugv[j];
                 }
             }
+            stamp(a, sb + 2);
 
-            // ============= MLP backward =======================================
             if constexpr (S_::MLP) {
-                f4 D[L][S_::KT0];  // D[k] = dpre_k (orientation A)
+                f4 D[L][KT0];  // D[k] = dpre_k (orientation A)
 #pragma unroll
                 for (int mt = 0; mt < MTL; ++mt) {
                     const f4 h = H[L][mt];
@@ -284,7 +441,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                     for (int r = 0; r < 4; ++r) {
                         const int o = 16 * mt + 4 * g + r;
                         const float hv = lane_get(h, r);
-                        const float wv = o < F ? prm[lay.wp + S_::POFF + o] : 0.f;
+                        const float wv = o < F ? sWP[S_::POFF + o] : 0.f;
                         set_r(d, r, hv > 0.f ? dz * wv : 0.f);
                     }
                     D[L - 1][mt] = d;
@@ -296,7 +453,6 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                 static_for<L>([&](auto ii) {
                     constexpr int k = L - 1 - decltype(ii)::value;
                     constexpr int RK = (k & 1) ? S_::R0 : 0;
-                    // ---- stage dpre_k (and H_k) row-major for the shared wgrad
                     float* st = sstage + w * S_::WAVE_STAGE + RK;
 #pragma unroll
                     for (int mt = 0; mt < S_::MT(k); ++mt)
@@ -306,66 +462,91 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
                         for (int t = 0; t < S_::KT(k); ++t)
                             *reinterpret_cast<f4*>(sh + c * S_::SH(k) + 16 * t + 4 * g) = H[k][t];
+                    } else {
+                        // publish the next tile's indices with the layer-0 barrier
+                        if (tid < TILE_ROWS) {
+                            su2[(buf ^ 1) * TILE_ROWS + tid] = nu;
+                            si2[(buf ^ 1) * TILE_ROWS + tid] = ni;
+                            slab2[(buf ^ 1) * TILE_ROWS + tid] = nlab;
+                        }
                     }
-                    __syncthreads();
-                    // ---- bias grad: this wave's 16 rows, lane = output feature
+                    lds_barrier();
+                    stamp(a, sb + 3 + 3 * (L - 1 - k));
+                    // bias grad: this wave's 16 rows, lane = output feature
                     if (l < S_::S(k + 1)) {
                         float s = 0.f;
 #pragma unroll
                         for (int rr = 0; rr < 16; ++rr) s += st[rr * S_::SD(k) + l];
                         dbAcc[k] += s;
                     }
-                    // ---- wgrad: dW_k[out][in] += sum_rows dpre_k[row][out] * H_k[row][in]
-                    constexpr int T = S_::MT(k) * S_::KT(k);
-                    constexpr int tpw = S_::TPW(k);
-                    float bx[k == 0 ? NWAVES * 4 : 1];
-                    int loaded_nt = -1;
+                    // wgrad: dW_k[out][in] += sum_rows dpre_k[row][out] * H_k[row][in]
+                    if constexpr (k == 0) {
+                        if (w < KT0 && !(a.diag & DIAG_NO_WGRAD)) {
 #pragma unroll
-                    for (int jl = 0; jl < tpw; ++jl) {
-                        const int j = w * tpw + jl;
-                        if (j < T && !(a.diag & DIAG_NO_WGRAD)) {
-                            const int mt = j % S_::MT(k);
-                            const int nt = j / S_::MT(k);
-                            if constexpr (k == 0) {
-                                if (nt != loaded_nt) {
-                                    // layer-0 input rows come straight from the embedding tables
-                                    constexpr int DM = S_::DM;
-                                    const int fj = 16 * nt + c;
+                            for (int mt = 0; mt < MT0; ++mt) {
+                                f4 acc0 = accW0[mt], acc1 = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                                    for (int ws = 0; ws < NWAVES; ++ws) {
+                                for (int ws = 0; ws < NWAVES; ++ws) {
+                                    const float* sto = sstage + ws * S_::WAVE_STAGE;
 #pragma unroll
-                                        for (int s = 0; s < 4; ++s) {
-                                            const int q = ws * 16 + 4 * g + s;
-                                            const bool isu = fj < DM;
-                                            const int id = max(isu ? su[q] : si[q], 0);
-                                            const int64_t off = (isu ? lay.um : lay.im - DM) + (int64_t)id * DM + fj;
-                                            bx[ws * 4 + s] = prm[off];
-                                        }
+                                    for (int s = 0; s < 4; ++s) {
+                                        const float av = sto[(4 * g + s) * S_::SD(0) + 16 * mt + c];
+                                        if (ws & 1)
+                                            acc1 = MFMA4(av, bx[ws * 4 + s], acc1);
+                                        else
+                                            acc0 = MFMA4(av, bx[ws * 4 + s], acc0);
                                     }
-                                    loaded_nt = nt;
+                                    if (ws & 1) __builtin_amdgcn_sched_barrier(0);
                                 }
+                                acc0.x += acc1.x;
+                                acc0.y += acc1.y;
+                                acc0.z += acc1.z;
+                                acc0.w += acc1.w;
+                                accW0[mt] = acc0;
                             }
-                            f4 acc = accW[k][jl];
+                        }
+                    } else {
+                        constexpr int T = S_::MT(k) * S_::KT(k);
+                        constexpr int tpw = S_::TPW(k);
 #pragma unroll
-                            for (int ws = 0; ws < NWAVES; ++ws) {
-                                const float* sto = sstage + ws * S_::WAVE_STAGE + RK;
+                        for (int jl = 0; jl < tpw; ++jl) {
+                            const int j = w * tpw + jl;
+                            if (j < T && !(a.diag & DIAG_NO_WGRAD)) {
+                                const int mt = j % S_::MT(k);
+                                const int nt = j / S_::MT(k);
+                                f4 acc0 = accWk[k][jl], acc1 = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                                for (int s = 0; s < 4; ++s) {
-                                    const int row = 4 * g + s;
-                                    const float av = sto[row * S_::SD(k) + 16 * mt + c];
-                                    float bv;
-                                    if constexpr (k >= 1)
-                                        bv = sto[16 * S_::SD(k) + row * S_::SH(k) + 16 * nt + c];
-                                    else
-                                        bv = bx[ws * 4 + s];
-                                    acc = MFMA4(av, bv, acc);
+                                for (int ws = 0; ws < NWAVES; ++ws) {
+                                    const float* sto = sstage + ws * S_::WAVE_STAGE + RK;
+#pragma unroll
+                                    for (int s = 0; s < 4; ++s) {
+                                        const int row = 4 * g + s;
+                                        const float av = sto[row * S_::SD(k) + 16 * mt + c];
+                                        const float bv = sto[16 * S_::SD(k) + row * S_::SH(k) + 16 * nt + c];
+                                        if (ws & 1)
+                                            acc1 = MFMA4(av, bv, acc1);
+                                        else
+                                            acc0 = MFMA4(av, bv, acc0);
+                                    }
+                                    if (ws & 1) __builtin_amdgcn_sched_barrier(0);
                                 }
-                                __builtin_amdgcn_sched_barrier(0);
+                                acc0.x += acc1.x;
+                                acc0.y += acc1.y;
+                                acc0.z += acc1.z;
+                                acc0.w += acc1.w;
+                                accWk[k][jl] = acc0;
                             }
-                            accW[k][jl] = acc;
                         }
                     }
-                    // ---- dgrad
+                    stamp(a, sb + 4 + 3 * (L - 1 - k));
+                    if constexpr (k == 0) {
+                        // (h) next tile's embedding fragments: after the layer-0 wgrad
+                        // (whose operand loads then wait on nothing younger than the
+                        // GMF atomics) and before this tile's scatter atomics (so
+                        // the next tile waits on them only, not on the atomics)
+                        load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
+                    }
+                    // dgrad
                     const float* Ws = sW + S_::woff(k);
                     if constexpr (k >= 1) {
                         f4 acc[S_::KT(k)];
@@ -397,10 +578,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                         }
                     } else {
                         // orientation B: C[i = row 4g+r][j = in-feature 16*nt + c]
-                        constexpr int DM = S_::DM;
-                        f4 acc[S_::KT(0)];
+                        f4 acc[KT0];
 #pragma unroll
-                        for (int nt = 0; nt < S_::KT(0); ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
+                        for (int nt = 0; nt < KT0; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                         for (int t = 0; t < S_::MT(0); ++t) {
                             const f4 dv = D[0][t];
@@ -408,32 +588,60 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                             for (int r = 0; r < 4; ++r) {
                                 const float av = lane_get(dv, r);
 #pragma unroll
-                                for (int nt = 0; nt < S_::KT(0); ++nt) {
+                                for (int nt = 0; nt < KT0; ++nt) {
                                     const float wv = Ws[(16 * t + 4 * g + r) * S_::SW(0) + 16 * nt + c];
                                     acc[nt] = MFMA4(av, wv, acc[nt]);
                                 }
                                 __builtin_amdgcn_sched_barrier(0);
                             }
                         }
+                        // item half -> this wave's scratch rows (segment-reduced below);
+                        // user half -> unconditional atomics (padding rows add 0 to row 0)
+                        float* scr = sstage + w * S_::WAVE_STAGE + S_::R0;
+                        if constexpr (DM >= 16) {  // the split is 16-column aligned
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int q = wr + 4 * g + r;
-                            const int uu = su[q];
-                            const int iq = si[q];
-                            if (uu >= 0 && !(a.diag & DIAG_NO_ATOMICS)) {
+                            for (int r = 0; r < 4; ++r) {
 #pragma unroll
-                                for (int nt = 0; nt < S_::KT(0); ++nt) {
-                                    const int fj = 16 * nt + c;
-                                    const bool isu = fj < DM;
-                                    const int64_t off = (isu ? lay.um : lay.im - DM) + (int64_t)(isu ? uu : iq) * DM + fj;
-                                    atomicAdd(a.grads + off, lane_get(acc[nt], r));
-                                }
+                                for (int nt = DM / 16; nt < KT0; ++nt)
+                                    scr[(4 * g + r) * S_::SCM + 16 * nt + c - DM] = lane_get(acc[nt], r);
+                            }
+                            item_segments(scr, a, su, si, wr, l, gIg, gf, gq0);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int uu = max(su[wr + 4 * g + r], 0);
+#pragma unroll
+                                for (int nt = 0; nt < DM / 16; ++nt)
+                                    atomicAdd(a.grads + lay.um + (int64_t)uu * DM + 16 * nt + c,
+                                              lane_get(acc[nt], r));
+                            }
+                        } else {  // DM == 8: one 16-column tile, lanes c < 8 user, c >= 8 item
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                if (c >= DM) scr[(4 * g + r) * S_::SCM + c - DM] = lane_get(acc[0], r);
+                            item_segments(scr, a, su, si, wr, l, gIg, gf, gq0);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int uu = max(su[wr + 4 * g + r], 0);
+                                if (c < DM) atomicAdd(a.grads + lay.um + (int64_t)uu * DM + c, lane_get(acc[0], r));
                             }
                         }
                     }
+                    stamp(a, sb + 5 + 3 * (L - 1 - k));
                 });
+            } else {
+                // GMF-only model: item-side GMF rows, then publish next indices
+                item_segments(sstage + w * S_::WAVE_STAGE + S_::R0, a, su, si, wr, l, gIg, gf, gq0);
+                if (tid < TILE_ROWS) {
+                    su2[(buf ^ 1) * TILE_ROWS + tid] = nu;
+                    si2[(buf ^ 1) * TILE_ROWS + tid] = ni;
+                    slab2[(buf ^ 1) * TILE_ROWS + tid] = nlab;
+                }
+                lds_barrier();
+                load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
             }
-            __syncthreads();
+            lds_barrier();
+            stamp(a, sb + 13);
+            ++titer;
         }
     }
 
@@ -444,25 +652,38 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         const int len = (int)lay.tower_len + 64;  // slab stride (ncf_slab_stride); loss at tower_len
         float* img = sstage;
         const int l = l0, c = c0, g = g0, gf = l0 % F;
-        __syncthreads();
+        lds_barrier();
         for (int e = lo + tid; e < len; e += NTHREADS) img[e] = 0.f;
-        __syncthreads();
+        lds_barrier();
         if constexpr (S_::MLP) {
+            if (w < KT0) {
+                float* dW = img + (lay.w[0] - tb);
+#pragma unroll
+                for (int mt = 0; mt < MT0; ++mt) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int o = 16 * mt + 4 * g + r;
+                        if (o < S_::S(1)) dW[o * S_::S(0) + 16 * w + c] = lane_get(accW0[mt], r);
+                    }
+                }
+            }
             static_for<L>([&](auto kk) {
                 constexpr int k = decltype(kk)::value;
-                constexpr int T = S_::MT(k) * S_::KT(k);
-                constexpr int tpw = S_::TPW(k);
-                float* dW = img + (lay.w[k] - tb);
+                if constexpr (k >= 1) {
+                    constexpr int T = S_::MT(k) * S_::KT(k);
+                    constexpr int tpw = S_::TPW(k);
+                    float* dW = img + (lay.w[k] - tb);
 #pragma unroll
-                for (int jl = 0; jl < tpw; ++jl) {
-                    const int j = w * tpw + jl;
-                    if (j < T) {
-                        const int mt = j % S_::MT(k);
-                        const int nt = j / S_::MT(k);
+                    for (int jl = 0; jl < tpw; ++jl) {
+                        const int j = w * tpw + jl;
+                        if (j < T) {
+                            const int mt = j % S_::MT(k);
+                            const int nt = j / S_::MT(k);
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int o = 16 * mt + 4 * g + r;
-                            if (o < S_::S(k + 1)) dW[o * S_::S(k) + 16 * nt + c] = lane_get(accW[k][jl], r);
+                            for (int r = 0; r < 4; ++r) {
+                                const int o = 16 * mt + 4 * g + r;
+                                if (o < S_::S(k + 1)) dW[o * S_::S(k) + 16 * nt + c] = lane_get(accWk[k][jl], r);
+                            }
                         }
                     }
                 }
@@ -482,9 +703,14 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
             atomicAdd(img + (lay.bp - tb), dbpAcc);
             atomicAdd(img + lay.tower_len, lossAcc / gb_f);
         }
-        __syncthreads();
+        lds_barrier();
+        stamp(a, 60);
         float* out = a.slab + (int64_t)blockIdx.x * len;
         for (int e = lo + tid; e < len; e += NTHREADS) out[e] = img[e];
+#ifdef NCF_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        stamp(a, 61);
     }
 }
 

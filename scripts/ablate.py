@@ -24,7 +24,7 @@ def main():
         eng, model, ds, _ = bench.setup_engine(cfg, 1, 0, dev, None, rows)
         eng.run(3, use_graph=False)
         torch.cuda.synchronize()
-        variants = {"full": 0, "no_atomics": 1, "no_wgrad": 2, "no_atomics_no_wgrad": 3}
+        variants = {"full": 0, "no_wgrad": 2}
         times = {k: [] for k in variants}
         for _ in range(5):
             for name, d in variants.items():

@@ -17,6 +17,11 @@ run() {  # name, seconds, cmd...
     local rc=$?
     echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
     tail -5 "gpurun_out/$name.log"
+    # a GPU fault can surface as a Python exception (exit 1): stop on its signature too
+    if grep -qE "illegal memory access|hipErrorIllegalAddress|HIP error|Memory access fault|GPU Hang" "gpurun_out/$name.log"; then
+        echo "stopping after $name: GPU fault signature in log"
+        exit 90
+    fi
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
         echo "stopping after $name (rc=$rc)"
         exit $rc

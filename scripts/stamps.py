@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Phase attribution of the fused step kernel from s_memtime stamps
+(diagnostics build: NCF_HIP_LIB=diag, `make -C ncf_amd/csrc diag`)."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+os.environ["NCF_HIP_LIB"] = "diag"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+NAMES = {0: "start", 1: "weights->LDS"}
+for t in range(4):
+    b = 2 + 14 * t
+    NAMES.update({b: f"t{t}:idx+barrier", b + 1: f"t{t}:fwd", b + 2: f"t{t}:loss+gmf_bwd"})
+    for j in range(3):
+        NAMES.update({b + 3 + 3 * j: f"t{t}:L{2-j}:stage+bar", b + 4 + 3 * j: f"t{t}:L{2-j}:wgrad",
+                      b + 5 + 3 * j: f"t{t}:L{2-j}:dgrad"})
+    NAMES[b + 13] = f"t{t}:end-barrier"
+NAMES.update({60: "epilogue:img", 61: "epilogue:store"})
+
+
+def main():
+    import bench
+    import ncf_amd._lib as L
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    rows = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    eng, model, ds, _ = bench.setup_engine("c3", 1, 0, dev, None, rows)
+    eng.run(5, use_graph=False)
+    nwg = L.hip().ncf_slab_rows()
+    buf = torch.zeros(nwg * 64, dtype=torch.int64, device=dev)
+    out = {}
+    for rep in range(3):
+        buf.zero_()
+        L.hip().ncf_debug_set_stamps(buf.data_ptr())
+        eng.run(1, use_graph=False)
+        torch.cuda.synchronize()
+        L.hip().ncf_debug_set_stamps(None)
+        st = buf.view(nwg, 64).cpu().numpy().astype(np.int64)
+        t0 = st[:, 0:1]
+        rel = st - t0
+        for idx, name in sorted(NAMES.items()):
+            col = st[:, idx]
+            ok = col > 0
+            if ok.sum() == 0:
+                continue
+            prev = [i for i in sorted(NAMES) if i < idx and (st[ok, i] > 0).all()]
+            d = (col[ok] - st[ok, prev[-1]]) if prev else col[ok] * 0
+            out.setdefault(name, []).append([float(np.median(d)), float(np.median(rel[ok, idx]))])
+    res = {k: {"delta_cycles_median": np.median([x[0] for x in v]), "since_start": np.median([x[1] for x in v])}
+           for k, v in out.items()}
+    print(json.dumps({"rows": rows, "phases": res}))
+
+
+if __name__ == "__main__":
+    main()

@@ -208,3 +208,29 @@ def test_gather_epoch():
     L.check(L.hip().ncf_gather_epoch(u.data_ptr(), i.data_ptr(), y.data_ptr(), perm.data_ptr(), n, uo.data_ptr(),
                                      io.data_ptr(), yo.data_ptr(), L.stream_ptr()), "gather")
     assert torch.equal(uo, u[perm]) and torch.equal(io, i[perm]) and torch.equal(yo, y[perm])
+
+
+@pytest.mark.parametrize("n,bs,n_items", [(10007, 1000, 37), (65536 * 2 + 123, 65536, 3707), (5000, 5000, 1)])
+def test_prepare_epoch_batches_grouped_by_item(n, bs, n_items):
+    """Per batch: same rows as the plain shuffle (DataLoader membership), grouped by item."""
+    import ncf_amd._lib as L
+    rng = np.random.default_rng(n)
+    u = torch.as_tensor(rng.integers(0, 500, n), dtype=torch.int32, device=DEV)
+    i = torch.as_tensor(rng.integers(0, n_items, n), dtype=torch.int32, device=DEV)
+    y = torch.as_tensor(rng.random(n) < 0.3, dtype=torch.float32, device=DEV)
+    perm = torch.randperm(n, device=DEV)
+    uo, io, yo = torch.empty_like(u), torch.empty_like(i), torch.empty_like(y)
+    L.check(L.hip().ncf_prepare_epoch(u.data_ptr(), i.data_ptr(), y.data_ptr(), perm.data_ptr(), n, bs, n_items,
+                                      uo.data_ptr(), io.data_ptr(), yo.data_ptr(), L.stream_ptr()), "prep")
+    torch.cuda.synchronize()
+    su, si, sy = u[perm].cpu().numpy(), i[perm].cpu().numpy(), y[perm].cpu().numpy()
+    go, gi, gy = uo.cpu().numpy(), io.cpu().numpy(), yo.cpu().numpy()
+    for b0 in range(0, n, bs):
+        sl = slice(b0, min(n, b0 + bs))
+        assert (np.diff(gi[sl]) >= 0).all(), "batch not grouped by item"
+        key = lambda a, b_, c: np.lexsort((c, a, b_))
+        e = np.stack([si[sl], su[sl], sy[sl]], 1)
+        o = np.stack([gi[sl], go[sl], gy[sl]], 1)
+        e = e[np.lexsort(e.T[::-1])]
+        o = o[np.lexsort(o.T[::-1])]
+        assert np.array_equal(e, o)
