@@ -1,0 +1,144 @@
+"""``Trainer.fit()/evaluate()`` -- the training loop of the reference scripts as an API.
+
+The reference has no Trainer: the loop is written inline in
+scripts/train_neumf.py:98-144 (and scripts/pretrain.py:61-106).  This class
+runs exactly that loop -- same RNG consumption, same batches, same loss,
+optimizer, evaluation, printed lines and return dict (train_neumf.py:159-167)
+-- with every step on the device engine (ncf_amd.engine.TrainEngine):
+
+  per epoch (train_neumf.py:98-131)
+    dataset.ng_sample()                       NumPy global MT19937 stream (C++ sampler)
+    DataLoader(shuffle=True) order            torch global generator: base_seed, sampler
+                                              seed, randperm (data.epoch_permutation)
+    for each batch: zero_grad/fwd/BCE/bwd/step -> one captured hipGraph replay
+    metrics(model, test_loader, top_k)        one forward + one HR/NDCG launch; one
+                                              base_seed draw, like the test DataLoader
+    "Epoch %03d: Loss=%.4f, HR=%.3f, NDCG=%.3f, Time=%.1fs"
+
+Data parallel (world_size > 1): every rank runs the same host stream (same
+seeds), processes its contiguous shard of each global batch, and the engine
+all-reduces gradients over RCCL; evaluation and checkpoints are rank 0's.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .data import NCFData, consume_test_pass, epoch_permutation
+from .engine import TrainEngine
+from .metrics import evaluate_arrays
+
+
+class Trainer:
+    def __init__(self, model, train_dataset: NCFData, test_loader=None, *, batch_size=256, lr=1e-3,
+                 optimizer="adam", top_k=10, device=None, world_size=1, rank=0, process_group=None,
+                 use_graph=True, save_path=None, verbose=True, test_batch=None):
+        self.model = model
+        self.ds = train_dataset
+        self.test_loader = test_loader
+        self.batch_size = int(batch_size)
+        self.top_k = int(top_k)
+        self.device = torch.device(device) if device is not None else model.embed_user_GMF.weight.device
+        if self.device.type != "cuda":
+            raise RuntimeError("Trainer runs the HIP engine: put the model on a HIP device")
+        if model.embed_user_GMF.weight.device != self.device:
+            model.to(self.device)
+        self.world_size, self.rank = int(world_size), int(rank)
+        self.engine = TrainEngine(model, lr=lr, optimizer=optimizer, world_size=world_size, rank=rank,
+                                  process_group=process_group)
+        self.use_graph = use_graph
+        self.save_path = save_path
+        self.verbose = verbose and self.rank == 0
+        self._test = None
+        self.test_batch = test_batch
+        self.history = []
+
+    # ------------------------------------------------------------------ data
+    def _epoch_stream(self):
+        """ng_sample + DataLoader order for one epoch -> device stream in batch order."""
+        self.ds.ng_sample()
+        u, i, y = self.ds.arrays()
+        n = len(u)
+        perm = epoch_permutation(n).to(self.device)
+        dev = self.device
+        if getattr(self, "_bufs", None) is None or self._bufs[0].numel() != n:
+            # persistent buffers: stable pointers keep the captured step graph valid
+            self._bufs = [torch.empty(n, dtype=t, device=dev)
+                          for t in (torch.int32, torch.int32, torch.float32) * 2]
+        u_d, i_d, y_d, us, its, ys = self._bufs
+        u_d.copy_(torch.from_numpy(np.ascontiguousarray(u, dtype=np.int32)))
+        i_d.copy_(torch.from_numpy(np.ascontiguousarray(i, dtype=np.int32)))
+        y_d.copy_(torch.from_numpy(np.ascontiguousarray(y, dtype=np.float32)))
+        L.check(L.hip().ncf_prepare_epoch(u_d.data_ptr(), i_d.data_ptr(), y_d.data_ptr(), perm.data_ptr(), n,
+                                          self.batch_size, int(self.model.item_num), us.data_ptr(),
+                                          its.data_ptr(), ys.data_ptr(), L.stream_ptr(dev)), "ncf_prepare_epoch")
+        return us, its, ys
+
+    def _test_arrays(self):
+        if self._test is None:
+            us, its, sizes = [], [], []
+            if self.test_loader is None:
+                raise RuntimeError("no test_loader given")
+            ds = getattr(self.test_loader, "dataset", None)
+            bs = getattr(self.test_loader, "batch_size", None)
+            if isinstance(ds, NCFData) and bs and not ds.is_training:
+                u, i, _ = ds.arrays()
+                self._test = (u.astype(np.int32), i.astype(np.int32), int(bs))
+            else:
+                for user, item, _ in self.test_loader:
+                    us.append(np.asarray(user).reshape(-1))
+                    its.append(np.asarray(item).reshape(-1))
+                    sizes.append(len(us[-1]))
+                self._test = (np.concatenate(us).astype(np.int32), np.concatenate(its).astype(np.int32),
+                              int(sizes[0]))
+        return self._test
+
+    # ------------------------------------------------------------------ API
+    def evaluate(self, top_k=None):
+        """metrics(model, test_loader, top_k) (metrics.py:4-25): per-batch HR/NDCG lists."""
+        k = self.top_k if top_k is None else int(top_k)
+        u, i, bs = self._test_arrays()
+        consume_test_pass()  # the test DataLoader iteration's base_seed draw
+        return evaluate_arrays(self.model, u, i, bs, k)
+
+    def train_epoch(self):
+        us, its, ys = self._epoch_stream()
+        self.engine.set_epoch_stream(us, its, ys, self.batch_size)
+        self.engine.run(self.engine.num_batches, use_graph=self.use_graph)
+        return float(np.mean(self.engine.epoch_losses()))
+
+    def fit(self, epochs, model_type=None, pretraining=False, save_fn=None):
+        best_hr = best_ndcg = 0
+        best_epoch = 0
+        for epoch in range(int(epochs)):
+            self.model.train()
+            t0 = time.time()
+            avg_loss = self.train_epoch()
+            self.model.eval()
+            if self.rank == 0:
+                HR, NDCG = self.evaluate()
+                hr, ndcg = float(np.mean(HR)), float(np.mean(NDCG))
+            else:
+                consume_test_pass()
+                hr = ndcg = 0.0
+            el = time.time() - t0
+            self.history.append({"epoch": epoch + 1, "loss": avg_loss, "hr": hr, "ndcg": ndcg, "time": el})
+            if self.verbose:
+                print(f"Epoch {epoch + 1:03d}: Loss={avg_loss:.4f}, HR={hr:.3f}, NDCG={ndcg:.3f}, Time={el:.1f}s")
+            if hr > best_hr:
+                best_hr, best_ndcg, best_epoch = hr, ndcg, epoch + 1
+                if save_fn is not None and self.rank == 0:
+                    save_fn(self.model)
+        n_params = sum(p.numel() for p in self.model.parameters() if p.requires_grad)
+        return {
+            "best_hr": best_hr,
+            "best_ndcg": best_ndcg,
+            "best_epoch": best_epoch,
+            "parameters": n_params,
+            "num_layers": self.model.num_layers,
+            "pretraining": pretraining,
+            "model_type": model_type or self.model.model_type,
+        }

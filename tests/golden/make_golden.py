@@ -295,6 +295,39 @@ def g6_metrics(NCF, NCFData):
     np.savez_compressed(os.path.join(HERE, "G6_metrics.npz"), **out)
 
 
+def g7_script(NCF):
+    """The reference's scripts/train_neumf.py, end to end (seeded, 2 epochs) on
+    the ml-100k-shaped synthetic files written by ncf_amd.synthetic (seed 0),
+    plus load_all's output hash on those files."""
+    import contextlib
+    import io
+    import runpy
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from ncf_amd import synthetic
+    from src.data.datasets import load_all
+    ds = synthetic.make_dataset("ml-100k", seed=0)
+    synthetic.write_reference_files(ds, "data/processed")
+    tr, te, un, inum, mat = load_all()
+    out = {"load_all_sha256": np.array(sha([np.asarray(tr, dtype=np.int64), np.asarray(te, dtype=np.int64)])),
+           "user_num": np.int64(un), "item_num": np.int64(inum), "nnz": np.int64(mat.nnz)}
+    for f, L in ((8, 3),):
+        np.random.seed(0)
+        torch.manual_seed(0)
+        argv = sys.argv
+        sys.argv = ["train_neumf.py", "--epochs", "2", "--factor_num", str(f), "--num_layers", str(L)]
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            runpy.run_path("scripts/train_neumf.py", run_name="__main__")
+        sys.argv = argv
+        lines = [l for l in buf.getvalue().splitlines() if l.startswith("Epoch ") or l.startswith("HR@")
+                 or l.startswith("NDCG@") or l.startswith("Parameters:") or l.startswith("Best Result")]
+        out[f"f{f}_L{L}_stdout"] = np.array(lines)
+        sd = torch.load(f"results/models/NeuMF_end_{L}l_{f}f_best.pth", weights_only=True)
+        out[f"f{f}_L{L}_best_sha256"] = np.array(sha([v.numpy() for v in sd.values()]))
+    np.savez_compressed(os.path.join(HERE, "G7_script.npz"), **out)
+
+
 def main():
     here_cwd = os.getcwd()
     NCF, NCFData, metrics_fn = _import_reference()
@@ -306,6 +339,7 @@ def main():
     g4_fwd_bwd(NCF)
     g5_steps(NCF)
     g6_metrics(NCF, NCFData)
+    g7_script(NCF)
     os.chdir(here_cwd)
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):

@@ -1,0 +1,76 @@
+"""End-to-end parity of Trainer.fit() / scripts/train_neumf.py against the
+reference's own scripts/train_neumf.py (tests/golden/G7_script.npz: seeded,
+2 epochs, NCF(944, 1683, 8, 3) on the ml-100k-shaped synthetic files).
+
+Same seeds -> same negatives (bit-exact), same batches (bit-exact), same init
+(bit-exact); the fp32 trajectory differs only in summation order, so per-epoch
+loss must agree to 1e-3 relative and HR@10 / NDCG@10 within 0.01 (SURVEY.md
+8(d) parity gate)."""
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _parse(lines):
+    out = []
+    for ln in lines:
+        m = re.match(r"Epoch (\d+): Loss=([\d.]+), HR=([\d.]+), NDCG=([\d.]+)", str(ln))
+        if m:
+            out.append((int(m.group(1)), float(m.group(2)), float(m.group(3)), float(m.group(4))))
+    return out
+
+
+@pytest.fixture()
+def ml100k_dir(tmp_path, monkeypatch):
+    from ncf_amd import synthetic
+    monkeypatch.chdir(tmp_path)
+    synthetic.write_reference_files(synthetic.make_dataset("ml-100k", seed=0), "data/processed")
+    return tmp_path
+
+
+def test_trainer_matches_reference_script(golden, ml100k_dir):
+    import torch.utils.data as data
+    from ncf_amd.data import NCFData, load_all
+    from ncf_amd.models import NCF
+    from ncf_amd.trainer import Trainer
+    g = golden("G7_script")
+    ref = _parse(g["f8_L3_stdout"])
+    np.random.seed(0)
+    torch.manual_seed(0)
+    train_data, test_data, U, I, mat = load_all()
+    train_ds = NCFData(train_data, I, mat, 4, True)
+    test_ds = NCFData(test_data, I, mat, 0, False)
+    loader = data.DataLoader(test_ds, batch_size=100, shuffle=False, num_workers=0)
+    model = NCF(U, I, 8, 3, 0.0, "NeuMF-end").to("cuda:0")
+    tr = Trainer(model, train_ds, loader, batch_size=256, lr=1e-3, top_k=10)
+    res = tr.fit(2)
+    assert res["parameters"] == 107841
+    for h, (e, l, hr, nd) in zip(tr.history, ref):
+        assert h["epoch"] == e
+        assert abs(h["loss"] - l) <= 1e-3 * l + 1e-4, (tr.history, ref)
+        assert abs(h["hr"] - hr) <= 0.01 and abs(h["ndcg"] - nd) <= 0.01, (tr.history, ref)
+
+
+def test_script_stdout_matches_reference(golden, ml100k_dir):
+    g = golden("G7_script")
+    ref = _parse(g["f8_L3_stdout"])
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "train_neumf.py"), "--epochs", "2",
+                          "--factor_num", "8", "--num_layers", "3", "--seed", "0"],
+                         capture_output=True, text=True, timeout=600, cwd=str(ml100k_dir))
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = _parse(out.stdout.splitlines())
+    assert len(got) == 2, out.stdout
+    for (e1, l1, h1, n1), (e2, l2, h2, n2) in zip(got, ref):
+        assert e1 == e2
+        assert abs(l1 - l2) <= 1e-3 * l2 + 1e-4, (got, ref)
+        assert abs(h1 - h2) <= 0.01 and abs(n1 - n2) <= 0.01, (got, ref)
+    assert "Parameters: 107841" in out.stdout and "--- RESULTS ---" in out.stdout
+    assert os.path.exists(os.path.join(str(ml100k_dir), "results", "models", "NeuMF_end_3l_8f_best.pth"))
