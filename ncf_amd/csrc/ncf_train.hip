@@ -606,13 +606,27 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                                     scr[(4 * g + r) * S_::SCM + 16 * nt + c - DM] = lane_get(acc[nt], r);
                             }
                             item_segments(scr, a, su, si, wr, l, gIg, gf, gq0);
+                            // user half: transpose through the (now free) scratch so each
+                            // atomic wave-instruction adds whole contiguous rows
+                            // (min(DM, 64) floats per row) instead of 4 rows x 64 B
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
-                                const int uu = max(su[wr + 4 * g + r], 0);
 #pragma unroll
                                 for (int nt = 0; nt < DM / 16; ++nt)
-                                    atomicAdd(a.grads + lay.um + (int64_t)uu * DM + 16 * nt + c,
-                                              lane_get(acc[nt], r));
+                                    scr[(4 * g + r) * S_::SCM + 16 * nt + c] = lane_get(acc[nt], r);
+                            }
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            constexpr int RPW = DM >= 64 ? 1 : 64 / DM;  // rows per wave-instruction
+                            constexpr int FPI = DM >= 64 ? 64 : DM;
+#pragma unroll
+                            for (int q0 = 0; q0 < 16; q0 += RPW) {
+                                const int q = q0 + l / FPI;
+                                const int uu = max(su[wr + q], 0);
+#pragma unroll
+                                for (int f0 = 0; f0 < DM; f0 += FPI) {
+                                    const int f = f0 + l % FPI;
+                                    atomicAdd(a.grads + lay.um + (int64_t)uu * DM + f, scr[q * S_::SCM + f]);
+                                }
                             }
                         } else {  // DM == 8: one 16-column tile, lanes c < 8 user, c >= 8 item
 #pragma unroll
