@@ -91,7 +91,7 @@ def setup_engine(config, world, rank, dev, group, global_batch, seed=0):
     from ncf_amd.data import HostSampler, epoch_permutation
     from ncf_amd.engine import TrainEngine
     from ncf_amd.models import NCF
-    import ncf_amd._lib as L
+    from ncf_amd import ops
     shape, f, nl, _ = CONFIGS[config]
     ds = synthetic.make_dataset(shape, seed=seed)
     U, I = ds["user_num"], ds["item_num"]
@@ -107,19 +107,14 @@ def setup_engine(config, world, rank, dev, group, global_batch, seed=0):
     labels = np.concatenate([np.ones(len(pu), np.float32), np.zeros(len(neg), np.float32)])
     model = NCF(U, I, f, nl, 0.0, "NeuMF-end").to(dev)
     perm = epoch_permutation(len(users)).to(dev)
-    u_d, i_d, y_d = (torch.from_numpy(users).to(dev), torch.from_numpy(items).to(dev),
-                     torch.from_numpy(labels).to(dev))
-    us, its, ys = torch.empty_like(u_d), torch.empty_like(i_d), torch.empty_like(y_d)
-    L.check(L.hip().ncf_prepare_epoch(u_d.data_ptr(), i_d.data_ptr(), y_d.data_ptr(), perm.data_ptr(), len(users),
-                                      global_batch, I, us.data_ptr(), its.data_ptr(), ys.data_ptr(),
-                                      L.stream_ptr(dev)), "prepare_epoch")
+    rows_d = torch.from_numpy(ops.pack_rows_host(users, items, labels)).to(dev)  # resident in HBM
+    prep = ops.EpochPrep(dev)
+    stream = prep(rows_d, perm, global_batch, I)
     eng = TrainEngine(model, lr=1e-3, world_size=world, rank=rank, process_group=group)
-    eng.set_epoch_stream(us, its, ys, global_batch)
+    eng.set_epoch_stream(stream, global_batch)
 
-    def prepare():  # per-epoch device work: shuffle + group each batch by item
-        L.check(L.hip().ncf_prepare_epoch(u_d.data_ptr(), i_d.data_ptr(), y_d.data_ptr(), perm.data_ptr(),
-                                          len(users), global_batch, I, us.data_ptr(), its.data_ptr(),
-                                          ys.data_ptr(), L.stream_ptr(dev)), "prepare_epoch")
+    def prepare():  # per-epoch device work: shuffle + group each batch by item (same output buffer)
+        prep(rows_d, perm, global_batch, I)
     eng.prepare_epoch = prepare
     return eng, model, ds, t_sample
 

@@ -21,12 +21,24 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 1
+#define NCF_ABI_VERSION 2
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
 #define NCF_E_ARG (-2)         /* bad pointer / size */
 #define NCF_E_LAUNCH (-3)      /* hipGetLastError() after launch */
+
+/*
+ * Packed interaction row: one uint64 per (user, item, label) sample of the
+ * training stream (datasets.py:57-60 features_fill / labels_fill):
+ *   bits  0..31  user id (int32; -1 marks a padding row, which is skipped)
+ *   bits 32..62  item id
+ *   bit  63      label (1 = positive; the reference labels are 1.0 / 0.0)
+ * 8 bytes per row instead of three 4-byte streams: one load per row in the fused
+ * step and one random gather per row in the epoch shuffle.
+ */
+#define NCF_ROW_PACK(u, i, y) \
+    ((uint64_t)(uint32_t)(u) | ((uint64_t)((uint32_t)(i) & 0x7fffffffu) << 32) | ((uint64_t)((y) != 0) << 63))
 
 /* model_type: src/ncf/models.py:30-33,98-107 */
 #define NCF_MODEL_GMF 0
@@ -83,23 +95,28 @@ int64_t ncf_slab_stride(const ncf_layout *lay);
  * loss.backward() train_neumf.py:114: embedding gathers, GMF product, MLP tower
  * GEMM+bias+ReLU, predict layer, BCE, tower dgrad/wgrad and embedding_dense_backward).
  *
- * Rows: global batch `ctl->batch % ceil(n_total / batch_global)` over the epoch stream
- * users/items/labels[0 .. ctl->n_total), last batch partial (DataLoader
- * drop_last=False); this rank takes rows [rank*ceil(gb/world), ...) of it.
+ * Rows: global batch `ctl->batch % ceil(n_total / batch_global)` of the packed epoch
+ * stream rows[0 .. ctl->n_total) (ncf_prepare_epoch output), last batch partial
+ * (DataLoader drop_last=False); this rank takes rows [rank*ceil(gb/world), ...) of it.
  * grads: dense flat gradient buffer; embedding rows are scatter-added (f32
  * atomics), the tower/predict part is written per workgroup into
  * slab[ncf_slab_rows()][ncf_slab_stride()] (reduce with ncf_reduce_slab).
- * dz_mode NCF_DZ_DLOGIT: `labels` holds dL/dlogit per row instead.
+ * dz_mode NCF_DZ_BCE: the label is bit 63 of the row, `dlogit` is ignored (may be NULL).
+ * dz_mode NCF_DZ_DLOGIT: dlogit[row] holds dL/dlogit per row (same indexing as rows).
  * logits_out (optional, may be NULL): per-row logits of this rank's rows.
  */
-int ncf_train_step(const ncf_layout *lay, const float *params, float *grads,
-                   const int32_t *users, const int32_t *items, const float *labels,
-                   const ncf_step_ctl *ctl, int64_t batch_global, int world, int rank,
-                   int dz_mode, float *slab, float *logits_out, void *stream);
+int ncf_train_step(const ncf_layout *lay, const float *params, float *grads, const uint64_t *rows,
+                   const float *dlogit, const ncf_step_ctl *ctl, int64_t batch_global, int world,
+                   int rank, int dz_mode, float *slab, float *logits_out, void *stream);
 
-/* Forward only (NCF.forward under no_grad, metrics.py:11-12): logits[n]. */
-int ncf_forward(const ncf_layout *lay, const float *params, const int32_t *users,
-                const int32_t *items, int64_t n, float *logits, void *stream);
+/* Forward only (NCF.forward under no_grad, metrics.py:11-12): logits[n] of rows[n]. */
+int ncf_forward(const ncf_layout *lay, const float *params, const uint64_t *rows, int64_t n,
+                float *logits, void *stream);
+
+/* rows_out[k] = NCF_ROW_PACK(users[k], items[k], labels ? labels[k] : 0) (the feature /
+ * label tensors the reference DataLoader yields, datasets.py:72-78). */
+int ncf_pack_rows(const int32_t *users, const int32_t *items, const float *labels, int64_t n,
+                  uint64_t *rows_out, void *stream);
 
 /* grads[tower_begin + j] = sum_w slab[w][j] over a slab row (loss slot included), in a
  * fixed order (bitwise reproducible).  If ctl != NULL, also advances ctl->batch and
@@ -124,22 +141,25 @@ int ncf_sgd_step(float *params, float *grads, const int64_t *ranges, int nranges
                  ncf_step_ctl *ctl, double lr, int64_t loss_slot, float *loss_hist, int64_t hist_len,
                  void *stream);
 
-/* out[k] = src[perm[k]] for the three epoch streams (DataLoader shuffle=True order). */
-int ncf_gather_epoch(const int32_t *users, const int32_t *items, const float *labels,
-                     const int64_t *perm, int64_t n, int32_t *users_out, int32_t *items_out,
-                     float *labels_out, void *stream);
+/* rows_out[k] = rows[perm[k]] (DataLoader shuffle=True order, no grouping). */
+int ncf_gather_epoch(const uint64_t *rows, const int64_t *perm, int64_t n, uint64_t *rows_out,
+                     void *stream);
 
 /*
  * Epoch stream for the fused step: global batch b holds rows perm[b*B .. b*B+cnt)
- * of the unshuffled stream (the DataLoader(shuffle=True) batch membership,
- * train_neumf.py:55,106), written back grouped by item id (counting sort per batch).
- * Order inside a batch does not change the batch gradient; grouping lets the fused
- * step reduce item-side gradients per item before its atomics.  item_num <= ~40k
- * (LDS histogram), else NCF_E_UNSUPPORTED.
+ * of the unshuffled packed stream (the DataLoader(shuffle=True) batch membership,
+ * train_neumf.py:55,106), written back grouped by item id (sort per batch; order
+ * inside an item group is unspecified).  Order inside a batch does not change the
+ * batch gradient; grouping lets the fused step reduce item-side gradients per item
+ * before its atomics.  Three kernels: shuffle + per-batch item histogram, per-batch
+ * scan into item offsets and part boundaries, per-part LDS sort with coalesced writes.
+ * Global batches under 4096 rows are only shuffled (item runs would be ~1 row long).
+ * workspace: device buffer of at least ncf_prepare_epoch_workspace() bytes.
  */
-int ncf_prepare_epoch(const int32_t *users, const int32_t *items, const float *labels,
-                      const int64_t *perm, int64_t n, int64_t batch_global, int item_num,
-                      int32_t *users_out, int32_t *items_out, float *labels_out, void *stream);
+int64_t ncf_prepare_epoch_workspace(int64_t n, int64_t batch_global, int item_num);
+int ncf_prepare_epoch(const uint64_t *rows, const int64_t *perm, int64_t n, int64_t batch_global,
+                      int item_num, uint64_t *rows_out, void *workspace, int64_t workspace_bytes,
+                      void *stream);
 
 /*
  * HR@K / NDCG@K per DataLoader batch (metrics.py:4-25): batches of `batch`

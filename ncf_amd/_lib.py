@@ -28,6 +28,7 @@ NCF_E_ARG = -2
 NCF_E_LAUNCH = -3
 MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
 DZ_BCE, DZ_DLOGIT = 0, 1
+ABI_VERSION = 2  # include/ncf_hip.h NCF_ABI_VERSION
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
 
 c_i64 = ctypes.c_int64
@@ -56,9 +57,10 @@ _HIP_PROTOS = {
     "ncf_supported": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "ncf_layout_init": (ctypes.c_int, [ctypes.c_int] * 5 + [ctypes.POINTER(NcfLayout)]),
     "ncf_slab_rows": (ctypes.c_int, []),
-    "ncf_train_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+    "ncf_train_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
-    "ncf_forward": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "ncf_forward": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "ncf_pack_rows": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "ncf_reduce_slab": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp]),
     "ncf_slab_stride": (c_i64, [ctypes.POINTER(NcfLayout)]),
     "ncf_debug_set_diag": (ctypes.c_int, [ctypes.c_int]),
@@ -68,9 +70,9 @@ _HIP_PROTOS = {
                                      c_i64, c_vp, c_i64, c_vp]),
     "ncf_sgd_step": (ctypes.c_int, [c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.c_int, c_vp, ctypes.c_double,
                                     c_i64, c_vp, c_i64, c_vp]),
-    "ncf_gather_epoch": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
-    "ncf_prepare_epoch": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, ctypes.c_int, c_vp, c_vp, c_vp,
-                                         c_vp]),
+    "ncf_gather_epoch": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "ncf_prepare_epoch_workspace": (c_i64, [c_i64, c_i64, ctypes.c_int]),
+    "ncf_prepare_epoch": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, ctypes.c_int, c_vp, c_vp, c_i64, c_vp]),
     "ncf_hr_ndcg": (ctypes.c_int, [c_vp, c_vp, c_i64, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
 }
 
@@ -107,7 +109,7 @@ def hip():
         with _lock:
             if _hip is None:
                 lib = _load(HIP_LIB_PATH, _HIP_PROTOS, "libncf_hip.so")
-                if lib.ncf_abi_version() != 1:
+                if lib.ncf_abi_version() != ABI_VERSION:
                     raise RuntimeError("libncf_hip.so ABI mismatch; rebuild")
                 _hip = lib
     return _hip

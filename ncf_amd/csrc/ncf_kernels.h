@@ -59,9 +59,8 @@ struct TrainArgs {
     ncf_layout lay;
     const float* params;
     float* grads;
-    const int32_t* users;
-    const int32_t* items;
-    const float* labels;
+    const uint64_t* rows;  // packed rows (NCF_ROW_PACK)
+    const float* dlogit;   // NCF_DZ_DLOGIT: dL/dlogit per row (BCE: aliases rows, unused)
     const ncf_step_ctl* ctl;
     int64_t batch_global;
     int world, rank, dz_mode;
@@ -77,6 +76,7 @@ constexpr int NSTAMP = 64;  // stamps per workgroup
 // Ablation switches for performance diagnosis (ncf_debug_set_diag); results are
 // wrong when any is set.
 constexpr int DIAG_NO_WGRAD = 2;  // skip the weight-gradient MFMAs
+constexpr int DIAG_PREP_DIRECT = 4;  // ncf_prepare_epoch: global-atomic histogram variant (still correct)
 
 struct KernelEntry {
     int mode, F, L;

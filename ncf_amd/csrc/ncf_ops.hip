@@ -160,56 +160,131 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* 
 }
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void gather_epoch_kernel(const int32_t* __restrict__ u, const int32_t* __restrict__ it,
-                                                           const float* __restrict__ y, const int64_t* __restrict__ perm,
-                                                           int64_t n, int32_t* uo, int32_t* io, float* yo) {
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t s = perm[k];
-        uo[k] = u[s];
-        io[k] = it[s];
-        yo[k] = y[s];
-    }
+// Packed rows (include/ncf_hip.h NCF_ROW_PACK): u | item << 32 | label << 63.
+__device__ __forceinline__ int row_item(uint64_t r) { return (int)((r >> 32) & 0x7fffffffu); }
+
+__global__ __launch_bounds__(256) void pack_rows_kernel(const int32_t* __restrict__ u, const int32_t* __restrict__ it,
+                                                        const float* __restrict__ y, int64_t n, uint64_t* __restrict__ out) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        out[k] = NCF_ROW_PACK(u[k], it[k], y ? y[k] : 0.f);
+}
+
+__global__ __launch_bounds__(256) void gather_epoch_kernel(const uint64_t* __restrict__ rows,
+                                                           const int64_t* __restrict__ perm, int64_t n,
+                                                           uint64_t* __restrict__ out) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        out[k] = rows[perm[k]];
 }
 
 // ---------------------------------------------------------------------------
-// Epoch preparation: one workgroup per global batch.  Rows perm[b*B .. b*B+cnt)
-// of the unshuffled stream are the batch (DataLoader shuffle=True membership);
-// they are written back grouped by item (counting sort in LDS).  Row order
-// inside a batch does not change the batch's gradient, it only lets the fused
-// step reduce item-side gradients per item segment before its atomics.
-constexpr int PREP_THREADS = 1024;
-__global__ __launch_bounds__(PREP_THREADS) void prepare_epoch_kernel(
-    const int32_t* __restrict__ users, const int32_t* __restrict__ items, const float* __restrict__ labels,
-    const int64_t* __restrict__ perm, int64_t n, int64_t B, int item_num, int32_t* __restrict__ uo,
-    int32_t* __restrict__ io, float* __restrict__ yo) {
-    extern __shared__ int hist[];  // [item_num] counts -> offsets, then [32] wave partials
-    int* part = hist + ((item_num + 3) & ~3);
-    const int tid = threadIdx.x;
-    const int64_t b0 = (int64_t)blockIdx.x * B;
-    const int cnt = (int)((n - b0) < B ? (n - b0) : B);
-    for (int i = tid; i < item_num; i += PREP_THREADS) hist[i] = 0;
-    __syncthreads();
-    constexpr int U16 = 16;
-    for (int j0 = 0; j0 < cnt; j0 += U16 * PREP_THREADS) {
-        int64_t src[U16];
-        int it[U16];
+// Epoch preparation (ncf_prepare_epoch).  Global batch b is rows perm[b*B ..
+// b*B+cnt) of the unshuffled stream (DataLoader shuffle=True membership); it is
+// written back grouped by item.  Three launches, all HBM/L2-bound byte work:
+//   1. shuffle_hist: shuf[j] = rows[perm[j]] (one random 8-byte gather per row,
+//      coalesced write) and hist[b][item]++ (global atomics, no return).
+//   2. scan_parts: per batch, hist -> exclusive item offsets in place, and the
+//      batch is cut into P parts of ~cnt/P rows at item boundaries: part q owns
+//      the items whose start offset s satisfies floor(s*P/cnt) == q, i.e. a
+//      contiguous item range [I_q, I_q+1) and output region [R_q, R_q+1).
+//   3. sort_part: one workgroup per (batch, part) streams the batch's shuffled
+//      rows (L2-resident: the P parts of a batch run on one XCD), keeps those of
+//      its items, places them by LDS atomics on the item offsets into an LDS
+//      staging buffer and writes its region out contiguously.  Regions or item
+//      ranges too large for LDS fall back to global offsets / direct writes.
+constexpr int SH_THREADS = 256, SH_UNROLL = 8;
+constexpr int SCAN_THREADS = 1024;
+constexpr int SORT_THREADS = 1024, SORT_UNROLL = 8;
+constexpr int STAGE_ROWS = 16384, ITEM_CAP = 6144;
+constexpr int64_t SORT_LDS = (int64_t)STAGE_ROWS * 8 + (int64_t)ITEM_CAP * 4;
+constexpr int PART_ROWS = 8192;  // nominal rows per part
+constexpr int64_t PREP_GROUP_MIN = 4096;  // smaller global batches are shuffled, not grouped
+
+__global__ __launch_bounds__(SH_THREADS) void shuffle_hist_kernel(const uint64_t* __restrict__ rows,
+                                                                  const int64_t* __restrict__ perm, int64_t n,
+                                                                  int64_t B, int item_num, uint64_t* __restrict__ shuf,
+                                                                  int* __restrict__ hist) {
+    const int64_t j0 = (int64_t)blockIdx.x * (SH_THREADS * SH_UNROLL) + threadIdx.x;
+    int64_t src[SH_UNROLL];
+    uint64_t r[SH_UNROLL];
 #pragma unroll
-        for (int k = 0; k < U16; ++k) {
-            const int j = j0 + k * PREP_THREADS + tid;
-            src[k] = j < cnt ? perm[b0 + j] : -1;
+    for (int k = 0; k < SH_UNROLL; ++k) {
+        const int64_t j = j0 + k * SH_THREADS;
+        const int64_t s = j < n ? perm[j] : 0;
+        src[k] = s < 0 ? 0 : (s >= n ? n - 1 : s);
+    }
+#pragma unroll
+    for (int k = 0; k < SH_UNROLL; ++k) r[k] = rows[src[k]];
+#pragma unroll
+    for (int k = 0; k < SH_UNROLL; ++k) {
+        const int64_t j = j0 + k * SH_THREADS;
+        if (j < n) {
+            shuf[j] = r[k];
+            atomicAdd(hist + (j / B) * item_num + min(row_item(r[k]), item_num - 1), 1);
+        }
+    }
+}
+
+// LDS-privatised variant for large batches: block (b, c) covers rows
+// [b*B + c*SH_CHUNK, ...) of batch b only, counts its items in LDS and adds each
+// non-zero bin to hist once -- no same-address atomic chains on hot items.
+constexpr int SH2_THREADS = 1024, SH2_UNROLL = 8, SH_CHUNK = 16384;
+constexpr int SH2_MAX_ITEMS = 32768;
+__global__ __launch_bounds__(SH2_THREADS) void shuffle_hist_lds_kernel(const uint64_t* __restrict__ rows,
+                                                                      const int64_t* __restrict__ perm, int64_t n,
+                                                                      int64_t B, int item_num, int chunks,
+                                                                      uint64_t* __restrict__ shuf,
+                                                                      int* __restrict__ hist) {
+    extern __shared__ int lh[];  // [item_num]
+    const int tid = threadIdx.x;
+    const int64_t b = blockIdx.x / chunks;
+    const int c = blockIdx.x - (int)(b * chunks);
+    const int64_t b0 = b * B;
+    const int cnt = (int)((n - b0) < B ? (n - b0) : B);
+    const int r0 = c * SH_CHUNK, r1 = min(cnt, r0 + SH_CHUNK);
+    if (r0 >= r1) return;  // block-uniform
+    for (int i = tid; i < item_num; i += SH2_THREADS) lh[i] = 0;
+    __syncthreads();
+    for (int q0 = r0; q0 < r1; q0 += SH2_UNROLL * SH2_THREADS) {
+        int64_t src[SH2_UNROLL];
+        uint64_t r[SH2_UNROLL];
+#pragma unroll
+        for (int k = 0; k < SH2_UNROLL; ++k) {
+            const int q = q0 + k * SH2_THREADS + tid;
+            const int64_t s = q < r1 ? perm[b0 + q] : 0;
+            src[k] = s < 0 ? 0 : (s >= n ? n - 1 : s);
         }
 #pragma unroll
-        for (int k = 0; k < U16; ++k) it[k] = items[src[k] < 0 ? 0 : src[k]];
+        for (int k = 0; k < SH2_UNROLL; ++k) r[k] = rows[src[k]];
 #pragma unroll
-        for (int k = 0; k < U16; ++k)
-            if (src[k] >= 0) atomicAdd(&hist[min(max(it[k], 0), item_num - 1)], 1);
+        for (int k = 0; k < SH2_UNROLL; ++k) {
+            const int q = q0 + k * SH2_THREADS + tid;
+            if (q < r1) {
+                shuf[b0 + q] = r[k];
+                atomicAdd(&lh[min(row_item(r[k]), item_num - 1)], 1);
+            }
+        }
     }
     __syncthreads();
-    // exclusive scan: contiguous chunk per thread, wave scan, then across waves
-    const int per = (item_num + PREP_THREADS - 1) / PREP_THREADS;
-    const int i0 = tid * per, i1 = min(item_num, i0 + per);
+    int* h = hist + b * item_num;
+    for (int i = tid; i < item_num; i += SH2_THREADS) {
+        const int v = lh[i];
+        if (v) atomicAdd(h + i, v);
+    }
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_parts_kernel(int* __restrict__ hist, int64_t n, int64_t B,
+                                                                  int item_num, int P, int* __restrict__ parts) {
+    __shared__ int wpart[SCAN_THREADS / 64];
+    const int tid = threadIdx.x;
+    const int64_t b = blockIdx.x;
+    const int64_t b0 = b * B;
+    const int cnt = (int)((n - b0) < B ? (n - b0) : B);
+    int* h = hist + b * item_num;
+    int* pb = parts + b * (P + 1) * 2;
+    const int per = (item_num + SCAN_THREADS - 1) / SCAN_THREADS;
+    const int i0 = min(item_num, tid * per), i1 = min(item_num, i0 + per);
     int tot = 0;
-    for (int i = i0; i < i1; ++i) tot += hist[i];
+    for (int i = i0; i < i1; ++i) tot += h[i];
     const int lane = tid & 63, wv = tid >> 6;
     int incl = tot;
 #pragma unroll
@@ -217,51 +292,104 @@ __global__ __launch_bounds__(PREP_THREADS) void prepare_epoch_kernel(
         const int y = __shfl_up(incl, o, 64);
         if (lane >= o) incl += y;
     }
-    if (lane == 63) part[wv] = incl;
+    if (lane == 63) wpart[wv] = incl;
     __syncthreads();
     if (tid == 0) {
         int acc = 0;
-        for (int q = 0; q < PREP_THREADS / 64; ++q) {
-            const int v = part[q];
-            part[q] = acc;
+        for (int q = 0; q < SCAN_THREADS / 64; ++q) {
+            const int v = wpart[q];
+            wpart[q] = acc;
             acc += v;
         }
+        pb[0] = 0;
+        pb[1] = 0;
     }
     __syncthreads();
-    int run = part[wv] + incl - tot;
+    int s = wpart[wv] + incl - tot;
+    // first part whose threshold T_q = ceil(q*cnt/P) lies above s
+    int q = (int)((int64_t)s * P / cnt) + 1;
     for (int i = i0; i < i1; ++i) {
-        const int v = hist[i];
-        hist[i] = run;
-        run += v;
+        const int c = h[i];
+        h[i] = s;
+        const int sn = s + c;
+        while (q <= P) {
+            const int T = (int)(((int64_t)q * cnt + P - 1) / P);
+            if (T > sn) break;
+            pb[2 * q] = i + 1;  // items [.., i] end before part q; item i + 1 starts it
+            pb[2 * q + 1] = sn;
+            ++q;
+        }
+        s = sn;
     }
+}
+
+__global__ __launch_bounds__(SORT_THREADS) void sort_part_kernel(const uint64_t* __restrict__ shuf,
+                                                                 int* __restrict__ hist, const int* __restrict__ parts,
+                                                                 int64_t n, int64_t B, int item_num, int P, int64_t nb,
+                                                                 uint64_t* __restrict__ out) {
+    extern __shared__ uint64_t stg[];                       // [STAGE_ROWS]
+    int* loff = reinterpret_cast<int*>(stg + STAGE_ROWS);  // [ITEM_CAP]
+    const int tid = threadIdx.x;
+    const int x = blockIdx.x;
+    int64_t b;
+    int o;
+    if (P >= 8) {  // the P parts of a batch share one XCD (blocks are dealt round-robin to the 8 XCDs)
+        const int xcd = x & 7, k = x >> 3;
+        b = (int64_t)(k / P) * 8 + xcd;
+        o = k % P;
+    } else {
+        b = x / P;
+        o = x % P;
+    }
+    if (b >= nb) return;
+    const int64_t b0 = b * B;
+    const int cnt = (int)((n - b0) < B ? (n - b0) : B);
+    const int* pb = parts + b * (P + 1) * 2;
+    const int ilo = pb[2 * o], rlo = pb[2 * o + 1], ihi = pb[2 * o + 2], rhi = pb[2 * o + 3];
+    const int nrows = rhi - rlo, nit = ihi - ilo;
+    if (nrows <= 0) return;  // block-uniform
+    int* h = hist + b * item_num;
+    const bool stage = nrows <= STAGE_ROWS, local = nit <= ITEM_CAP;
+    if (local)
+        for (int e = tid; e < nit; e += SORT_THREADS) loff[e] = h[ilo + e] - rlo;
     __syncthreads();
-    for (int j0 = 0; j0 < cnt; j0 += U16 * PREP_THREADS) {
-        int64_t src[U16];
-        int it[U16], us[U16];
-        float ys[U16];
+    const uint64_t* sb = shuf + b0;
+    uint64_t* ob = out + b0 + rlo;
+    for (int j0 = 0; j0 < cnt; j0 += SORT_UNROLL * SORT_THREADS) {
+        uint64_t r[SORT_UNROLL];
 #pragma unroll
-        for (int k = 0; k < U16; ++k) {
-            const int j = j0 + k * PREP_THREADS + tid;
-            src[k] = j < cnt ? perm[b0 + j] : -1;
+        for (int k = 0; k < SORT_UNROLL; ++k) {
+            const int j = j0 + k * SORT_THREADS + tid;
+            r[k] = sb[j < cnt ? j : 0];
         }
 #pragma unroll
-        for (int k = 0; k < U16; ++k) {
-            const int64_t sk = src[k] < 0 ? 0 : src[k];
-            it[k] = items[sk];
-            us[k] = users[sk];
-            ys[k] = labels[sk];
-        }
-#pragma unroll
-        for (int k = 0; k < U16; ++k) {
-            if (src[k] >= 0) {
-                const int pos = atomicAdd(&hist[min(max(it[k], 0), item_num - 1)], 1);
-                uo[b0 + pos] = us[k];
-                io[b0 + pos] = it[k];
-                yo[b0 + pos] = ys[k];
+        for (int k = 0; k < SORT_UNROLL; ++k) {
+            const int j = j0 + k * SORT_THREADS + tid;
+            const int it = min(row_item(r[k]), item_num - 1);
+            if (j < cnt && it >= ilo && it < ihi) {
+                const int pos = local ? atomicAdd(&loff[it - ilo], 1) : atomicAdd(&h[it], 1) - rlo;
+                if (stage)
+                    stg[pos] = r[k];
+                else
+                    ob[pos] = r[k];
             }
         }
     }
+    if (stage) {
+        __syncthreads();
+        for (int e = tid; e < nrows; e += SORT_THREADS) ob[e] = stg[e];
+    }
 }
+
+static int prep_parts(int64_t B) {
+    if (B <= PART_ROWS) return 1;
+    const int64_t need = (B + PART_ROWS - 1) / PART_ROWS;
+    int P = 1;
+    while (P < need) P <<= 1;
+    return P;
+}
+
+static int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
 // ---------------------------------------------------------------------------
 // HR / NDCG per batch.  One wave per batch; the batch's logits staged in LDS.
@@ -418,12 +546,13 @@ int ncf_supported(int mode, int F, int L) {
     return train_lds_floats(e, &lay) * 4 <= LDS_LIMIT_BYTES ? 1 : 0;
 }
 
-int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, const int32_t* users,
-                   const int32_t* items, const float* labels, const ncf_step_ctl* ctl, int64_t batch_global,
-                   int world, int rank, int dz_mode, float* slab, float* logits_out, void* stream) {
-    if (!lay || !params || !grads || !users || !items || !labels || !ctl || !slab) return NCF_E_ARG;
+int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
+                   const float* dlogit, const ncf_step_ctl* ctl, int64_t batch_global, int world, int rank,
+                   int dz_mode, float* slab, float* logits_out, void* stream) {
+    if (!lay || !params || !grads || !rows || !ctl || !slab) return NCF_E_ARG;
     if (batch_global <= 0 || world < 1 || rank < 0 || rank >= world) return NCF_E_ARG;
     if (dz_mode != NCF_DZ_BCE && dz_mode != NCF_DZ_DLOGIT) return NCF_E_ARG;
+    if (dz_mode == NCF_DZ_DLOGIT && !dlogit) return NCF_E_ARG;
     const KernelEntry* e = find_entry(lay->model_type, lay->factor_num, lay->num_layers);
     if (!e) return NCF_E_UNSUPPORTED;
     const int64_t lds = train_lds_floats(e, lay) * 4;
@@ -434,9 +563,9 @@ int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, con
     a.lay = *lay;
     a.params = params;
     a.grads = grads;
-    a.users = users;
-    a.items = items;
-    a.labels = labels;
+    a.rows = rows;
+    // BCE mode: point dlogit at the rows so the per-row load stays unconditional
+    a.dlogit = dz_mode == NCF_DZ_DLOGIT ? dlogit : reinterpret_cast<const float*>(rows);
     a.ctl = ctl;
     a.batch_global = batch_global;
     a.world = world;
@@ -453,9 +582,9 @@ int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, con
     return launch_status();
 }
 
-int ncf_forward(const ncf_layout* lay, const float* params, const int32_t* users, const int32_t* items, int64_t n,
-                float* logits, void* stream) {
-    if (!lay || !params || !users || !items || !logits || n < 0) return NCF_E_ARG;
+int ncf_forward(const ncf_layout* lay, const float* params, const uint64_t* rows, int64_t n, float* logits,
+                void* stream) {
+    if (!lay || !params || !rows || !logits || n < 0) return NCF_E_ARG;
     if (n == 0) return NCF_OK;
     const KernelEntry* e = find_entry(lay->model_type, lay->factor_num, lay->num_layers);
     if (!e) return NCF_E_UNSUPPORTED;
@@ -466,8 +595,7 @@ int ncf_forward(const ncf_layout* lay, const float* params, const int32_t* users
     memset(&a, 0, sizeof(a));
     a.lay = *lay;
     a.params = params;
-    a.users = users;
-    a.items = items;
+    a.rows = rows;
     a.logits_out = logits;
     a.fwd_n = n;
     a.world = 1;
@@ -522,31 +650,71 @@ int ncf_sgd_step(float* params, float* grads, const int64_t* ranges, int nranges
     return launch_status();
 }
 
-int ncf_gather_epoch(const int32_t* users, const int32_t* items, const float* labels, const int64_t* perm, int64_t n,
-                     int32_t* users_out, int32_t* items_out, float* labels_out, void* stream) {
-    if (!users || !items || !labels || !perm || !users_out || !items_out || !labels_out || n < 0) return NCF_E_ARG;
+int ncf_pack_rows(const int32_t* users, const int32_t* items, const float* labels, int64_t n, uint64_t* rows_out,
+                  void* stream) {
+    if (!users || !items || !rows_out || n < 0) return NCF_E_ARG;
     if (n == 0) return NCF_OK;
     int64_t grid = (n + 255) / 256;
     if (grid > 4096) grid = 4096;
-    hipLaunchKernelGGL(gather_epoch_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, users, items, labels,
-                       perm, n, users_out, items_out, labels_out);
+    hipLaunchKernelGGL(pack_rows_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, users, items, labels, n,
+                       rows_out);
     return launch_status();
 }
 
-int ncf_prepare_epoch(const int32_t* users, const int32_t* items, const float* labels, const int64_t* perm,
-                      int64_t n, int64_t batch_global, int item_num, int32_t* users_out, int32_t* items_out,
-                      float* labels_out, void* stream) {
-    if (!users || !items || !labels || !perm || !users_out || !items_out || !labels_out || n < 0 ||
-        batch_global <= 0 || item_num <= 0)
-        return NCF_E_ARG;
+int ncf_gather_epoch(const uint64_t* rows, const int64_t* perm, int64_t n, uint64_t* rows_out, void* stream) {
+    if (!rows || !perm || !rows_out || n < 0) return NCF_E_ARG;
     if (n == 0) return NCF_OK;
-    const int64_t lds = (int64_t)(((item_num + 3) & ~3) + 32) * 4;
-    if (lds > LDS_LIMIT_BYTES) return NCF_E_UNSUPPORTED;
-    if (ensure_lds(reinterpret_cast<const void*>(&prepare_epoch_kernel), lds) != NCF_OK) return NCF_E_LAUNCH;
+    int64_t grid = (n + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(gather_epoch_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, rows, perm, n,
+                       rows_out);
+    return launch_status();
+}
+
+int64_t ncf_prepare_epoch_workspace(int64_t n, int64_t batch_global, int item_num) {
+    if (n < 0 || batch_global <= 0 || item_num <= 0) return -1;
     const int64_t nb = (n + batch_global - 1) / batch_global;
-    hipLaunchKernelGGL(prepare_epoch_kernel, dim3((unsigned)nb), dim3(PREP_THREADS), (size_t)lds,
-                       (hipStream_t)stream, users, items, labels, perm, n, batch_global, item_num, users_out,
-                       items_out, labels_out);
+    const int P = prep_parts(batch_global);
+    return al256(n * 8) + al256(nb * item_num * 4) + al256(nb * (P + 1) * 2 * 4);
+}
+
+int ncf_prepare_epoch(const uint64_t* rows, const int64_t* perm, int64_t n, int64_t batch_global, int item_num,
+                      uint64_t* rows_out, void* workspace, int64_t workspace_bytes, void* stream) {
+    if (!rows || !perm || !rows_out || !workspace || n < 0 || batch_global <= 0 || item_num <= 0) return NCF_E_ARG;
+    if (batch_global > 0x7fffffff) return NCF_E_ARG;
+    if (workspace_bytes < ncf_prepare_epoch_workspace(n, batch_global, item_num)) return NCF_E_ARG;
+    if (n == 0) return NCF_OK;
+    const int64_t nb = (n + batch_global - 1) / batch_global;
+    const int P = prep_parts(batch_global);
+    char* ws = static_cast<char*>(workspace);
+    uint64_t* shuf = reinterpret_cast<uint64_t*>(ws);
+    int* hist = reinterpret_cast<int*>(ws + al256(n * 8));
+    int* parts = reinterpret_cast<int*>(ws + al256(n * 8) + al256(nb * item_num * 4));
+    hipStream_t st = (hipStream_t)stream;
+    if (batch_global < PREP_GROUP_MIN) {  // small batches: item runs ~1 row, grouping buys nothing
+        int64_t grid = (n + 255) / 256;
+        if (grid > 8192) grid = 8192;
+        hipLaunchKernelGGL(gather_epoch_kernel, dim3((int)grid), dim3(256), 0, st, rows, perm, n, rows_out);
+        return launch_status();
+    }
+    if (hipMemsetAsync(hist, 0, (size_t)(nb * item_num * 4), st) != hipSuccess) return NCF_E_LAUNCH;
+    if (item_num <= SH2_MAX_ITEMS && !(g_diag & DIAG_PREP_DIRECT)) {
+        const int chunks = (int)((batch_global + SH_CHUNK - 1) / SH_CHUNK);
+        const int64_t lds = (int64_t)item_num * 4;
+        if (ensure_lds(reinterpret_cast<const void*>(&shuffle_hist_lds_kernel), lds) != NCF_OK) return NCF_E_LAUNCH;
+        hipLaunchKernelGGL(shuffle_hist_lds_kernel, dim3((unsigned)(nb * chunks)), dim3(SH2_THREADS), (size_t)lds, st,
+                           rows, perm, n, batch_global, item_num, chunks, shuf, hist);
+    } else {
+        const int64_t g1 = (n + SH_THREADS * SH_UNROLL - 1) / (SH_THREADS * SH_UNROLL);
+        hipLaunchKernelGGL(shuffle_hist_kernel, dim3((unsigned)g1), dim3(SH_THREADS), 0, st, rows, perm, n,
+                           batch_global, item_num, shuf, hist);
+    }
+    hipLaunchKernelGGL(scan_parts_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, st, hist, n, batch_global,
+                       item_num, P, parts);
+    if (ensure_lds(reinterpret_cast<const void*>(&sort_part_kernel), SORT_LDS) != NCF_OK) return NCF_E_LAUNCH;
+    const int64_t g3 = P >= 8 ? ((nb + 7) / 8) * 8 * P : nb * P;
+    hipLaunchKernelGGL(sort_part_kernel, dim3((unsigned)g3), dim3(SORT_THREADS), (size_t)SORT_LDS, st, shuf, hist,
+                       parts, n, batch_global, item_num, P, nb, rows_out);
     return launch_status();
 }
 

@@ -122,16 +122,20 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     const int64_t ntiles = (nloc + TILE_ROWS - 1) / TILE_ROWS;
     stamp(a, 0);
 
-    // Index prefetch: every thread issues the same three loads (clamped row), so
-    // the vector-memory stream is straight-line and hipcc can count vmcnt waits
+    // Row prefetch: every thread issues the same loads (clamped row), so the
+    // vector-memory stream is straight-line and hipcc can count vmcnt waits
     // exactly instead of draining everything at a branch merge.
     auto load_idx = [&](int64_t row0, int& u, int& it, float& y) {
         const int64_t r = row0 + (tid & (TILE_ROWS - 1));
         const bool ok = r < nloc;
         const int64_t rc = base + (ok ? r : 0);
-        u = a.users[rc];
-        it = a.items[rc];
-        if constexpr (!FWD_ONLY) y = a.labels[rc];  // forward launches carry no labels
+        const uint64_t pr = a.rows[rc];
+        u = (int)(uint32_t)pr;
+        it = (int)((pr >> 32) & 0x7fffffffu);
+        if constexpr (!FWD_ONLY) {  // forward launches carry no labels
+            const float dl = a.dlogit[rc];
+            y = a.dz_mode == NCF_DZ_DLOGIT ? dl : (float)(uint32_t)(pr >> 63);
+        }
         if (!ok) u = it = -1;
     };
     int nu = -1, ni = -1;

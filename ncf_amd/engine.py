@@ -71,22 +71,20 @@ class TrainEngine:
         self._ranges = (ctypes.c_int64 * (2 * len(rng)))(*[x for r in rng for x in r])
         self._nranges = len(rng)
         self.loss_hist = torch.zeros(max_batches, dtype=torch.float32, device=dev)
-        self.users = self.items = self.labels = None
+        self.rows = None
         self.n_total = 0
         self.batch_size = None
         self._graph = None
         self._graph_key = None
 
     # ------------------------------------------------------------------ data
-    def set_epoch_stream(self, users_i32, items_i32, labels_f32, batch_size):
-        """Device tensors already in training (shuffled) order."""
-        assert users_i32.dtype == torch.int32 and items_i32.dtype == torch.int32
-        assert labels_f32.dtype == torch.float32
-        assert users_i32.is_contiguous() and items_i32.is_contiguous() and labels_f32.is_contiguous()
-        n = users_i32.numel()
-        if items_i32.numel() != n or labels_f32.numel() != n:
-            raise ValueError("epoch stream arrays must have equal length")
-        self.users, self.items, self.labels = users_i32, items_i32, labels_f32
+    def set_epoch_stream(self, rows, batch_size):
+        """Packed int64 rows (ops.pack_rows / ncf_prepare_epoch output) already in
+        training order: batch b is rows[b*batch_size, ...)."""
+        if rows.dtype != torch.int64 or not rows.is_contiguous() or rows.device != self.device:
+            raise ValueError("epoch stream: contiguous int64 packed rows on the engine's device")
+        n = rows.numel()
+        self.rows = rows
         self.n_total = n
         if self.batch_size != batch_size:
             self._graph = None
@@ -104,8 +102,8 @@ class TrainEngine:
         st = L.stream_ptr(self.device)
         lib = L.hip()
         lay = ctypes.byref(self.lay)
-        L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.users.data_ptr(),
-                                   self.items.data_ptr(), self.labels.data_ptr(), self.ctl.data_ptr(),
+        L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.rows.data_ptr(),
+                                   None, self.ctl.data_ptr(),
                                    self.batch_size, self.world_size, self.rank, L.DZ_BCE,
                                    self.slab.data_ptr(), None, st), "ncf_train_step")
         L.check(lib.ncf_reduce_slab(lay, self.slab.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(), st), "ncf_reduce_slab")
@@ -137,8 +135,8 @@ class TrainEngine:
         for _ in range(n_steps):
             e = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
             e[0].record(st)
-            L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.users.data_ptr(),
-                                       self.items.data_ptr(), self.labels.data_ptr(), self.ctl.data_ptr(),
+            L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.rows.data_ptr(),
+                                       None, self.ctl.data_ptr(),
                                        self.batch_size, self.world_size, self.rank, L.DZ_BCE,
                                        self.slab.data_ptr(), None, sp), "ncf_train_step")
             e[1].record(st)
@@ -180,7 +178,7 @@ class TrainEngine:
                 self._step_body()
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._graph = g
-        self._graph_key = (self.batch_size, self.n_total, self.users.data_ptr())
+        self._graph_key = (self.batch_size, self.n_total, self.rows.data_ptr())
         return g
 
     def run(self, n_steps, use_graph=True):
@@ -189,7 +187,7 @@ class TrainEngine:
             for _ in range(n_steps):
                 self._step_body()
             return
-        key = (self.batch_size, self.n_total, self.users.data_ptr())
+        key = (self.batch_size, self.n_total, self.rows.data_ptr())
         done = 0
         if self._graph is None or self._graph_key != key:
             # eager first step also sets kernel attributes outside the capture

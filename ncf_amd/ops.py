@@ -13,6 +13,7 @@ module's ``state_dict`` / stock optimizers keep working.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import _lib as L
@@ -72,24 +73,71 @@ def _as_i32(x, dev):
     return x.contiguous()
 
 
-def forward_logits(flat, lay, users_i32, items_i32, out=None):
+def pack_rows(users_i32, items_i32, labels_f32=None, out=None):
+    """Packed uint64 rows (stored as int64): user | item << 32 | (label != 0) << 63
+    (include/ncf_hip.h NCF_ROW_PACK), built on the device by ncf_pack_rows."""
     n = users_i32.numel()
+    dev = users_i32.device
+    if items_i32.numel() != n or (labels_f32 is not None and labels_f32.numel() != n):
+        raise ValueError("users/items/labels must have equal length")
     if out is None:
-        out = torch.empty(n, dtype=torch.float32, device=flat.device)
-    L.check(L.hip().ncf_forward(L.ctypes.byref(lay), flat.data_ptr(), users_i32.data_ptr(),
-                                items_i32.data_ptr(), n, out.data_ptr(), L.stream_ptr(flat.device)),
-            "ncf_forward")
+        out = torch.empty(n, dtype=torch.int64, device=dev)
+    L.check(L.hip().ncf_pack_rows(users_i32.data_ptr(), items_i32.data_ptr(),
+                                  None if labels_f32 is None else labels_f32.data_ptr(), n, out.data_ptr(),
+                                  L.stream_ptr(dev)), "ncf_pack_rows")
     return out
 
 
-def fused_backward(flat, lay, users_i32, items_i32, dlogit, gflat, slab, ctl):
+def pack_rows_host(users, items, labels=None):
+    """Host-side NCF_ROW_PACK of numpy arrays -> int64 numpy array."""
+    r = np.asarray(users).astype(np.int64) & 0xFFFFFFFF
+    r |= (np.asarray(items).astype(np.int64) & 0x7FFFFFFF) << 32
+    if labels is not None:
+        r |= (np.asarray(labels) != 0).astype(np.int64) << 63
+    return r
+
+
+class EpochPrep:
+    """ncf_prepare_epoch with its device workspace kept between epochs (stable
+    pointers, so the output can feed a captured step graph)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.ws = None
+        self.out = None
+
+    def __call__(self, rows, perm, batch_size, item_num):
+        n = rows.numel()
+        need = int(L.hip().ncf_prepare_epoch_workspace(n, int(batch_size), int(item_num)))
+        if need < 0:
+            raise ValueError("bad ncf_prepare_epoch sizes")
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        if self.out is None or self.out.numel() != n:
+            self.out = torch.empty(n, dtype=torch.int64, device=self.device)
+        L.check(L.hip().ncf_prepare_epoch(rows.data_ptr(), perm.data_ptr(), n, int(batch_size), int(item_num),
+                                          self.out.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
+                                          L.stream_ptr(self.device)), "ncf_prepare_epoch")
+        return self.out
+
+
+def forward_logits(flat, lay, rows, out=None):
+    n = rows.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=flat.device)
+    L.check(L.hip().ncf_forward(L.ctypes.byref(lay), flat.data_ptr(), rows.data_ptr(), n, out.data_ptr(),
+                                L.stream_ptr(flat.device)), "ncf_forward")
+    return out
+
+
+def fused_backward(flat, lay, rows, dlogit, gflat, slab, ctl):
     """grads of sum_i dlogit[i] * logit[i] into gflat (zero-initialised)."""
-    n = users_i32.numel()
+    n = rows.numel()
     dev = flat.device
     st = L.stream_ptr(dev)
-    L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), users_i32.data_ptr(),
-                                   items_i32.data_ptr(), dlogit.data_ptr(), ctl.data_ptr(), int(n), 1, 0,
-                                   L.DZ_DLOGIT, slab.data_ptr(), None, st), "ncf_train_step")
+    L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
+                                   dlogit.data_ptr(), ctl.data_ptr(), int(n), 1, 0, L.DZ_DLOGIT,
+                                   slab.data_ptr(), None, st), "ncf_train_step")
     L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st),
             "ncf_reduce_slab")
 
@@ -105,28 +153,28 @@ def new_ctl(n_total, dev, batch=0, adam_t=0):
 
 class _NCFFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, users, items, model, *params):
+    def forward(ctx, rows, model, *params):
         flat, lay = model._ncf_flat, model._ncf_layout
-        logits = forward_logits(flat, lay, users, items)
+        logits = forward_logits(flat, lay, rows)
         ctx.model = model
-        ctx.save_for_backward(users, items)
+        ctx.save_for_backward(rows)
         return logits
 
     @staticmethod
     def backward(ctx, grad_out):
-        users, items = ctx.saved_tensors
+        (rows,) = ctx.saved_tensors
         model = ctx.model
         flat, lay = model._ncf_flat, model._ncf_layout
         dev = flat.device
         gflat = torch.zeros(int(lay.total), dtype=torch.float32, device=dev)
         slab = new_slab(lay, dev)
-        ctl = new_ctl(users.numel(), dev)
+        ctl = new_ctl(rows.numel(), dev)
         dlogit = grad_out.contiguous().to(torch.float32)
-        fused_backward(flat, lay, users, items, dlogit, gflat, slab, ctl)
+        fused_backward(flat, lay, rows, dlogit, gflat, slab, ctl)
         grads = []
         for (p, off), act in zip(_segments(model, lay), active_mask(model)):
             grads.append(gflat[off:off + p.numel()].view_as(p) if act and p.requires_grad else None)
-        return (None, None, None, *grads)
+        return (None, None, *grads)
 
 
 def ncf_forward(model, user, item):
@@ -134,6 +182,15 @@ def ncf_forward(model, user, item):
     dev = flat.device
     u = _as_i32(user, dev).view(-1)
     i = _as_i32(item, dev).view(-1)
+    if u.numel() != i.numel():
+        raise ValueError("user and item must have the same number of elements")
+    if u.numel():
+        # nn.Embedding raises on an out-of-range id (models.py:98-103); the kernel
+        # does not bound-check its gathers, so check here (one host sync).
+        lo_hi = torch.stack([u.min(), u.max(), i.min(), i.max()]).tolist()
+        if lo_hi[0] < 0 or lo_hi[1] >= model.user_num or lo_hi[2] < 0 or lo_hi[3] >= model.item_num:
+            raise IndexError("index out of range in self")
+    rows = pack_rows(u, i)
     if torch.is_grad_enabled() and any(p.requires_grad for p in model.ordered_params()):
-        return _NCFFunction.apply(u, i, model, *model.ordered_params())
-    return forward_logits(flat, lay, u, i)
+        return _NCFFunction.apply(rows, model, *model.ordered_params())
+    return forward_logits(flat, lay, rows)

@@ -26,7 +26,7 @@ import time
 import numpy as np
 import torch
 
-from . import _lib as L
+from . import ops
 from .data import NCFData, consume_test_pass, epoch_permutation
 from .engine import TrainEngine
 from .metrics import evaluate_arrays
@@ -63,19 +63,12 @@ class Trainer:
         u, i, y = self.ds.arrays()
         n = len(u)
         perm = epoch_permutation(n).to(self.device)
-        dev = self.device
-        if getattr(self, "_bufs", None) is None or self._bufs[0].numel() != n:
-            # persistent buffers: stable pointers keep the captured step graph valid
-            self._bufs = [torch.empty(n, dtype=t, device=dev)
-                          for t in (torch.int32, torch.int32, torch.float32) * 2]
-        u_d, i_d, y_d, us, its, ys = self._bufs
-        u_d.copy_(torch.from_numpy(np.ascontiguousarray(u, dtype=np.int32)))
-        i_d.copy_(torch.from_numpy(np.ascontiguousarray(i, dtype=np.int32)))
-        y_d.copy_(torch.from_numpy(np.ascontiguousarray(y, dtype=np.float32)))
-        L.check(L.hip().ncf_prepare_epoch(u_d.data_ptr(), i_d.data_ptr(), y_d.data_ptr(), perm.data_ptr(), n,
-                                          self.batch_size, int(self.model.item_num), us.data_ptr(),
-                                          its.data_ptr(), ys.data_ptr(), L.stream_ptr(dev)), "ncf_prepare_epoch")
-        return us, its, ys
+        if getattr(self, "_rows", None) is None or self._rows.numel() != n:
+            self._rows = torch.empty(n, dtype=torch.int64, device=self.device)
+            self._prep = ops.EpochPrep(self.device)
+        # packed on the host (one int64 per row), one upload, shuffle+group on the device
+        self._rows.copy_(torch.from_numpy(ops.pack_rows_host(u, i, y)))
+        return self._prep(self._rows, perm, self.batch_size, int(self.model.item_num))
 
     def _test_arrays(self):
         if self._test is None:
@@ -105,8 +98,8 @@ class Trainer:
         return evaluate_arrays(self.model, u, i, bs, k)
 
     def train_epoch(self):
-        us, its, ys = self._epoch_stream()
-        self.engine.set_epoch_stream(us, its, ys, self.batch_size)
+        rows = self._epoch_stream()
+        self.engine.set_epoch_stream(rows, self.batch_size)
         self.engine.run(self.engine.num_batches, use_graph=self.use_graph)
         return float(np.mean(self.engine.epoch_losses()))
 

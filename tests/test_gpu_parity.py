@@ -85,7 +85,8 @@ def _stream(eng, users, items, labels, bs):
     u = torch.as_tensor(np.asarray(users).reshape(-1), dtype=torch.int32, device=DEV).contiguous()
     i = torch.as_tensor(np.asarray(items).reshape(-1), dtype=torch.int32, device=DEV).contiguous()
     y = torch.as_tensor(np.asarray(labels).reshape(-1), dtype=torch.float32, device=DEV).contiguous()
-    eng.set_epoch_stream(u, i, y, bs)
+    from ncf_amd import ops
+    eng.set_epoch_stream(ops.pack_rows(u, i, y), bs)
 
 
 @pytest.mark.parametrize("mt,opt", [("NeuMF-end", "adam"), ("GMF", "adam"), ("MLP", "adam"), ("NeuMF-end", "sgd")])
@@ -126,8 +127,9 @@ def test_one_step_grads_vs_oracle(cfg):
     y = torch.as_tensor(labels, dtype=torch.float32, device=DEV)
     logits = torch.empty(B, device=DEV)
     st = L.stream_ptr()
-    L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), u.data_ptr(),
-                                   it.data_ptr(), y.data_ptr(), ctl.data_ptr(), B, 1, 0, L.DZ_BCE,
+    rows = ops.pack_rows(u, it, y)
+    L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
+                                   None, ctl.data_ptr(), B, 1, 0, L.DZ_BCE,
                                    slab.data_ptr(), logits.data_ptr(), st), "train")
     L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st), "reduce")
     torch.cuda.synchronize()
@@ -151,13 +153,14 @@ def test_rank_shards_sum_to_full_batch(world):
     it = torch.as_tensor(rng.integers(0, I, B), dtype=torch.int32, device=DEV)
     y = torch.as_tensor((rng.random(B) < 0.2), dtype=torch.float32, device=DEV)
     st = L.stream_ptr()
+    rows = ops.pack_rows(u, it, y)
 
     def run(world, rank):
         gflat = torch.zeros(int(lay.total), device=DEV)
         slab = ops.new_slab(lay, DEV)
         ctl = ops.new_ctl(B, DEV)
-        L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), u.data_ptr(),
-                                       it.data_ptr(), y.data_ptr(), ctl.data_ptr(), B, world, rank, L.DZ_BCE,
+        L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
+                                       None, ctl.data_ptr(), B, world, rank, L.DZ_BCE,
                                        slab.data_ptr(), None, st), "train")
         L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st), "reduce")
         return gflat
@@ -196,41 +199,71 @@ def test_hr_ndcg_short_batch_raises(golden):
                                nd.data_ptr(), L.stream_ptr()) == L.NCF_E_ARG
 
 
+def _rand_rows(rng, n, n_users, n_items, pos_frac=0.3, hot=None):
+    from ncf_amd import ops
+    u = rng.integers(0, n_users, n)
+    i = rng.integers(0, n_items, n)
+    if hot is not None:  # fraction of rows on item 0: one item group larger than a part
+        i[rng.random(n) < hot] = 0
+    y = rng.random(n) < pos_frac
+    return torch.as_tensor(ops.pack_rows_host(u, i, y), device=DEV)
+
+
+def test_pack_rows_matches_host_packing():
+    from ncf_amd import ops
+    rng = np.random.default_rng(1)
+    n = 4099
+    u, i = rng.integers(0, 2**31 - 1, n), rng.integers(0, 2**31 - 1, n)
+    y = (rng.random(n) < 0.5).astype(np.float32)
+    got = ops.pack_rows(torch.as_tensor(u, dtype=torch.int32, device=DEV),
+                        torch.as_tensor(i, dtype=torch.int32, device=DEV),
+                        torch.as_tensor(y, device=DEV)).cpu().numpy()
+    assert np.array_equal(got, ops.pack_rows_host(u, i, y))
+
+
 def test_gather_epoch():
     import ncf_amd._lib as L
     n = 10007
-    rng = np.random.default_rng(0)
-    u = torch.as_tensor(rng.integers(0, 100, n), dtype=torch.int32, device=DEV)
-    i = torch.as_tensor(rng.integers(0, 100, n), dtype=torch.int32, device=DEV)
-    y = torch.as_tensor(rng.random(n), dtype=torch.float32, device=DEV)
+    rows = _rand_rows(np.random.default_rng(0), n, 100, 100)
     perm = torch.randperm(n, device=DEV)
-    uo, io, yo = torch.empty_like(u), torch.empty_like(i), torch.empty_like(y)
-    L.check(L.hip().ncf_gather_epoch(u.data_ptr(), i.data_ptr(), y.data_ptr(), perm.data_ptr(), n, uo.data_ptr(),
-                                     io.data_ptr(), yo.data_ptr(), L.stream_ptr()), "gather")
-    assert torch.equal(uo, u[perm]) and torch.equal(io, i[perm]) and torch.equal(yo, y[perm])
+    out = torch.empty_like(rows)
+    L.check(L.hip().ncf_gather_epoch(rows.data_ptr(), perm.data_ptr(), n, out.data_ptr(), L.stream_ptr()), "gather")
+    assert torch.equal(out, rows[perm])
 
 
-@pytest.mark.parametrize("n,bs,n_items", [(10007, 1000, 37), (65536 * 2 + 123, 65536, 3707), (5000, 5000, 1)])
-def test_prepare_epoch_batches_grouped_by_item(n, bs, n_items):
+# (rows, batch, items, hot-item fraction): one part (B <= 8192), 8 and 16 parts with
+# XCD-grouped blocks, a partial last batch, item ranges above the LDS offset table
+# (global offsets), an item group above the LDS staging buffer (direct writes),
+# the reference's batch_size=256, odd batch sizes, one item.
+PREP_CASES = [(10007, 1000, 37, None), (65536 * 2 + 123, 65536, 3707, None), (5000, 5000, 1, None),
+              (131072 + 77, 131072, 3707, None), (70001, 65536, 100000, None), (70001, 65536, 3707, 0.4),
+              (20000, 256, 3707, None), (99999, 33333, 999, 0.05)]
+
+
+@pytest.mark.parametrize("n,bs,n_items,hot", PREP_CASES)
+def test_prepare_epoch_batches_grouped_by_item(n, bs, n_items, hot):
     """Per batch: same rows as the plain shuffle (DataLoader membership), grouped by item."""
-    import ncf_amd._lib as L
-    rng = np.random.default_rng(n)
-    u = torch.as_tensor(rng.integers(0, 500, n), dtype=torch.int32, device=DEV)
-    i = torch.as_tensor(rng.integers(0, n_items, n), dtype=torch.int32, device=DEV)
-    y = torch.as_tensor(rng.random(n) < 0.3, dtype=torch.float32, device=DEV)
+    from ncf_amd import ops
+    rng = np.random.default_rng(n + bs)
+    rows = _rand_rows(rng, n, 500, n_items, hot=hot)
     perm = torch.randperm(n, device=DEV)
-    uo, io, yo = torch.empty_like(u), torch.empty_like(i), torch.empty_like(y)
-    L.check(L.hip().ncf_prepare_epoch(u.data_ptr(), i.data_ptr(), y.data_ptr(), perm.data_ptr(), n, bs, n_items,
-                                      uo.data_ptr(), io.data_ptr(), yo.data_ptr(), L.stream_ptr()), "prep")
+    prep = ops.EpochPrep(DEV)
+    out = prep(rows, perm, bs, n_items)
     torch.cuda.synchronize()
-    su, si, sy = u[perm].cpu().numpy(), i[perm].cpu().numpy(), y[perm].cpu().numpy()
-    go, gi, gy = uo.cpu().numpy(), io.cpu().numpy(), yo.cpu().numpy()
+    exp = rows[perm].cpu().numpy()
+    got = out.cpu().numpy()
     for b0 in range(0, n, bs):
         sl = slice(b0, min(n, b0 + bs))
-        assert (np.diff(gi[sl]) >= 0).all(), "batch not grouped by item"
-        key = lambda a, b_, c: np.lexsort((c, a, b_))
-        e = np.stack([si[sl], su[sl], sy[sl]], 1)
-        o = np.stack([gi[sl], go[sl], gy[sl]], 1)
-        e = e[np.lexsort(e.T[::-1])]
-        o = o[np.lexsort(o.T[::-1])]
-        assert np.array_equal(e, o)
+        gi = (got[sl] >> 32) & 0x7FFFFFFF
+        if bs >= 4096:  # smaller batches are shuffled only (include/ncf_hip.h)
+            assert (np.diff(gi) >= 0).all(), "batch not grouped by item"
+        else:
+            assert np.array_equal(got[sl], exp[sl])
+        assert np.array_equal(np.sort(exp[sl]), np.sort(got[sl])), "batch membership changed"
+    # second epoch through the same workspace: identical multiset per batch again
+    perm2 = torch.randperm(n, device=DEV)
+    out2 = prep(rows, perm2, bs, n_items).cpu().numpy()
+    exp2 = rows[perm2].cpu().numpy()
+    for b0 in range(0, n, bs):
+        sl = slice(b0, min(n, b0 + bs))
+        assert np.array_equal(np.sort(exp2[sl]), np.sort(out2[sl]))
