@@ -49,12 +49,31 @@ def tower_flops_per_row(f, L, model="NeuMF-end"):
 
 
 def gather_scatter_bytes_per_row(f, L):
-    """Algorithmic HBM bytes per row of the fused kernel: int32 user+item ids,
-    f32 label, the four embedding rows read, and the same four rows' gradient
-    added (f32 atomics: read-modify-write at the memory side)."""
+    """Algorithmic HBM bytes per row of the fused kernel: the 8-byte packed row
+    (user, item, label), the four embedding rows read, and the same four rows'
+    gradient added (f32 atomics: read-modify-write at the memory side)."""
     dm = f * 2 ** (L - 1)
     rows = 2 * (f + dm) * 4
-    return 12 + rows + rows
+    return 8 + rows + rows
+
+
+def pmc_traffic(f, L):
+    """HBM bytes per launch of the fused step kernel from the newest committed
+    rocprofv3 PMC summary (profiles/r*_prof_summary.json, written by
+    scripts/profile.sh + scripts/prof_summary.py from separate FETCH_SIZE and
+    WRITE_SIZE passes of this bench: bytes = (2 * FETCH_SIZE + WRITE_SIZE) KB * 1024,
+    the gfx950 correction of the MI355X guide).  (None, None) if absent."""
+    import glob
+    name = f"ncf::ncf_step_kernel<{f}, {L}, 2, false>"
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_prof_summary.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        for k in d.get("kernels", []):
+            if k.get("kernel") == name and k.get("hbm_bytes_corrected"):
+                return float(k["hbm_bytes_corrected"]), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def cpu_baseline(f, L, U, I, batch, seconds, threads):
@@ -202,18 +221,16 @@ def main():
     e1.record()
     torch.cuda.synchronize(dev)
     kt["prepare_epoch_per_epoch"] = e0.elapsed_time(e1) / 5
+    kt["ncf_train_step_per_launch_b2b"] = eng.time_train_kernel(50)
     rows_per_launch = per_gpu
     flops = tower_flops_per_row(f, nl) * rows_per_launch
-    ms = kt["ncf_train_step"]
+    ms = kt["ncf_train_step_per_launch_b2b"]
     achieved_tf = flops / (ms * 1e-3) / 1e12
     bytes_launch = gather_scatter_bytes_per_row(f, nl) * rows_per_launch
     achieved_gbs = bytes_launch / (ms * 1e-3) / 1e9
     P = sum(p.numel() for p in model.parameters())
     adam_bytes = 32 * P  # read p,g,m,v; write p,m,v,g(=0)
-    traffic = None
-    tfile = os.environ.get("NCF_PMC_TRAFFIC_JSON")
-    if tfile and os.path.exists(tfile):
-        traffic = json.load(open(tfile)).get("ncf_train_step_bytes_per_launch")
+    traffic, traffic_src = pmc_traffic(f, nl)
 
     # ---- quality: HR@10 / NDCG@10 on the leave-one-out test set ---------------
     hr10 = ndcg10 = None
@@ -248,7 +265,7 @@ def main():
                        "global_batch": global_batch, "per_gpu_batch": per_gpu, "parallelism": f"dp{world}",
                        "hip_graph": use_graph},
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": 157.3, "unit": "TFLOP/s",
-                         "frac": achieved_tf / 157.3, "traffic": traffic,
+                         "frac": achieved_tf / 157.3, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "ncf_step_kernel<16,3,NeuMF> (fused fwd+bwd)",
                          "flops_per_launch": flops, "kernel_ms": ms},
             "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": 8000.0, "unit": "GB/s",

@@ -164,6 +164,30 @@ class TrainEngine:
                 acc[name] += e[k].elapsed_time(e[k + 1])
         return {k: v / max(1, n_steps) for k, v in acc.items()}
 
+    def time_train_kernel(self, reps):
+        """Mean duration (ms) of the fused step kernel alone: `reps` back-to-back
+        launches on the current batch between one HIP event pair on the launch
+        stream (per-launch event pairs add several microseconds each).  The
+        gradient buffer is zeroed afterwards (the launches accumulate into it)."""
+        st = torch.cuda.current_stream(self.device)
+        lib = L.hip()
+        lay = ctypes.byref(self.lay)
+        sp = L.stream_ptr(self.device)
+
+        def launch():
+            L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.rows.data_ptr(),
+                                       None, self.ctl.data_ptr(), self.batch_size, self.world_size, self.rank,
+                                       L.DZ_BCE, self.slab.data_ptr(), None, sp), "ncf_train_step")
+        launch()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            launch()
+        e1.record(st)
+        torch.cuda.synchronize(self.device)
+        self.grads.zero_()
+        return e0.elapsed_time(e1) / reps
+
     def step(self):
         """One optimizer step on global batch ctl.batch (eager launches)."""
         self._step_body()
