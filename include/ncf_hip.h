@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 2
+#define NCF_ABI_VERSION 3
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -76,14 +76,26 @@ typedef struct ncf_step_ctl {
 
 int ncf_abi_version(void);
 
-/* 1 if a fused kernel is compiled for this shape, else 0. */
+/* Which path runs this shape: NCF_PATH_FUSED (one fused launch per step, tower
+ * weights in LDS), NCF_PATH_LAYERED (per-layer MFMA GEMM kernels with activations in
+ * the workspace: any factor_num, tower weights of any size), 0 = invalid shape. */
+#define NCF_PATH_FUSED 1
+#define NCF_PATH_LAYERED 2
 int ncf_supported(int model_type, int factor_num, int num_layers);
+
+/* Bytes of the `workspace` that ncf_train_step needs for up to `rows` rows per launch
+ * (rows = ceil(batch_global / world)): the fused path's partial slab
+ * [ncf_slab_rows()][ncf_slab_stride()], or the layered path's slab row + activations. */
+int64_t ncf_workspace_bytes(const ncf_layout *lay, int64_t rows);
+
+/* Bytes of the workspace ncf_forward needs for n rows (0 on the fused path). */
+int64_t ncf_forward_workspace_bytes(const ncf_layout *lay, int64_t n);
 
 /* Host-only: fill *out for NCF(user_num, item_num, factor_num, num_layers, model_type). */
 int ncf_layout_init(int user_num, int item_num, int factor_num, int num_layers, int model_type,
                     ncf_layout *out);
 
-/* Workgroups the fused step launches (rows of the partial slab). */
+/* Workgroups the fused step launches (rows of its partial slab). */
 int ncf_slab_rows(void);
 
 /* Floats per slab row: tower_len + 64 (16-byte aligned rows; loss at index tower_len). */
@@ -99,29 +111,34 @@ int64_t ncf_slab_stride(const ncf_layout *lay);
  * stream rows[0 .. ctl->n_total) (ncf_prepare_epoch output), last batch partial
  * (DataLoader drop_last=False); this rank takes rows [rank*ceil(gb/world), ...) of it.
  * grads: dense flat gradient buffer; embedding rows are scatter-added (f32
- * atomics), the tower/predict part is written per workgroup into
- * slab[ncf_slab_rows()][ncf_slab_stride()] (reduce with ncf_reduce_slab).
+ * atomics), the tower/predict part is written to the slab at the start of
+ * `workspace` (ncf_workspace_bytes(lay, ceil(batch_global/world)) bytes) and moved into
+ * grads by ncf_reduce_slab.
  * dz_mode NCF_DZ_BCE: the label is bit 63 of the row, `dlogit` is ignored (may be NULL).
  * dz_mode NCF_DZ_DLOGIT: dlogit[row] holds dL/dlogit per row (same indexing as rows).
  * logits_out (optional, may be NULL): per-row logits of this rank's rows.
  */
 int ncf_train_step(const ncf_layout *lay, const float *params, float *grads, const uint64_t *rows,
                    const float *dlogit, const ncf_step_ctl *ctl, int64_t batch_global, int world,
-                   int rank, int dz_mode, float *slab, float *logits_out, void *stream);
+                   int rank, int dz_mode, void *workspace, int64_t workspace_bytes,
+                   float *logits_out, void *stream);
 
-/* Forward only (NCF.forward under no_grad, metrics.py:11-12): logits[n] of rows[n]. */
+/* Forward only (NCF.forward under no_grad, metrics.py:11-12): logits[n] of rows[n].
+ * workspace: ncf_forward_workspace_bytes(lay, n) bytes (may be NULL when that is 0). */
 int ncf_forward(const ncf_layout *lay, const float *params, const uint64_t *rows, int64_t n,
-                float *logits, void *stream);
+                float *logits, void *workspace, int64_t workspace_bytes, void *stream);
 
 /* rows_out[k] = NCF_ROW_PACK(users[k], items[k], labels ? labels[k] : 0) (the feature /
  * label tensors the reference DataLoader yields, datasets.py:72-78). */
 int ncf_pack_rows(const int32_t *users, const int32_t *items, const float *labels, int64_t n,
                   uint64_t *rows_out, void *stream);
 
-/* grads[tower_begin + j] = sum_w slab[w][j] over a slab row (loss slot included), in a
- * fixed order (bitwise reproducible).  If ctl != NULL, also advances ctl->batch and
- * ctl->adam_t by one: the step's optimizer then runs as step t = ctl->adam_t. */
-int ncf_reduce_slab(const ncf_layout *lay, const float *slab, float *grads, ncf_step_ctl *ctl, void *stream);
+/* grads[tower_begin + j] = sum_w slab[w][j] over the slab rows at the start of the
+ * train workspace (loss slot included), in a fixed order (bitwise reproducible).  If
+ * ctl != NULL, also advances ctl->batch and ctl->adam_t by one: the step's optimizer
+ * then runs as step t = ctl->adam_t. */
+int ncf_reduce_slab(const ncf_layout *lay, const void *workspace, float *grads, ncf_step_ctl *ctl,
+                    void *stream);
 
 /*
  * Dense Adam over the active ranges of the flat buffers (torch.optim.Adam,

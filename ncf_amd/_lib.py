@@ -28,7 +28,8 @@ NCF_E_ARG = -2
 NCF_E_LAUNCH = -3
 MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
 DZ_BCE, DZ_DLOGIT = 0, 1
-ABI_VERSION = 2  # include/ncf_hip.h NCF_ABI_VERSION
+ABI_VERSION = 3  # include/ncf_hip.h NCF_ABI_VERSION
+PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
 
 c_i64 = ctypes.c_int64
@@ -58,8 +59,10 @@ _HIP_PROTOS = {
     "ncf_layout_init": (ctypes.c_int, [ctypes.c_int] * 5 + [ctypes.POINTER(NcfLayout)]),
     "ncf_slab_rows": (ctypes.c_int, []),
     "ncf_train_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp,
-                                      c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
-    "ncf_forward": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_i64, c_vp, c_vp]),
+                                      c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_i64, c_vp, c_vp]),
+    "ncf_forward": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "ncf_workspace_bytes": (c_i64, [ctypes.POINTER(NcfLayout), c_i64]),
+    "ncf_forward_workspace_bytes": (c_i64, [ctypes.POINTER(NcfLayout), c_i64]),
     "ncf_pack_rows": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "ncf_reduce_slab": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp]),
     "ncf_slab_stride": (c_i64, [ctypes.POINTER(NcfLayout)]),
@@ -138,9 +141,10 @@ def layout(user_num: int, item_num: int, factor_num: int, num_layers: int, model
     return lay
 
 
-def supported(model_type, factor_num: int, num_layers: int) -> bool:
+def supported(model_type, factor_num: int, num_layers: int) -> int:
+    """PATH_FUSED, PATH_LAYERED, or 0 for an invalid shape (ncf_supported)."""
     mode = MODEL_CODES[model_type] if isinstance(model_type, str) else int(model_type)
-    return bool(hip().ncf_supported(mode, int(factor_num), int(num_layers)))
+    return int(hip().ncf_supported(mode, int(factor_num), int(num_layers)))
 
 
 def stream_ptr(device=None) -> int:

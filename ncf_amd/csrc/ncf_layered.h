@@ -1,0 +1,32 @@
+// Layered (unfused) NeuMF step: the path for shapes without a fused kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ncf_hip.h"
+
+namespace ncf {
+
+static inline int64_t rup64(int64_t x) { return (x + 63) / 64 * 64; }
+
+struct LyrArgs {
+    ncf_layout lay;
+    const float* params;
+    float* grads;            // train: dense gradient buffer (embedding scatter targets)
+    const uint64_t* rows;    // packed rows (NCF_ROW_PACK)
+    const float* dlogit;     // NCF_DZ_DLOGIT: dL/dlogit per row
+    const ncf_step_ctl* ctl; // train: batch selection; nullptr = forward over fwd_n rows
+    int64_t batch_global, fwd_n;
+    int world, rank, dz_mode;
+    float* slab;             // one row [tower_len + 64] of tower/predict partials (+ loss)
+    float* logits_out;       // optional per-row logits
+};
+
+// Workspace floats for `rows` rows per launch (slab row + activations [+ dY buffers]).
+int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train);
+
+// Launch the layered forward (train = false) or forward + BCE + backward (train = true)
+// over at most R rows; ws = lyr_workspace_floats(lay, R, train) floats.
+int lyr_run(const LyrArgs& a, float* ws, int64_t R, bool train, hipStream_t st);
+
+}  // namespace ncf

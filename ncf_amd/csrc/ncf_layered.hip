@@ -1,0 +1,490 @@
+// Layered NeuMF step for every shape the fused kernel does not cover: tower
+// weights too large for LDS (e.g. NCF(32,3): 172 KB; NCF(64,4): 2.8 MB) or a
+// factor_num without an instantiation (the reference's factor sweeps use any f).
+//
+// Same arithmetic as NCF.forward / BCEWithLogitsLoss / loss.backward()
+// (reference src/ncf/models.py:97-118, scripts/train_neumf.py:112-114), one
+// layer at a time, activations staged in a caller-provided HBM workspace:
+//
+//   lyr_fwd<FIRST>        H_{k+1} = ReLU(A_k W_k^T + b_k)       A_0 gathered from Um/Im rows
+//   lyr_predict<TRAIN>    logit = wp.[Ug*Ig || H_L] + bp; BCE; dz; GMF scatter;
+//                         dY_{L-1} = dz * wp_mlp * [H_L > 0]; dwp, dbp, loss -> slab
+//   lyr_bwd_w<FIRST>      dW_k += dY_k^T A_k,  db_k += colsum(dY_k)   (split over rows)
+//   lyr_bwd_data<FIRST>   dY_{k-1} = (dY_k W_k) * [H_k > 0], or for k = 0 the
+//                         Um/Im embedding scatter-add
+//
+// All three GEMM shapes run on one MFMA core: v_mfma_f32_16x16x4f32 (exact
+// fp32), 256 threads = 4 waves, 64x64 block tile, each wave a 32x32 sub-tile
+// (2x2 MFMA tiles), K in steps of 16 through double-buffered LDS.  Operand
+// loaders map lanes along the operand's contiguous memory dimension.  Rows at
+// or past the batch's end are padding: they gather id 0 and their dz is 0, so
+// every gradient contribution from them is zero.
+#include "ncf_common.h"
+#include "ncf_layered.h"
+
+namespace ncf {
+namespace {
+
+constexpr int GBM = 64, GBN = 64, GBK = 16, GNT = 256, GPAD = 4;
+
+struct Sel {
+    int64_t base, nloc;
+    float gb;
+};
+
+// Rows of this launch: the fused kernel's selection (ncf_train.hip), i.e. global
+// batch ctl->batch of the epoch stream, this rank's contiguous shard of it.
+__device__ __forceinline__ Sel select_rows(const LyrArgs& a) {
+    if (a.ctl == nullptr) return Sel{0, a.fwd_n, 1.f};
+    const int64_t ntot = a.ctl->n_total;
+    const int64_t nbatch = (ntot + a.batch_global - 1) / a.batch_global;
+    const int64_t b = nbatch > 0 ? a.ctl->batch % nbatch : 0;
+    const int64_t b0 = b * a.batch_global;
+    int64_t gb = ntot - b0;
+    if (gb > a.batch_global) gb = a.batch_global;
+    if (gb < 0) gb = 0;
+    const int64_t per = (gb + a.world - 1) / a.world;
+    int64_t lo = (int64_t)a.rank * per, hi = lo + per;
+    if (lo > gb) lo = gb;
+    if (hi > gb) hi = gb;
+    return Sel{b0 + lo, hi - lo, (float)gb};
+}
+
+__device__ __forceinline__ void row_ids(const LyrArgs& a, const Sel& s, int64_t m, int& u, int& it) {
+    if (m < s.nloc) {
+        const uint64_t r = a.rows[s.base + m];
+        u = (int)(uint32_t)r;
+        it = (int)((r >> 32) & 0x7fffffffu);
+        if (u < 0) it = -1;
+    } else {
+        u = it = -1;
+    }
+}
+
+// Lane -> tile-element maps.  KC: the operand is contiguous along K (16 lanes
+// per row, 4 passes of 16 rows); otherwise contiguous along M/N (64 lanes per
+// k, 4 passes of 4 k).
+template <bool KC>
+__device__ __forceinline__ int map_mn(int t, int p) { return KC ? (t >> 4) + 16 * p : (t & 63); }
+template <bool KC>
+__device__ __forceinline__ int map_k(int t, int p) { return KC ? (t & 15) : (t >> 6) + 4 * p; }
+
+// C[mb..mb+32) x [nb..nb+32) for this wave: acc[ti][tj] reg r at
+// row 16*ti + 4*(l>>4) + r, col 16*tj + (l&15).
+template <bool AKC, bool BKC, class GA, class GB, class EP>
+__device__ __forceinline__ void gemm_block(int64_t m0, int64_t n0, int64_t kbeg, int64_t kend, GA ga, GB gb,
+                                           EP ep) {
+    __shared__ float As[2][GBK][GBM + GPAD];
+    __shared__ float Bs[2][GBK][GBN + GPAD];
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+    float ra[4], rb[4];
+    auto load = [&](int64_t k0) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) ra[p] = ga(map_mn<AKC>(t, p), k0 + map_k<AKC>(t, p));
+#pragma unroll
+        for (int p = 0; p < 4; ++p) rb[p] = gb(k0 + map_k<BKC>(t, p), map_mn<BKC>(t, p));
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) As[buf][map_k<AKC>(t, p)][map_mn<AKC>(t, p)] = ra[p];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) Bs[buf][map_k<BKC>(t, p)][map_mn<BKC>(t, p)] = rb[p];
+    };
+    f4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    load(kbeg);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t k0 = kbeg; k0 < kend; k0 += GBK) {
+        const bool more = k0 + GBK < kend;
+        if (more) load(k0 + GBK);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int kk = 4 * s + (l >> 4);
+            const float a0 = As[buf][kk][wm + (l & 15)], a1 = As[buf][kk][wm + 16 + (l & 15)];
+            const float b0 = Bs[buf][kk][wn + (l & 15)], b1 = Bs[buf][kk][wn + 16 + (l & 15)];
+            acc[0][0] = MFMA4(a0, b0, acc[0][0]);
+            acc[0][1] = MFMA4(a0, b1, acc[0][1]);
+            acc[1][0] = MFMA4(a1, b0, acc[1][0]);
+            acc[1][1] = MFMA4(a1, b1, acc[1][1]);
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    (void)m0;
+    (void)n0;
+    ep(acc, wm, wn, l);
+}
+
+// ---------------------------------------------------------------------------
+// Forward layer k: H_{k+1}[m][n] = ReLU(sum_c A[m][c] W_k[n][c] + b_k[n]).
+// grid (ceil(R/64), ceil(N/64)).
+template <bool FIRST>
+__global__ __launch_bounds__(GNT) void lyr_fwd_kernel(LyrArgs a, int k, const float* __restrict__ Ain,
+                                                      float* __restrict__ Hout, int64_t R) {
+    __shared__ int su[GBM], si[GBM];
+    const Sel s = select_rows(a);
+    const ncf_layout& lay = a.lay;
+    const int DM = lay.factor_num << (lay.num_layers - 1);
+    const int K = (2 * DM) >> k, N = K / 2;
+    const int64_t m0 = (int64_t)blockIdx.x * GBM;
+    const int n0 = blockIdx.y * GBN;
+    const float* prm = a.params;
+    const float* W = prm + lay.w[k];
+    const float* bias = prm + lay.b[k];
+    if (FIRST && threadIdx.x < GBM) {
+        int u, it;
+        row_ids(a, s, m0 + threadIdx.x, u, it);
+        su[threadIdx.x] = u < 0 ? 0 : u;
+        si[threadIdx.x] = it < 0 ? 0 : it;
+    }
+    if (FIRST) __syncthreads();
+    auto ga = [&](int r, int64_t c) -> float {
+        const int64_t m = m0 + r;
+        if (m >= R || c >= K) return 0.f;
+        if constexpr (FIRST) {
+            return c < DM ? prm[lay.um + (int64_t)su[r] * DM + c] : prm[lay.im + (int64_t)si[r] * DM + (c - DM)];
+        } else {
+            return Ain[m * K + c];
+        }
+    };
+    auto gb = [&](int64_t c, int n) -> float {
+        const int nn = n0 + n;
+        return (nn < N && c < K) ? W[(int64_t)nn * K + c] : 0.f;
+    };
+    auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) {
+                const int n = n0 + wn + 16 * tj + (l & 15);
+                if (n >= N) continue;
+                const float bn = bias[n];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t m = m0 + wm + 16 * ti + 4 * (l >> 4) + r;
+                    if (m < R) Hout[m * N + n] = fmaxf(lane_get(acc[ti][tj], r) + bn, 0.f);
+                }
+            }
+    };
+    gemm_block<true, true>(m0, n0, 0, K, ga, gb, ep);
+}
+
+// ---------------------------------------------------------------------------
+// Backward data of layer k: C[m][n] = sum_j dY_k[m][j] W_k[j][n]   (n < s_k).
+//   k > 0: dY_{k-1}[m][n] = C * [H_k[m][n] > 0]
+//   k = 0: scatter-add C into grad Um[u_m] (n < dm) / Im[i_m] (n >= dm)
+// grid (ceil(R/64), ceil(s_k/64)).
+template <bool FIRST>
+__global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, const float* __restrict__ D,
+                                                           const float* __restrict__ Hk, float* __restrict__ Dout,
+                                                           int64_t R) {
+    __shared__ int su[GBM], si[GBM];
+    const Sel s = select_rows(a);
+    const ncf_layout& lay = a.lay;
+    const int DM = lay.factor_num << (lay.num_layers - 1);
+    const int N = (2 * DM) >> k, J = N / 2;  // this layer: in = N, out = J
+    const int64_t m0 = (int64_t)blockIdx.x * GBM;
+    const int n0 = blockIdx.y * GBN;
+    const float* W = a.params + lay.w[k];
+    if (FIRST && threadIdx.x < GBM) {
+        int u, it;
+        row_ids(a, s, m0 + threadIdx.x, u, it);
+        su[threadIdx.x] = u;
+        si[threadIdx.x] = it;
+    }
+    if (FIRST) __syncthreads();
+    auto ga = [&](int r, int64_t j) -> float {
+        const int64_t m = m0 + r;
+        return (m < R && j < J) ? D[m * J + j] : 0.f;
+    };
+    auto gb = [&](int64_t j, int n) -> float {
+        const int nn = n0 + n;
+        return (j < J && nn < N) ? W[j * N + nn] : 0.f;
+    };
+    auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) {
+                const int n = n0 + wn + 16 * tj + (l & 15);
+                if (n >= N) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int rr = wm + 16 * ti + 4 * (l >> 4) + r;
+                    const int64_t m = m0 + rr;
+                    if (m >= R) continue;
+                    const float v = lane_get(acc[ti][tj], r);
+                    if constexpr (FIRST) {
+                        const int id = n < DM ? su[rr] : si[rr];
+                        if (id >= 0)
+                            atomicAdd(a.grads + (n < DM ? lay.um + (int64_t)id * DM + n
+                                                        : lay.im + (int64_t)id * DM + (n - DM)),
+                                      v);
+                    } else {
+                        Dout[m * N + n] = Hk[m * N + n] > 0.f ? v : 0.f;
+                    }
+                }
+            }
+    };
+    gemm_block<true, false>(m0, n0, 0, J, ga, gb, ep);
+}
+
+// ---------------------------------------------------------------------------
+// Backward weight of layer k over the row chunk of blockIdx.z:
+//   dW_k[j][c] += sum_m dY_k[m][j] A_k[m][c]   (c < s_k)
+//   db_k[j]    += sum_m dY_k[m][j]             (the extra column c = s_k of ones)
+// into the slab (tower partials, reduced by ncf_reduce_slab).
+// grid (ceil(J/64), ceil((s_k+1)/64), splits).
+template <bool FIRST>
+__global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const float* __restrict__ D,
+                                                        const float* __restrict__ Ain, int64_t R, int64_t chunk) {
+    __shared__ int su[GBK * 64], si[GBK * 64];  // ids of up to 1024 rows of the chunk (FIRST)
+    const Sel s = select_rows(a);
+    const ncf_layout& lay = a.lay;
+    const int DM = lay.factor_num << (lay.num_layers - 1);
+    const int K = (2 * DM) >> k, J = K / 2;
+    const int j0 = blockIdx.x * GBM;
+    const int c0 = blockIdx.y * GBN;
+    const int64_t r0 = (int64_t)blockIdx.z * chunk;
+    int64_t r1 = r0 + chunk;
+    if (r1 > R) r1 = R;
+    if (r1 > s.nloc) r1 = s.nloc;  // padding rows carry dY = 0
+    if (r0 >= r1) return;          // block-uniform
+    const float* prm = a.params;
+    float* slab = a.slab;
+    const int64_t tb = lay.tower_begin;
+    auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) {
+                const int c = c0 + wn + 16 * tj + (l & 15);
+                if (c > K) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = j0 + wm + 16 * ti + 4 * (l >> 4) + r;
+                    if (j >= J) continue;
+                    const float v = lane_get(acc[ti][tj], r);
+                    if (c < K)
+                        atomicAdd(slab + (lay.w[k] - tb) + (int64_t)j * K + c, v);
+                    else
+                        atomicAdd(slab + (lay.b[k] - tb) + j, v);
+                }
+            }
+    };
+    auto ga = [&](int jr, int64_t m) -> float {
+        const int j = j0 + jr;
+        return (m < r1 && j < J) ? D[m * J + j] : 0.f;
+    };
+    if constexpr (FIRST) {
+        // rows processed in sub-chunks of 1024 with their ids staged in LDS
+        for (int64_t q0 = r0; q0 < r1; q0 += GBK * 64) {
+            const int64_t q1 = q0 + GBK * 64 < r1 ? q0 + GBK * 64 : r1;
+            __syncthreads();
+            for (int e = threadIdx.x; e < GBK * 64; e += GNT) {
+                int u, it;
+                row_ids(a, s, q0 + e, u, it);
+                su[e] = u < 0 ? 0 : u;
+                si[e] = it < 0 ? 0 : it;
+            }
+            __syncthreads();
+            auto gb = [&](int64_t m, int cr) -> float {
+                const int c = c0 + cr;
+                if (m >= q1 || c > K) return 0.f;
+                if (c == K) return 1.f;
+                const int e = (int)(m - q0);
+                return c < DM ? prm[lay.um + (int64_t)su[e] * DM + c] : prm[lay.im + (int64_t)si[e] * DM + (c - DM)];
+            };
+            auto ga2 = [&](int jr, int64_t m) -> float {
+                const int j = j0 + jr;
+                return (m < q1 && j < J) ? D[m * J + j] : 0.f;
+            };
+            gemm_block<false, false>(j0, c0, q0, q1, ga2, gb, ep);
+        }
+    } else {
+        auto gb = [&](int64_t m, int cr) -> float {
+            const int c = c0 + cr;
+            if (m >= r1 || c > K) return 0.f;
+            return c == K ? 1.f : Ain[m * K + c];
+        };
+        gemm_block<false, false>(j0, c0, r0, r1, ga, gb, ep);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Predict + loss + GMF backward.  G lanes per row (G = min(64, pow2 >= F)),
+// feature f handled by lane f % G.  Block partials of dwp / dbp / loss in LDS,
+// one global atomic per value per block.
+template <bool TRAIN>
+__global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float* __restrict__ HL,
+                                                          float* __restrict__ Dout, int64_t R, int G) {
+    extern __shared__ float red[];  // [P + 2]: dwp[P], dbp, loss
+    const Sel s = select_rows(a);
+    const ncf_layout& lay = a.lay;
+    const int F = lay.factor_num;
+    const bool gmf = lay.model_type != NCF_MODEL_MLP, mlp = lay.model_type != NCF_MODEL_GMF;
+    const int Pg = gmf ? F : 0, P = Pg + (mlp ? F : 0);
+    const float* prm = a.params;
+    const float* wp = prm + lay.wp;
+    const int t = threadIdx.x;
+    if (TRAIN) {
+        for (int e = t; e < P + 2; e += GNT) red[e] = 0.f;
+        __syncthreads();
+    }
+    const int rows_per_block = GNT / G;
+    const int gl = t % G;
+    const int64_t m = (int64_t)blockIdx.x * rows_per_block + t / G;
+    int u, it;
+    row_ids(a, s, m, u, it);
+    const bool valid = m < R && u >= 0;
+    const int uu = u < 0 ? 0 : u, ii = it < 0 ? 0 : it;
+    float part = 0.f;
+    if (valid) {
+        for (int f = gl; f < F; f += G) {
+            if (gmf) part += wp[f] * (prm[lay.ug + (int64_t)uu * F + f] * prm[lay.ig + (int64_t)ii * F + f]);
+            if (mlp) part += wp[Pg + f] * HL[m * F + f];
+        }
+    }
+    for (int o = G >> 1; o >= 1; o >>= 1) part += __shfl_xor(part, o, 64);
+    const float z = part + prm[lay.bp];
+    if (valid && gl == 0 && a.logits_out != nullptr) a.logits_out[m] = z;
+    if constexpr (TRAIN) {
+        float dz = 0.f;
+        if (valid) {
+            const uint64_t rw = a.rows[s.base + m];
+            if (a.dz_mode == NCF_DZ_BCE) {
+                const float y = (float)(uint32_t)(rw >> 63);
+                dz = (sigmoidf_(z) - y) / s.gb;
+                if (gl == 0) atomicAdd(&red[P + 1], bce_loss(z, y) / s.gb);
+            } else {
+                dz = a.dlogit[s.base + m];
+            }
+            if (gl == 0) atomicAdd(&red[P], dz);
+            for (int f = gl; f < F; f += G) {
+                if (gmf) {
+                    const float ug = prm[lay.ug + (int64_t)uu * F + f], ig = prm[lay.ig + (int64_t)ii * F + f];
+                    atomicAdd(&red[f], dz * (ug * ig));
+                    const float dg = dz * wp[f];
+                    atomicAdd(a.grads + lay.ug + (int64_t)uu * F + f, dg * ig);
+                    atomicAdd(a.grads + lay.ig + (int64_t)ii * F + f, dg * ug);
+                }
+                if (mlp) {
+                    const float h = HL[m * F + f];
+                    atomicAdd(&red[Pg + f], dz * h);
+                    Dout[m * F + f] = h > 0.f ? dz * wp[Pg + f] : 0.f;
+                }
+            }
+        } else if (mlp && m < R) {
+            for (int f = gl; f < F; f += G) Dout[m * F + f] = 0.f;
+        }
+        __syncthreads();
+        const int64_t tb = lay.tower_begin;
+        for (int e = t; e < P + 2; e += GNT) {
+            const float v = red[e];
+            if (v == 0.f) continue;
+            const int64_t off = e < P ? (lay.wp - tb) + e : (e == P ? (lay.bp - tb) : lay.tower_len);
+            atomicAdd(a.slab + off, v);
+        }
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train) {
+    int64_t fl = rup64(lay->tower_len + 64);
+    if (lay->model_type == NCF_MODEL_GMF) return fl;
+    const int DM = lay->factor_num << (lay->num_layers - 1);
+    for (int k = 1; k <= lay->num_layers; ++k) fl += rup64(rows * ((2 * DM) >> k));
+    if (train) fl += 2 * rup64(rows * DM);
+    return fl;
+}
+
+int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st) {
+    LyrArgs a = a0;
+    const ncf_layout& lay = a.lay;
+    const int L = lay.num_layers, F = lay.factor_num;
+    const int DM = F << (L - 1);
+    const bool mlp = lay.model_type != NCF_MODEL_GMF;
+    float* slab = ws;
+    a.slab = slab;
+    float* H[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    float* Da = nullptr;
+    float* Db = nullptr;
+    int64_t off = rup64(lay.tower_len + 64);
+    if (mlp) {
+        for (int k = 1; k <= L; ++k) {
+            H[k] = ws + off;
+            off += rup64(R * ((2 * DM) >> k));
+        }
+        if (train) {
+            Da = ws + off;
+            off += rup64(R * DM);
+            Db = ws + off;
+        }
+    }
+    if (train && hipMemsetAsync(slab, 0, (size_t)(lay.tower_len + 64) * 4, st) != hipSuccess) return NCF_E_LAUNCH;
+    const unsigned mt = (unsigned)((R + GBM - 1) / GBM);
+    if (mlp) {
+        for (int k = 0; k < L; ++k) {
+            const int N = (2 * DM) >> (k + 1);
+            const dim3 grid(mt, (unsigned)((N + GBN - 1) / GBN));
+            if (k == 0)
+                hipLaunchKernelGGL(lyr_fwd_kernel<true>, grid, dim3(GNT), 0, st, a, k, nullptr, H[1], R);
+            else
+                hipLaunchKernelGGL(lyr_fwd_kernel<false>, grid, dim3(GNT), 0, st, a, k, H[k], H[k + 1], R);
+        }
+    }
+    int G = 1;
+    while (G < F && G < 64) G <<= 1;
+    const int P = (lay.model_type == NCF_MODEL_NEUMF ? 2 : 1) * F;
+    const int64_t rpb = GNT / G;
+    const unsigned pg = (unsigned)((R + rpb - 1) / rpb);
+    const size_t lds = (size_t)(P + 2) * 4;
+    float* Dtop = Da;
+    if (train)
+        hipLaunchKernelGGL(lyr_predict_kernel<true>, dim3(pg), dim3(GNT), lds, st, a, mlp ? H[L] : nullptr, Dtop, R,
+                           G);
+    else
+        hipLaunchKernelGGL(lyr_predict_kernel<false>, dim3(pg), dim3(GNT), lds, st, a, mlp ? H[L] : nullptr, nullptr,
+                           R, G);
+    if (!train || !mlp) return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
+    float* Dcur = Da;
+    float* Dnext = Db;
+    for (int k = L - 1; k >= 0; --k) {
+        const int K = (2 * DM) >> k, J = K / 2;
+        // weight gradient: split the rows so the launch has ~512 blocks
+        const int64_t tiles = (int64_t)((J + GBM - 1) / GBM) * ((K + 1 + GBN - 1) / GBN);
+        int64_t splits = 512 / tiles;
+        const int64_t max_splits = (R + 255) / 256;
+        if (splits > max_splits) splits = max_splits;
+        if (splits < 1) splits = 1;
+        int64_t chunk = (R + splits - 1) / splits;
+        chunk = (chunk + GBK - 1) / GBK * GBK;
+        splits = (R + chunk - 1) / chunk;
+        const dim3 gw((unsigned)((J + GBM - 1) / GBM), (unsigned)((K + 1 + GBN - 1) / GBN), (unsigned)splits);
+        if (k == 0)
+            hipLaunchKernelGGL(lyr_bwd_w_kernel<true>, gw, dim3(GNT), 0, st, a, k, Dcur, nullptr, R, chunk);
+        else
+            hipLaunchKernelGGL(lyr_bwd_w_kernel<false>, gw, dim3(GNT), 0, st, a, k, Dcur, H[k], R, chunk);
+        const dim3 gd(mt, (unsigned)((K + GBN - 1) / GBN));
+        if (k == 0) {
+            hipLaunchKernelGGL(lyr_bwd_data_kernel<true>, gd, dim3(GNT), 0, st, a, k, Dcur, nullptr, nullptr, R);
+        } else {
+            hipLaunchKernelGGL(lyr_bwd_data_kernel<false>, gd, dim3(GNT), 0, st, a, k, Dcur, H[k], Dnext, R);
+            float* tmp = Dcur;
+            Dcur = Dnext;
+            Dnext = tmp;
+        }
+    }
+    return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
+}
+
+}  // namespace ncf

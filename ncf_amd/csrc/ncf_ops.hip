@@ -4,10 +4,9 @@
 #include <string.h>
 
 #include "ncf_kernels.h"
+#include "ncf_layered.h"
 
 namespace ncf {
-
-static inline int64_t rup64(int64_t x) { return (x + 63) / 64 * 64; }
 
 // ---------------------------------------------------------------------------
 // Slab reduction: grads[tb + j] = sum_w slab[w][j], fixed order (bitwise
@@ -28,6 +27,10 @@ __global__ __launch_bounds__(256) void reduce_slab_kernel(const float* __restric
 #pragma unroll 16
         for (int r = 0; r < per; ++r) {
             const f4 v = *reinterpret_cast<const f4*>(p + (int64_t)r * 16 * stride);
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+        if (rg < rows - 16 * per) {  // rows not a multiple of 16 (the layered path's single row)
+            const f4 v = *reinterpret_cast<const f4*>(p + (int64_t)per * 16 * stride);
             s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
         }
     }
@@ -538,23 +541,58 @@ int ncf_layout_init(int U, int I, int F, int L, int mode, ncf_layout* o) {
     return NCF_OK;
 }
 
+// Fused kernel for this layout, or nullptr (then the layered path runs).
+static const KernelEntry* fused_entry(const ncf_layout* lay) {
+    const KernelEntry* e = find_entry(lay->model_type, lay->factor_num, lay->num_layers);
+    if (!e) return nullptr;
+    return train_lds_floats(e, lay) * 4 <= LDS_LIMIT_BYTES ? e : nullptr;
+}
+
 int ncf_supported(int mode, int F, int L) {
-    const KernelEntry* e = find_entry(mode, F, L);
-    if (!e) return 0;
     ncf_layout lay;
     if (ncf_layout_init(1, 1, F, L, mode, &lay) != NCF_OK) return 0;
-    return train_lds_floats(e, &lay) * 4 <= LDS_LIMIT_BYTES ? 1 : 0;
+    return fused_entry(&lay) ? NCF_PATH_FUSED : NCF_PATH_LAYERED;
+}
+
+int64_t ncf_workspace_bytes(const ncf_layout* lay, int64_t rows) {
+    if (!lay || rows < 0) return -1;
+    if (fused_entry(lay)) return (int64_t)SLAB_ROWS * ncf_slab_stride(lay) * 4;
+    return lyr_workspace_floats(lay, rows, true) * 4;
+}
+
+int64_t ncf_forward_workspace_bytes(const ncf_layout* lay, int64_t n) {
+    if (!lay || n < 0) return -1;
+    if (fused_entry(lay)) return 0;
+    return lyr_workspace_floats(lay, n, false) * 4;
 }
 
 int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
                    const float* dlogit, const ncf_step_ctl* ctl, int64_t batch_global, int world, int rank,
-                   int dz_mode, float* slab, float* logits_out, void* stream) {
-    if (!lay || !params || !grads || !rows || !ctl || !slab) return NCF_E_ARG;
+                   int dz_mode, void* workspace, int64_t workspace_bytes, float* logits_out, void* stream) {
+    if (!lay || !params || !grads || !rows || !ctl || !workspace) return NCF_E_ARG;
     if (batch_global <= 0 || world < 1 || rank < 0 || rank >= world) return NCF_E_ARG;
     if (dz_mode != NCF_DZ_BCE && dz_mode != NCF_DZ_DLOGIT) return NCF_E_ARG;
     if (dz_mode == NCF_DZ_DLOGIT && !dlogit) return NCF_E_ARG;
-    const KernelEntry* e = find_entry(lay->model_type, lay->factor_num, lay->num_layers);
-    if (!e) return NCF_E_UNSUPPORTED;
+    const int64_t rows_max = (batch_global + world - 1) / world;
+    if (workspace_bytes < ncf_workspace_bytes(lay, rows_max)) return NCF_E_ARG;
+    float* slab = static_cast<float*>(workspace);
+    const KernelEntry* e = fused_entry(lay);
+    if (!e) {
+        LyrArgs la;
+        memset(&la, 0, sizeof(la));
+        la.lay = *lay;
+        la.params = params;
+        la.grads = grads;
+        la.rows = rows;
+        la.dlogit = dlogit;
+        la.ctl = ctl;
+        la.batch_global = batch_global;
+        la.world = world;
+        la.rank = rank;
+        la.dz_mode = dz_mode;
+        la.logits_out = logits_out;
+        return lyr_run(la, slab, rows_max, true, (hipStream_t)stream);
+    }
     const int64_t lds = train_lds_floats(e, lay) * 4;
     if (lds > LDS_LIMIT_BYTES) return NCF_E_UNSUPPORTED;
     if (ensure_lds(e->train, lds) != NCF_OK) return NCF_E_LAUNCH;
@@ -583,11 +621,22 @@ int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, con
 }
 
 int ncf_forward(const ncf_layout* lay, const float* params, const uint64_t* rows, int64_t n, float* logits,
-                void* stream) {
+                void* workspace, int64_t workspace_bytes, void* stream) {
     if (!lay || !params || !rows || !logits || n < 0) return NCF_E_ARG;
     if (n == 0) return NCF_OK;
     const KernelEntry* e = find_entry(lay->model_type, lay->factor_num, lay->num_layers);
-    if (!e) return NCF_E_UNSUPPORTED;
+    if (!fused_entry(lay)) {
+        if (!workspace || workspace_bytes < ncf_forward_workspace_bytes(lay, n)) return NCF_E_ARG;
+        LyrArgs la;
+        memset(&la, 0, sizeof(la));
+        la.lay = *lay;
+        la.params = params;
+        la.rows = rows;
+        la.fwd_n = n;
+        la.world = 1;
+        la.logits_out = logits;
+        return lyr_run(la, static_cast<float*>(workspace), n, false, (hipStream_t)stream);
+    }
     const int64_t lds = (int64_t)(e->w_total + e->misc) * 4;
     if (lds > LDS_LIMIT_BYTES) return NCF_E_UNSUPPORTED;
     if (ensure_lds(e->fwd, lds) != NCF_OK) return NCF_E_LAUNCH;
@@ -609,13 +658,15 @@ int ncf_forward(const ncf_layout* lay, const float* params, const uint64_t* rows
 
 int64_t ncf_slab_stride(const ncf_layout* lay) { return lay ? lay->tower_len + 64 : -1; }
 
-int ncf_reduce_slab(const ncf_layout* lay, const float* slab, float* grads, ncf_step_ctl* ctl, void* stream) {
-    if (!lay || !slab || !grads) return NCF_E_ARG;
+int ncf_reduce_slab(const ncf_layout* lay, const void* workspace, float* grads, ncf_step_ctl* ctl, void* stream) {
+    if (!lay || !workspace || !grads) return NCF_E_ARG;
+    const float* slab = static_cast<const float*>(workspace);
     const int stride = (int)ncf_slab_stride(lay);
     const int lo = lay->model_type == NCF_MODEL_GMF ? (int)(lay->wp - lay->tower_begin) : 0;
     const int blocks = (stride - lo + 63) / 64;
+    const int rows = fused_entry(lay) ? SLAB_ROWS : 1;  // the layered path accumulates into one row
     hipLaunchKernelGGL(reduce_slab_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab,
-                       grads + lay->tower_begin, lo, stride, SLAB_ROWS, ctl);
+                       grads + lay->tower_begin, lo, stride, rows, ctl);
     return launch_status();
 }
 

@@ -64,7 +64,7 @@ class TrainEngine:
         elif optimizer != "sgd":
             raise ValueError(optimizer)
         self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
-        self.slab = ops.new_slab(self.lay, dev)
+        self.ws = None  # ncf_train_step workspace, sized by set_epoch_stream
         self.ctl = ops.new_ctl(0, dev)
         self.world_size, self.rank, self.group = int(world_size), int(rank), process_group
         rng = _active_ranges(model, self.lay)
@@ -86,8 +86,10 @@ class TrainEngine:
         n = rows.numel()
         self.rows = rows
         self.n_total = n
-        if self.batch_size != batch_size:
+        if self.batch_size != batch_size or self.ws is None:
             self._graph = None
+            per = (int(batch_size) + self.world_size - 1) // self.world_size
+            self.ws = ops.new_workspace(self.lay, per, self.device)
         self.batch_size = int(batch_size)
         self.ctl[0] = 0
         self.ctl[2] = n
@@ -105,8 +107,8 @@ class TrainEngine:
         L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.rows.data_ptr(),
                                    None, self.ctl.data_ptr(),
                                    self.batch_size, self.world_size, self.rank, L.DZ_BCE,
-                                   self.slab.data_ptr(), None, st), "ncf_train_step")
-        L.check(lib.ncf_reduce_slab(lay, self.slab.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(), st), "ncf_reduce_slab")
+                                   self.ws.data_ptr(), self.ws.numel() * 4, None, st), "ncf_train_step")
+        L.check(lib.ncf_reduce_slab(lay, self.ws.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(), st), "ncf_reduce_slab")
         if self.world_size > 1:
             import torch.distributed as dist
             dist.all_reduce(self.grads, group=self.group)
@@ -138,9 +140,9 @@ class TrainEngine:
             L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.rows.data_ptr(),
                                        None, self.ctl.data_ptr(),
                                        self.batch_size, self.world_size, self.rank, L.DZ_BCE,
-                                       self.slab.data_ptr(), None, sp), "ncf_train_step")
+                                       self.ws.data_ptr(), self.ws.numel() * 4, None, sp), "ncf_train_step")
             e[1].record(st)
-            L.check(lib.ncf_reduce_slab(lay, self.slab.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(), sp), "ncf_reduce_slab")
+            L.check(lib.ncf_reduce_slab(lay, self.ws.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(), sp), "ncf_reduce_slab")
             e[2].record(st)
             if self.world_size > 1:
                 import torch.distributed as dist
@@ -177,7 +179,7 @@ class TrainEngine:
         def launch():
             L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.rows.data_ptr(),
                                        None, self.ctl.data_ptr(), self.batch_size, self.world_size, self.rank,
-                                       L.DZ_BCE, self.slab.data_ptr(), None, sp), "ncf_train_step")
+                                       L.DZ_BCE, self.ws.data_ptr(), self.ws.numel() * 4, None, sp), "ncf_train_step")
         launch()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)

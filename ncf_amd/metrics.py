@@ -38,7 +38,7 @@ def evaluate_arrays(model, users, items, batch, top_k):
     u = torch.as_tensor(np.asarray(users), dtype=torch.int32).to(dev)
     i = torch.as_tensor(np.asarray(items), dtype=torch.int32).to(dev)
     with torch.no_grad():
-        logits = ops.forward_logits(flat, lay, ops.pack_rows(u, i))
+        logits = ops.forward_logits(flat, lay, ops.pack_rows(u, i), ws_owner=model)
     hr, nd = _hr_ndcg_device(logits, i, batch, top_k)
     return hr.cpu().tolist(), nd.double().cpu().tolist()
 

@@ -53,7 +53,7 @@ def ensure_flat(model):
             return flat, lay
     if not L.supported(model.model_type, model.factor_num, model.num_layers):
         raise NotImplementedError(
-            f"no fused HIP kernel for model_type={model.model_type} factor_num={model.factor_num} "
+            f"no HIP path for model_type={model.model_type} factor_num={model.factor_num} "
             f"num_layers={model.num_layers}")
     flat = torch.zeros(int(lay.total), dtype=torch.float32, device=dev)
     with torch.no_grad():
@@ -121,30 +121,55 @@ class EpochPrep:
         return self.out
 
 
-def forward_logits(flat, lay, rows, out=None):
+def _ws(owner, attr, nbytes, dev):
+    """Device workspace of at least nbytes, cached on `owner` (grown, never shrunk)."""
+    if nbytes <= 0:
+        return None
+    ws = getattr(owner, attr, None)
+    if ws is None or ws.numel() * 4 < nbytes or ws.device != dev:
+        ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+        setattr(owner, attr, ws)
+    return ws
+
+
+def forward_logits(flat, lay, rows, out=None, ws_owner=None):
     n = rows.numel()
+    dev = flat.device
     if out is None:
-        out = torch.empty(n, dtype=torch.float32, device=flat.device)
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+    need = int(L.hip().ncf_forward_workspace_bytes(L.ctypes.byref(lay), n))
+    ws = _ws(ws_owner if ws_owner is not None else _scratch, "_ncf_fwd_ws", need, dev)
     L.check(L.hip().ncf_forward(L.ctypes.byref(lay), flat.data_ptr(), rows.data_ptr(), n, out.data_ptr(),
-                                L.stream_ptr(flat.device)), "ncf_forward")
+                                None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel() * 4,
+                                L.stream_ptr(dev)), "ncf_forward")
     return out
 
 
-def fused_backward(flat, lay, rows, dlogit, gflat, slab, ctl):
+def new_workspace(lay, rows, dev):
+    """ncf_train_step workspace for up to `rows` rows per launch (float32 storage)."""
+    need = int(L.hip().ncf_workspace_bytes(L.ctypes.byref(lay), int(rows)))
+    if need < 0:
+        raise ValueError("ncf_workspace_bytes failed")
+    return torch.empty((need + 3) // 4, dtype=torch.float32, device=dev)
+
+
+def fused_backward(flat, lay, rows, dlogit, gflat, ws, ctl):
     """grads of sum_i dlogit[i] * logit[i] into gflat (zero-initialised)."""
     n = rows.numel()
     dev = flat.device
     st = L.stream_ptr(dev)
     L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
                                    dlogit.data_ptr(), ctl.data_ptr(), int(n), 1, 0, L.DZ_DLOGIT,
-                                   slab.data_ptr(), None, st), "ncf_train_step")
-    L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st),
+                                   ws.data_ptr(), ws.numel() * 4, None, st), "ncf_train_step")
+    L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), ws.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st),
             "ncf_reduce_slab")
 
 
-def new_slab(lay, dev):
-    stride = int(L.hip().ncf_slab_stride(L.ctypes.byref(lay)))
-    return torch.empty((L.hip().ncf_slab_rows(), stride), dtype=torch.float32, device=dev)
+class _Scratch:
+    pass
+
+
+_scratch = _Scratch()
 
 
 def new_ctl(n_total, dev, batch=0, adam_t=0):
@@ -155,7 +180,7 @@ class _NCFFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, rows, model, *params):
         flat, lay = model._ncf_flat, model._ncf_layout
-        logits = forward_logits(flat, lay, rows)
+        logits = forward_logits(flat, lay, rows, ws_owner=model)
         ctx.model = model
         ctx.save_for_backward(rows)
         return logits
@@ -167,10 +192,10 @@ class _NCFFunction(torch.autograd.Function):
         flat, lay = model._ncf_flat, model._ncf_layout
         dev = flat.device
         gflat = torch.zeros(int(lay.total), dtype=torch.float32, device=dev)
-        slab = new_slab(lay, dev)
+        ws = new_workspace(lay, rows.numel(), dev)
         ctl = new_ctl(rows.numel(), dev)
         dlogit = grad_out.contiguous().to(torch.float32)
-        fused_backward(flat, lay, rows, dlogit, gflat, slab, ctl)
+        fused_backward(flat, lay, rows, dlogit, gflat, ws, ctl)
         grads = []
         for (p, off), act in zip(_segments(model, lay), active_mask(model)):
             grads.append(gflat[off:off + p.numel()].view_as(p) if act and p.requires_grad else None)
@@ -193,4 +218,4 @@ def ncf_forward(model, user, item):
     rows = pack_rows(u, i)
     if torch.is_grad_enabled() and any(p.requires_grad for p in model.ordered_params()):
         return _NCFFunction.apply(rows, model, *model.ordered_params())
-    return forward_logits(flat, lay, rows)
+    return forward_logits(flat, lay, rows, ws_owner=model)

@@ -105,14 +105,26 @@ def test_engine_trajectory_vs_golden(golden, mt, opt, use_graph):
     assert eng.state_step() == T
 
 
-@pytest.mark.parametrize("cfg", ["C2", "C3", "default"])
+ONE_STEP = {  # name: (model_type, f, L, B, expected path)
+    "C2": ("NeuMF-end", 8, 3, 1024, 1), "C3": ("NeuMF-end", 16, 3, 8192, 1),
+    "default": ("NeuMF-end", 32, 2, 4096, 1),
+    # layered path: tower too large for LDS, or factor_num without a fused kernel
+    "cli-default-32x3": ("NeuMF-end", 32, 3, 4096, 2), "stress-64x4": ("NeuMF-end", 64, 4, 1000, 2),
+    "odd-f6": ("NeuMF-end", 6, 3, 3001, 2), "mlp-f11": ("MLP", 11, 2, 777, 2),
+    "gmf-f5": ("GMF", 5, 1, 2000, 2), "pre-f12": ("NeuMF-pre", 12, 2, 513, 2),
+    "mlp-f1": ("MLP", 1, 1, 300, 2),
+}
+
+
+@pytest.mark.parametrize("cfg", list(ONE_STEP))
 def test_one_step_grads_vs_oracle(cfg):
-    """Full-size shapes (ml-1m ids): logits, loss and every gradient of one step."""
+    """Full-size id spaces (ml-1m): logits, loss and every gradient of one step."""
     import ncf_amd._lib as L
     from ncf_amd import ops
-    f, Lyr, B = {"C2": (8, 3, 1024), "C3": (16, 3, 8192), "default": (32, 2, 4096)}[cfg]
+    mt, f, Lyr, B, path = ONE_STEP[cfg]
+    assert L.supported(mt, f, Lyr) == path
     U, I = 6041, 3707
-    ref, m = _models("NeuMF-end", f, Lyr, U=U, I=I, seed=11)
+    ref, m = _models(mt, f, Lyr, U=U, I=I, seed=11)
     rng = np.random.default_rng(3)
     users = rng.integers(0, U, B)
     items = np.minimum(rng.zipf(1.3, B) - 1, I - 1)  # hot items: heavy atomic contention
@@ -120,7 +132,7 @@ def test_one_step_grads_vs_oracle(cfg):
     logits_ref, loss_ref, grads_ref = O.forward_backward(ref, users, items, labels)
     flat, lay = ops.ensure_flat(m)
     gflat = torch.zeros(int(lay.total), device=DEV)
-    slab = ops.new_slab(lay, DEV)
+    ws = ops.new_workspace(lay, B, DEV)
     ctl = ops.new_ctl(B, DEV)
     u = torch.as_tensor(users, dtype=torch.int32, device=DEV)
     it = torch.as_tensor(items, dtype=torch.int32, device=DEV)
@@ -130,23 +142,27 @@ def test_one_step_grads_vs_oracle(cfg):
     rows = ops.pack_rows(u, it, y)
     L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
                                    None, ctl.data_ptr(), B, 1, 0, L.DZ_BCE,
-                                   slab.data_ptr(), logits.data_ptr(), st), "train")
-    L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st), "reduce")
+                                   ws.data_ptr(), ws.numel() * 4, logits.data_ptr(), st), "train")
+    L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), ws.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st), "reduce")
     torch.cuda.synchronize()
     np.testing.assert_allclose(logits.cpu().numpy(), logits_ref.numpy(), rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(gflat[lay.loss_slot].item(), loss_ref, rtol=1e-5)
     for (p, off), (name, _) in zip(ops._segments(m, lay), m.named_parameters()):
         got = gflat[off:off + p.numel()].view_as(p).cpu().numpy()
-        _close_grad(got, grads_ref[name].numpy(), name)
+        if name in grads_ref:
+            _close_grad(got, grads_ref[name].numpy(), name)
+        else:  # unused in this model type (reference grad None): nothing may be written
+            assert not got.any(), name
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_rank_shards_sum_to_full_batch(world):
+@pytest.mark.parametrize("f,Lyr", [(16, 3), (32, 3)])
+def test_rank_shards_sum_to_full_batch(world, f, Lyr):
     """DP decomposition: sum over ranks of shard grads == single-device grads."""
     import ncf_amd._lib as L
     from ncf_amd import ops
     U, I, B = 6041, 3707, 3000
-    _, m = _models("NeuMF-end", 16, 3, U=U, I=I, seed=5)
+    _, m = _models("NeuMF-end", f, Lyr, U=U, I=I, seed=5)
     flat, lay = ops.ensure_flat(m)
     rng = np.random.default_rng(9)
     u = torch.as_tensor(rng.integers(0, U, B), dtype=torch.int32, device=DEV)
@@ -157,12 +173,12 @@ def test_rank_shards_sum_to_full_batch(world):
 
     def run(world, rank):
         gflat = torch.zeros(int(lay.total), device=DEV)
-        slab = ops.new_slab(lay, DEV)
+        ws = ops.new_workspace(lay, (B + world - 1) // world, DEV)
         ctl = ops.new_ctl(B, DEV)
         L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
                                        None, ctl.data_ptr(), B, world, rank, L.DZ_BCE,
-                                       slab.data_ptr(), None, st), "train")
-        L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), slab.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st), "reduce")
+                                       ws.data_ptr(), ws.numel() * 4, None, st), "train")
+        L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), ws.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st), "reduce")
         return gflat
     full = run(1, 0)
     parts = sum(run(world, r) for r in range(world))
@@ -267,3 +283,51 @@ def test_prepare_epoch_batches_grouped_by_item(n, bs, n_items, hot):
     for b0 in range(0, n, bs):
         sl = slice(b0, min(n, b0 + bs))
         assert np.array_equal(np.sort(exp2[sl]), np.sort(out2[sl]))
+
+
+LAYERED = [("NeuMF-end", 32, 3), ("MLP", 6, 2), ("GMF", 5, 1), ("NeuMF-pre", 64, 4)]
+
+
+@pytest.mark.parametrize("mt,f,Lyr", LAYERED)
+def test_layered_module_autograd_and_forward(mt, f, Lyr):
+    """NCF.forward / autograd on the layered path vs the oracle, incl. edge sizes."""
+    import ncf_amd._lib as L
+    assert L.supported(mt, f, Lyr) == L.PATH_LAYERED
+    ref, m = _models(mt, f, Lyr, U=300, I=500, seed=8)
+    for n in (1, 63, 64, 65, 1000):
+        rng = np.random.default_rng(n)
+        u = rng.integers(0, 300, n)
+        i = rng.integers(0, 500, n)
+        y = (rng.random(n) < 0.3).astype(np.int64)
+        lg_ref, loss_ref, g_ref = O.forward_backward(ref, u, i, y)
+        m.zero_grad(set_to_none=True)
+        pred = m(torch.from_numpy(u).to(DEV), torch.from_numpy(i).to(DEV))
+        np.testing.assert_allclose(pred.detach().cpu().numpy(), lg_ref.numpy(), rtol=1e-5, atol=1e-7)
+        loss = torch.nn.BCEWithLogitsLoss()(pred, torch.from_numpy(y).float().to(DEV))
+        np.testing.assert_allclose(loss.item(), loss_ref, rtol=1e-5)
+        loss.backward()
+        for k, p in m.named_parameters():
+            if k in g_ref:
+                _close_grad(p.grad.cpu().numpy(), g_ref[k].numpy(), f"{k} n={n}")
+            else:
+                assert p.grad is None, k
+
+
+@pytest.mark.parametrize("mt,f,Lyr", [("NeuMF-end", 32, 3), ("GMF", 5, 1)])
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_layered_engine_trajectory_vs_oracle(mt, f, Lyr, use_graph):
+    """30 fused-engine Adam steps on the layered path vs torch.optim.Adam on the oracle."""
+    T, B = 30, 512
+    ref, m, eng = _engine_for(mt, f, Lyr, 200, 300, 6)
+    rng = np.random.default_rng(12)
+    users = rng.integers(0, 200, (T, B))
+    items = rng.integers(0, 300, (T, B))
+    labels = (rng.random((T, B)) < 0.2).astype(np.int64)
+    _stream(eng, users, items, labels, B)
+    eng.run(T, use_graph=use_graph)
+    torch.cuda.synchronize()
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    losses = O.train_steps(ref, opt, users, items, labels)
+    np.testing.assert_allclose(eng.epoch_losses()[:T], losses, rtol=1e-5)
+    for (k, v), (k2, v2) in zip(m.state_dict().items(), ref.state_dict().items()):
+        np.testing.assert_allclose(v.cpu().numpy(), v2.numpy(), rtol=1e-4, atol=1e-6, err_msg=k)

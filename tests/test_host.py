@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol(header, lib):
 
 def test_abi_version_and_layout():
     import ncf_amd._lib as L
-    assert L.hip().ncf_abi_version() == L.ABI_VERSION == 2
+    assert L.hip().ncf_abi_version() == L.ABI_VERSION == 3
     for U, I, f, nl, mt in ((944, 1683, 8, 3, "NeuMF-end"), (6041, 3707, 16, 3, "NeuMF-end"), (50, 80, 8, 1, "GMF")):
         lay = L.layout(U, I, f, nl, mt)
         from ncf_amd.models import NCF
@@ -43,7 +43,17 @@ def test_abi_version_and_layout():
         assert lay.tower_begin == lay.w[0] and lay.loss_slot == lay.tower_begin + lay.tower_len
         assert lay.total >= lay.loss_slot + 1
         assert L.hip().ncf_slab_stride(ctypes.byref(lay)) == lay.tower_len + 64
-    assert L.supported("NeuMF-end", 16, 3) and L.supported("GMF", 8, 3) and not L.supported("NeuMF-end", 64, 4)
+    assert L.supported("NeuMF-end", 16, 3) == L.supported("GMF", 8, 3) == L.PATH_FUSED
+    # towers too large for LDS and factor sizes without a fused kernel take the layered path
+    for mt, f, nl in [("NeuMF-end", 64, 4), ("NeuMF-end", 32, 3), ("MLP", 6, 2), ("GMF", 5, 1)]:
+        assert L.supported(mt, f, nl) == L.PATH_LAYERED
+    assert L.supported("NeuMF-end", 16, 5) == 0  # num_layers > 4: no layout
+    lay = L.layout(6041, 3707, 64, 4, "NeuMF-end")
+    ws = L.hip().ncf_workspace_bytes(ctypes.byref(lay), 65536)
+    dm = 64 * 8
+    acts = 65536 * (dm + dm // 2 + dm // 4 + dm // 8) + 2 * 65536 * dm
+    assert acts * 4 <= ws <= (acts + lay.tower_len + 64 * 8) * 4
+    assert L.hip().ncf_forward_workspace_bytes(ctypes.byref(L.layout(6041, 3707, 16, 3, "NeuMF-end")), 10 ** 6) == 0
 
 
 def test_product_sampler_bit_exact(golden):
