@@ -37,6 +37,8 @@ CONFIGS = {
     "c3": ("ml-1m", 16, 3, 65536),     # headline: NeuMF-64 (MLP [128,64,32,16])
     "c2": ("ml-1m", 8, 3, 1024),       # NeuMF [64,32,16,8], bs 1024
     "c4": ("ml-20m", 16, 3, 65536),    # ml-20m shape
+    "cli": ("ml-1m", 32, 3, 65536),    # train_neumf.py --num_layers 3 with the config's factor_num 32 (layered path)
+    "stress": ("ml-1m", 64, 4, 65536), # NCF(64,4): MLP [1024,512,256,128,64] (layered path)
 }
 
 
@@ -231,6 +233,8 @@ def main():
     P = sum(p.numel() for p in model.parameters())
     adam_bytes = 32 * P  # read p,g,m,v; write p,m,v,g(=0)
     traffic, traffic_src = pmc_traffic(f, nl)
+    import ncf_amd._lib as L
+    path = L.supported("NeuMF-end", f, nl)
 
     # ---- quality: HR@10 / NDCG@10 on the leave-one-out test set ---------------
     hr10 = ndcg10 = None
@@ -266,7 +270,8 @@ def main():
                        "hip_graph": use_graph},
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": 157.3, "unit": "TFLOP/s",
                          "frac": achieved_tf / 157.3, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "ncf_step_kernel<16,3,NeuMF> (fused fwd+bwd)",
+                         "kernel": (f"ncf_step_kernel<{f},{nl},NeuMF> (fused fwd+bwd)" if path == 1 else
+                                    "layered path: all kernels of ncf_train_step (fwd/predict/bwd GEMMs)"),
                          "flops_per_launch": flops, "kernel_ms": ms},
             "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": 8000.0, "unit": "GB/s",
                              "frac": achieved_gbs / 8000.0, "bytes_per_launch": bytes_launch,

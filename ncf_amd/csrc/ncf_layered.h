@@ -7,6 +7,8 @@
 
 namespace ncf {
 
+constexpr int LYR_MAX_FACTOR = 256;  // predict kernel: <= 4 features per lane
+
 static inline int64_t rup64(int64_t x) { return (x + 63) / 64 * 64; }
 
 struct LyrArgs {

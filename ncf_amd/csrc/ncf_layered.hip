@@ -320,8 +320,10 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
 
 // ---------------------------------------------------------------------------
 // Predict + loss + GMF backward.  G lanes per row (G = min(64, pow2 >= F)),
-// feature f handled by lane f % G.  Block partials of dwp / dbp / loss in LDS,
-// one global atomic per value per block.
+// feature f handled by lane f % G, slot f / G (< PSLOTS).  Each block loops over
+// row groups; dwp / dbp / loss accumulate in registers across its rows and are
+// combined once per block (LDS, then one global atomic per value).
+constexpr int PSLOTS = 4;  // F <= 256
 template <bool TRAIN>
 __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float* __restrict__ HL,
                                                           float* __restrict__ Dout, int64_t R, int G) {
@@ -336,53 +338,79 @@ __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float
     const int t = threadIdx.x;
     if (TRAIN) {
         for (int e = t; e < P + 2; e += GNT) red[e] = 0.f;
-        __syncthreads();
     }
-    const int rows_per_block = GNT / G;
+    const int rpb = GNT / G;
     const int gl = t % G;
-    const int64_t m = (int64_t)blockIdx.x * rows_per_block + t / G;
-    int u, it;
-    row_ids(a, s, m, u, it);
-    const bool valid = m < R && u >= 0;
-    const int uu = u < 0 ? 0 : u, ii = it < 0 ? 0 : it;
-    float part = 0.f;
-    if (valid) {
-        for (int f = gl; f < F; f += G) {
-            if (gmf) part += wp[f] * (prm[lay.ug + (int64_t)uu * F + f] * prm[lay.ig + (int64_t)ii * F + f]);
-            if (mlp) part += wp[Pg + f] * HL[m * F + f];
+    float accG[PSLOTS], accM[PSLOTS];
+#pragma unroll
+    for (int q = 0; q < PSLOTS; ++q) accG[q] = accM[q] = 0.f;
+    float accB = 0.f, accL = 0.f;
+    const float bp = prm[lay.bp];
+    for (int64_t m0 = (int64_t)blockIdx.x * rpb; m0 < R; m0 += (int64_t)gridDim.x * rpb) {
+        const int64_t m = m0 + t / G;
+        int u, it;
+        row_ids(a, s, m, u, it);
+        const bool valid = m < R && u >= 0;
+        const int uu = u < 0 ? 0 : u, ii = it < 0 ? 0 : it;
+        float part = 0.f;
+        if (valid) {
+#pragma unroll
+            for (int q = 0; q < PSLOTS; ++q) {
+                const int f = gl + q * G;
+                if (f >= F) break;
+                if (gmf) part += wp[f] * (prm[lay.ug + (int64_t)uu * F + f] * prm[lay.ig + (int64_t)ii * F + f]);
+                if (mlp) part += wp[Pg + f] * HL[m * F + f];
+            }
+        }
+        for (int o = G >> 1; o >= 1; o >>= 1) part += __shfl_xor(part, o, 64);
+        const float z = part + bp;
+        if (valid && gl == 0 && a.logits_out != nullptr) a.logits_out[m] = z;
+        if constexpr (TRAIN) {
+            if (valid) {
+                float dz;
+                const uint64_t rw = a.rows[s.base + m];
+                if (a.dz_mode == NCF_DZ_BCE) {
+                    const float y = (float)(uint32_t)(rw >> 63);
+                    dz = (sigmoidf_(z) - y) / s.gb;
+                    if (gl == 0) accL += bce_loss(z, y) / s.gb;
+                } else {
+                    dz = a.dlogit[s.base + m];
+                }
+                if (gl == 0) accB += dz;
+#pragma unroll
+                for (int q = 0; q < PSLOTS; ++q) {
+                    const int f = gl + q * G;
+                    if (f >= F) break;
+                    if (gmf) {
+                        const float ug = prm[lay.ug + (int64_t)uu * F + f], ig = prm[lay.ig + (int64_t)ii * F + f];
+                        accG[q] += dz * (ug * ig);
+                        const float dg = dz * wp[f];
+                        atomicAdd(a.grads + lay.ug + (int64_t)uu * F + f, dg * ig);
+                        atomicAdd(a.grads + lay.ig + (int64_t)ii * F + f, dg * ug);
+                    }
+                    if (mlp) {
+                        const float h = HL[m * F + f];
+                        accM[q] += dz * h;
+                        Dout[m * F + f] = h > 0.f ? dz * wp[Pg + f] : 0.f;
+                    }
+                }
+            } else if (mlp && m < R) {
+                for (int f = gl; f < F; f += G) Dout[m * F + f] = 0.f;
+            }
         }
     }
-    for (int o = G >> 1; o >= 1; o >>= 1) part += __shfl_xor(part, o, 64);
-    const float z = part + prm[lay.bp];
-    if (valid && gl == 0 && a.logits_out != nullptr) a.logits_out[m] = z;
     if constexpr (TRAIN) {
-        float dz = 0.f;
-        if (valid) {
-            const uint64_t rw = a.rows[s.base + m];
-            if (a.dz_mode == NCF_DZ_BCE) {
-                const float y = (float)(uint32_t)(rw >> 63);
-                dz = (sigmoidf_(z) - y) / s.gb;
-                if (gl == 0) atomicAdd(&red[P + 1], bce_loss(z, y) / s.gb);
-            } else {
-                dz = a.dlogit[s.base + m];
-            }
-            if (gl == 0) atomicAdd(&red[P], dz);
-            for (int f = gl; f < F; f += G) {
-                if (gmf) {
-                    const float ug = prm[lay.ug + (int64_t)uu * F + f], ig = prm[lay.ig + (int64_t)ii * F + f];
-                    atomicAdd(&red[f], dz * (ug * ig));
-                    const float dg = dz * wp[f];
-                    atomicAdd(a.grads + lay.ug + (int64_t)uu * F + f, dg * ig);
-                    atomicAdd(a.grads + lay.ig + (int64_t)ii * F + f, dg * ug);
-                }
-                if (mlp) {
-                    const float h = HL[m * F + f];
-                    atomicAdd(&red[Pg + f], dz * h);
-                    Dout[m * F + f] = h > 0.f ? dz * wp[Pg + f] : 0.f;
-                }
-            }
-        } else if (mlp && m < R) {
-            for (int f = gl; f < F; f += G) Dout[m * F + f] = 0.f;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PSLOTS; ++q) {
+            const int f = gl + q * G;
+            if (f >= F) break;
+            if (gmf) atomicAdd(&red[f], accG[q]);
+            if (mlp) atomicAdd(&red[Pg + f], accM[q]);
+        }
+        if (gl == 0) {
+            atomicAdd(&red[P], accB);
+            atomicAdd(&red[P + 1], accL);
         }
         __syncthreads();
         const int64_t tb = lay.tower_begin;
@@ -413,6 +441,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
     const int L = lay.num_layers, F = lay.factor_num;
     const int DM = F << (L - 1);
     const bool mlp = lay.model_type != NCF_MODEL_GMF;
+    if (F > LYR_MAX_FACTOR) return NCF_E_UNSUPPORTED;
     float* slab = ws;
     a.slab = slab;
     float* H[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -446,7 +475,9 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
     while (G < F && G < 64) G <<= 1;
     const int P = (lay.model_type == NCF_MODEL_NEUMF ? 2 : 1) * F;
     const int64_t rpb = GNT / G;
-    const unsigned pg = (unsigned)((R + rpb - 1) / rpb);
+    int64_t pgl = (R + rpb - 1) / rpb;
+    if (pgl > 2048) pgl = 2048;  // blocks loop over row groups beyond this
+    const unsigned pg = (unsigned)pgl;
     const size_t lds = (size_t)(P + 2) * 4;
     float* Dtop = Da;
     if (train)
@@ -462,7 +493,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
         const int K = (2 * DM) >> k, J = K / 2;
         // weight gradient: split the rows so the launch has ~512 blocks
         const int64_t tiles = (int64_t)((J + GBM - 1) / GBM) * ((K + 1 + GBN - 1) / GBN);
-        int64_t splits = 512 / tiles;
+        int64_t splits = 1024 / tiles;
         const int64_t max_splits = (R + 255) / 256;
         if (splits > max_splits) splits = max_splits;
         if (splits < 1) splits = 1;

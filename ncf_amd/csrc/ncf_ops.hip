@@ -551,7 +551,8 @@ static const KernelEntry* fused_entry(const ncf_layout* lay) {
 int ncf_supported(int mode, int F, int L) {
     ncf_layout lay;
     if (ncf_layout_init(1, 1, F, L, mode, &lay) != NCF_OK) return 0;
-    return fused_entry(&lay) ? NCF_PATH_FUSED : NCF_PATH_LAYERED;
+    if (fused_entry(&lay)) return NCF_PATH_FUSED;
+    return F <= LYR_MAX_FACTOR ? NCF_PATH_LAYERED : 0;
 }
 
 int64_t ncf_workspace_bytes(const ncf_layout* lay, int64_t rows) {

@@ -2,7 +2,8 @@
 
 One optimizer step over one global batch is four launches on the current
 stream, with no host synchronisation and no per-step allocation, so the whole
-step is captured once into a hipGraph and replayed:
+step is captured once into a hipGraph and replayed (world > 1: two graphs
+with the all-reduce issued between them, see ``_capture_collective``):
 
   1. ``ncf_train_step``  fused gather / GMF / MFMA tower fwd / BCE / MFMA tower
                          bwd / embedding scatter-add   (models.py:97-118,
@@ -21,6 +22,7 @@ the single-device mean gradient of ``BCEWithLogitsLoss``.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -100,7 +102,8 @@ class TrainEngine:
         return (self.n_total + self.batch_size - 1) // self.batch_size
 
     # ------------------------------------------------------------------ step
-    def _step_body(self):
+    def _compute(self):
+        """Launches 1-2: fused (or layered) step + slab reduction (advances ctl)."""
         st = L.stream_ptr(self.device)
         lib = L.hip()
         lay = ctypes.byref(self.lay)
@@ -109,9 +112,17 @@ class TrainEngine:
                                    self.batch_size, self.world_size, self.rank, L.DZ_BCE,
                                    self.ws.data_ptr(), self.ws.numel() * 4, None, st), "ncf_train_step")
         L.check(lib.ncf_reduce_slab(lay, self.ws.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(), st), "ncf_reduce_slab")
+
+    def _allreduce(self):
+        """Launch 3 (world > 1): sum of the flat gradient over ranks (RCCL on ROCm)."""
         if self.world_size > 1:
             import torch.distributed as dist
             dist.all_reduce(self.grads, group=self.group)
+
+    def _optimize(self):
+        """Launch 4: dense Adam / SGD + grad zeroing + loss bookkeeping."""
+        st = L.stream_ptr(self.device)
+        lib = L.hip()
         hist_len = self.num_batches
         if self.optimizer == "adam":
             L.check(lib.ncf_adam_step(self.flat.data_ptr(), self.grads.data_ptr(), self.exp_avg.data_ptr(),
@@ -123,6 +134,11 @@ class TrainEngine:
             L.check(lib.ncf_sgd_step(self.flat.data_ptr(), self.grads.data_ptr(), self._ranges, self._nranges,
                                      self.ctl.data_ptr(), self.lr, self.lay.loss_slot,
                                      self.loss_hist.data_ptr(), hist_len, st), "ncf_sgd_step")
+
+    def _step_body(self):
+        self._compute()
+        self._allreduce()
+        self._optimize()
 
     def time_kernels(self, n_steps):
         """Run n_steps eager steps with HIP events around each launch (on the
@@ -194,18 +210,40 @@ class TrainEngine:
         """One optimizer step on global batch ctl.batch (eager launches)."""
         self._step_body()
 
-    def capture(self):
-        """Capture one step into a hipGraph (after at least one eager step)."""
+    @property
+    def _capture_collective(self):
+        """Capture the all-reduce inside the step graph (one graph per step).  Off by
+        default for world > 1: the step is then two graphs (compute, optimizer)
+        with the collective issued eagerly between them, which needs nothing of
+        the process group beyond a plain all_reduce (any backend)."""
+        return self.world_size == 1 or os.environ.get("NCF_CAPTURE_ALLREDUCE", "0") == "1"
+
+    def _graph_of(self, fn):
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s):
-                self._step_body()
+                fn()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        self._graph = g
-        self._graph_key = (self.batch_size, self.n_total, self.rows.data_ptr())
         return g
+
+    def capture(self):
+        """Capture the step into hipGraph(s) (after at least one eager step)."""
+        if self._capture_collective:
+            self._graph = (self._graph_of(self._step_body),)
+        else:
+            self._graph = (self._graph_of(self._compute), self._graph_of(self._optimize))
+        self._graph_key = (self.batch_size, self.n_total, self.rows.data_ptr())
+        return self._graph
+
+    def _replay(self):
+        if len(self._graph) == 1:
+            self._graph[0].replay()
+        else:
+            self._graph[0].replay()
+            self._allreduce()
+            self._graph[1].replay()
 
     def run(self, n_steps, use_graph=True):
         """n_steps consecutive optimizer steps (batches advance on device)."""
@@ -221,11 +259,9 @@ class TrainEngine:
             done = 1
             if n_steps <= 1:
                 return
-            # capture replays the *current* batch: rewind the counters it advanced
-            self.capture()
-            # the captured body was not executed during capture
+            self.capture()  # captured launches are recorded, not executed
         for _ in range(n_steps - done):
-            self._graph.replay()
+            self._replay()
 
     def epoch_losses(self):
         """Per-batch mean BCE of the last epoch (host copy)."""

@@ -1,0 +1,88 @@
+"""Data-parallel engine on the GPU: two ranks (gloo, both on cuda:0, spawned
+processes) run TrainEngine with world_size=2 -- row shards inside
+ncf_train_step, the flat-gradient all-reduce between the compute and optimizer
+graphs, replicated Adam -- and must (a) stay bitwise identical to each other
+and (b) match a single-rank run over the same global batches (per-step loss
+rtol 1e-5; parameters rtol 1e-4 / atol 1e-6: the summed shard gradients differ
+from the full-batch gradient only in fp32 summation order).
+
+RCCL needs one GPU per rank, which the single-GPU test box does not have; gloo
+all-reduces the same device buffer through the host, so everything but the
+transport is the bench's N>1 path."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+T, B = 12, 1000
+U, I = 300, 400
+
+
+def _batches():
+    rng = np.random.default_rng(5)
+    users = rng.integers(0, U, T * B)
+    items = rng.integers(0, I, T * B)
+    labels = (rng.random(T * B) < 0.2).astype(np.float32)
+    return users, items, labels
+
+
+def _run(world, rank, group, mt, f, nl, use_graph):
+    from ncf_amd import ops
+    from ncf_amd.engine import TrainEngine
+    from ncf_amd.models import NCF
+    torch.manual_seed(3)
+    m = NCF(U, I, f, nl, 0.0, mt).to("cuda:0")
+    eng = TrainEngine(m, lr=1e-3, world_size=world, rank=rank, process_group=group)
+    u, i, y = _batches()
+    rows = torch.as_tensor(ops.pack_rows_host(u, i, y), device="cuda:0")
+    eng.set_epoch_stream(rows, B)
+    eng.run(T, use_graph=use_graph)
+    torch.cuda.synchronize()
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+    return flat, eng.epoch_losses()[:T].copy()
+
+
+def _worker(rank, world, port, mt, f, nl, use_graph, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    flat, losses = _run(world, rank, dist.group.WORLD, mt, f, nl, use_graph)
+    q.put((rank, flat, losses))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("mt,f,nl,use_graph", [("NeuMF-end", 16, 3, True), ("NeuMF-end", 16, 3, False),
+                                               ("NeuMF-end", 32, 3, True)])
+def test_two_ranks_match_single_rank(mt, f, nl, use_graph):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mt, f, nl, use_graph, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, flat, losses = q.get(timeout=300)
+        res[r] = (flat, losses)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert np.array_equal(res[0][0], res[1][0]), "ranks diverged"
+    flat1, losses1 = _run(1, 0, None, mt, f, nl, use_graph)
+    np.testing.assert_allclose(res[0][1], losses1, rtol=1e-5)
+    np.testing.assert_allclose(res[0][0], flat1, rtol=1e-4, atol=1e-6)
