@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 3
+#define NCF_ABI_VERSION 4
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -65,13 +65,15 @@ typedef struct ncf_layout {
     int32_t user_num, item_num, factor_num, num_layers, model_type, pad_;
 } ncf_layout;
 
-/* Device-resident step control block (16-byte aligned, 4 x int64).  Lets a
+/* Device-resident step control block (16-byte aligned, 6 x int64).  Lets a
  * captured hipGraph replay consecutive batches with no host involvement. */
 typedef struct ncf_step_ctl {
-    int64_t batch;   /* global batch index inside the epoch stream            */
-    int64_t adam_t;  /* optimizer steps completed (torch Adam state['step'])  */
-    int64_t n_total; /* rows in the epoch stream (positives + negatives)      */
-    int64_t reserved; /* keep 0                                               */
+    int64_t batch;      /* global batch index inside the epoch stream             */
+    int64_t adam_t;     /* optimizer steps completed (torch Adam state['step'])   */
+    int64_t n_total;    /* rows in the epoch stream (positives + negatives)       */
+    int64_t reserved;   /* keep 0                                                */
+    int64_t snap_batch; /* written by ncf_train_step: the batch this step trains  */
+    int64_t snap_t;     /* written by ncf_train_step: adam_t + 1 (this step's t)  */
 } ncf_step_ctl;
 
 int ncf_abi_version(void);
@@ -119,7 +121,7 @@ int64_t ncf_slab_stride(const ncf_layout *lay);
  * logits_out (optional, may be NULL): per-row logits of this rank's rows.
  */
 int ncf_train_step(const ncf_layout *lay, const float *params, float *grads, const uint64_t *rows,
-                   const float *dlogit, const ncf_step_ctl *ctl, int64_t batch_global, int world,
+                   const float *dlogit, ncf_step_ctl *ctl, int64_t batch_global, int world,
                    int rank, int dz_mode, void *workspace, int64_t workspace_bytes,
                    float *logits_out, void *stream);
 
@@ -152,6 +154,20 @@ int ncf_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq
                   const int64_t *ranges, int nranges, ncf_step_ctl *ctl, double lr,
                   double beta1, double beta2, double eps, int64_t loss_slot, float *loss_hist,
                   int64_t hist_len, void *stream);
+
+/*
+ * ncf_reduce_slab + ncf_adam_step in one launch (single-process training: no
+ * gradient exchange between the two).  The tower/predict gradient is summed from
+ * the slab in the same fixed order and applied by Adam in the same block, without
+ * being stored; embedding ranges take the plain Adam path.  Reads the step from the
+ * snapshot ncf_train_step wrote (ctl->snap_t, ctl->snap_batch), then sets
+ * ctl->adam_t = snap_t and ctl->batch = snap_batch + 1, and records the loss into
+ * loss_hist[snap_batch % hist_len].
+ */
+int ncf_reduce_adam_step(const ncf_layout *lay, const void *workspace, float *params, float *grads,
+                         float *exp_avg, float *exp_avg_sq, const int64_t *ranges, int nranges,
+                         ncf_step_ctl *ctl, double lr, double beta1, double beta2, double eps,
+                         float *loss_hist, int64_t hist_len, void *stream);
 
 /* Plain SGD p -= lr * g (optim.SGD(lr*10) on the --pretraining path, train_neumf.py:87-88). */
 int ncf_sgd_step(float *params, float *grads, const int64_t *ranges, int nranges,

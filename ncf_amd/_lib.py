@@ -28,7 +28,7 @@ NCF_E_ARG = -2
 NCF_E_LAUNCH = -3
 MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
 DZ_BCE, DZ_DLOGIT = 0, 1
-ABI_VERSION = 3  # include/ncf_hip.h NCF_ABI_VERSION
+ABI_VERSION = 4  # include/ncf_hip.h NCF_ABI_VERSION
 PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
 
@@ -50,7 +50,8 @@ class NcfLayout(ctypes.Structure):
 
 
 class NcfStepCtl(ctypes.Structure):
-    _fields_ = [("batch", c_i64), ("adam_t", c_i64), ("n_total", c_i64), ("reserved", c_i64)]
+    _fields_ = [("batch", c_i64), ("adam_t", c_i64), ("n_total", c_i64), ("reserved", c_i64),
+                ("snap_batch", c_i64), ("snap_t", c_i64)]
 
 
 _HIP_PROTOS = {
@@ -71,6 +72,9 @@ _HIP_PROTOS = {
     "ncf_adam_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.c_int, c_vp,
                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                      c_i64, c_vp, c_i64, c_vp]),
+    "ncf_reduce_adam_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp,
+                                            ctypes.POINTER(c_i64), ctypes.c_int, c_vp, ctypes.c_double,
+                                            ctypes.c_double, ctypes.c_double, ctypes.c_double, c_vp, c_i64, c_vp]),
     "ncf_sgd_step": (ctypes.c_int, [c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.c_int, c_vp, ctypes.c_double,
                                     c_i64, c_vp, c_i64, c_vp]),
     "ncf_gather_epoch": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),

@@ -61,7 +61,7 @@ struct TrainArgs {
     float* grads;
     const uint64_t* rows;  // packed rows (NCF_ROW_PACK)
     const float* dlogit;   // NCF_DZ_DLOGIT: dL/dlogit per row (BCE: aliases rows, unused)
-    const ncf_step_ctl* ctl;
+    ncf_step_ctl* ctl;
     int64_t batch_global;
     int world, rank, dz_mode;
     float* slab;
@@ -76,6 +76,9 @@ constexpr int NSTAMP = 64;  // stamps per workgroup
 // Ablation switches for performance diagnosis (ncf_debug_set_diag); results are
 // wrong when any is set.
 constexpr int DIAG_NO_WGRAD = 2;  // skip the weight-gradient MFMAs
+constexpr int DIAG_NO_USER_SCATTER = 8;   // diag build only: skip the Um atomics
+constexpr int DIAG_NO_ITEM_SCATTER = 16;  // diag build only: skip the Im segment atomics
+constexpr int DIAG_NO_GMF_SCATTER = 32;   // diag build only: skip the Ug / Ig atomics
 constexpr int DIAG_PREP_DIRECT = 4;  // ncf_prepare_epoch: global-atomic histogram variant (still correct)
 
 struct KernelEntry {

@@ -17,7 +17,7 @@ struct LyrArgs {
     float* grads;            // train: dense gradient buffer (embedding scatter targets)
     const uint64_t* rows;    // packed rows (NCF_ROW_PACK)
     const float* dlogit;     // NCF_DZ_DLOGIT: dL/dlogit per row
-    const ncf_step_ctl* ctl; // train: batch selection; nullptr = forward over fwd_n rows
+    ncf_step_ctl* ctl;       // train: batch selection; nullptr = forward over fwd_n rows
     int64_t batch_global, fwd_n;
     int world, rank, dz_mode;
     float* slab;             // one row [tower_len + 64] of tower/predict partials (+ loss)

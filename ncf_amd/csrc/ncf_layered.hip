@@ -338,6 +338,10 @@ __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float
     const int t = threadIdx.x;
     if (TRAIN) {
         for (int e = t; e < P + 2; e += GNT) red[e] = 0.f;
+        if (blockIdx.x == 0 && t == 0) {  // step snapshot for ncf_reduce_adam_step
+            a.ctl->snap_batch = a.ctl->batch;
+            a.ctl->snap_t = a.ctl->adam_t + 1;
+        }
     }
     const int rpb = GNT / G;
     const int gl = t % G;

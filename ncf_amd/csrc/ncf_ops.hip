@@ -163,6 +163,102 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* 
 }
 
 // ---------------------------------------------------------------------------
+// ncf_reduce_adam_step: blocks [0, nA) each reduce 64 slab columns (the order of
+// reduce_slab_kernel) and apply Adam to the active ones in place; blocks
+// [nA, grid) run the plain Adam over the embedding ranges RE.  t and the batch
+// come from the snapshot the train step wrote; block 0 commits them.
+__device__ __forceinline__ bool in_ranges(const Ranges& R, int64_t i) {
+    for (int k = 0; k < R.n; ++k)
+        if (i >= R.begin[k] && i < R.begin[k] + (R.prefix[k + 1] - R.prefix[k]) * 4) return true;
+    return false;
+}
+
+__global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restrict__ slab, int lo, int stride, int rows,
+                                                          int nA, int64_t tb, int64_t tower_len, float* __restrict__ p,
+                                                          float* __restrict__ g, float* __restrict__ m,
+                                                          float* __restrict__ v, Ranges R, Ranges RE,
+                                                          ncf_step_ctl* ctl, double lr, double beta1, double beta2,
+                                                          float eps, float* loss_hist, int64_t hist_len) {
+#pragma clang fp contract(off)
+    __shared__ float sc[2];
+    __shared__ f4 part[16][16];
+    const int64_t t_step = ctl->snap_t;
+    const int64_t b_step = ctl->snap_batch;
+    if (threadIdx.x == 0) {
+        const double t = (double)t_step;
+        const double bc1 = 1.0 - pow(beta1, t);
+        const double bc2 = 1.0 - pow(beta2, t);
+        sc[0] = (float)(-(lr / bc1));
+        sc[1] = (float)sqrt(bc2);
+    }
+    __syncthreads();
+    const float neg_step = sc[0], bc2s = sc[1];
+    const float w1 = (float)(1.0 - beta1);
+    const float b2 = (float)beta2;
+    const float omb2 = (float)(1.0 - beta2);
+    if ((int)blockIdx.x < nA) {
+        const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
+        const int j = lo + (blockIdx.x * 16 + c4) * 4;
+        f4 s = f4{0.f, 0.f, 0.f, 0.f};
+        if (j < stride) {
+            const float* q = slab + (int64_t)rg * stride + j;
+            const int per = rows / 16;
+#pragma unroll 16
+            for (int r = 0; r < per; ++r) {
+                const f4 x = *reinterpret_cast<const f4*>(q + (int64_t)r * 16 * stride);
+                s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+            }
+            if (rg < rows - 16 * per) {
+                const f4 x = *reinterpret_cast<const f4*>(q + (int64_t)per * 16 * stride);
+                s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+            }
+        }
+        part[rg][c4] = s;
+        __syncthreads();
+        if (rg == 0 && j < stride) {
+            f4 gs = part[0][c4];
+#pragma unroll
+            for (int q = 1; q < 16; ++q) {
+                const f4 x = part[q][c4];
+                gs.x += x.x; gs.y += x.y; gs.z += x.z; gs.w += x.w;
+            }
+            const int64_t i = tb + j;
+            if (j == tower_len) {
+                if (loss_hist != nullptr && hist_len > 0) loss_hist[((b_step % hist_len) + hist_len) % hist_len] = gs.x;
+            } else if (j < tower_len && in_ranges(R, i)) {
+                f4 pp = *reinterpret_cast<const f4*>(p + i);
+                f4 mm = *reinterpret_cast<const f4*>(m + i);
+                f4 vv = *reinterpret_cast<const f4*>(v + i);
+                adam_f4(pp, mm, vv, gs, w1, b2, omb2, bc2s, eps, neg_step);
+                *reinterpret_cast<f4*>(m + i) = mm;
+                *reinterpret_cast<f4*>(v + i) = vv;
+                *reinterpret_cast<f4*>(p + i) = pp;
+            }
+        }
+    } else {
+        const int64_t total = RE.prefix[RE.n];
+        const int64_t nthr = (int64_t)(gridDim.x - nA) * blockDim.x;
+        for (int64_t q = (int64_t)(blockIdx.x - nA) * blockDim.x + threadIdx.x; q < total; q += nthr) {
+            int which;
+            const int64_t i = range_locate(RE, q, &which);
+            const f4 gg = *reinterpret_cast<const f4*>(g + i);
+            f4 mm = *reinterpret_cast<const f4*>(m + i);
+            f4 vv = *reinterpret_cast<const f4*>(v + i);
+            f4 pp = *reinterpret_cast<const f4*>(p + i);
+            adam_f4(pp, mm, vv, gg, w1, b2, omb2, bc2s, eps, neg_step);
+            *reinterpret_cast<f4*>(m + i) = mm;
+            *reinterpret_cast<f4*>(v + i) = vv;
+            *reinterpret_cast<f4*>(p + i) = pp;
+            *reinterpret_cast<f4*>(g + i) = f4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // no other block of this launch reads these two
+        ctl->adam_t = t_step;
+        ctl->batch = b_step + 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Packed rows (include/ncf_hip.h NCF_ROW_PACK): u | item << 32 | label << 63.
 __device__ __forceinline__ int row_item(uint64_t r) { return (int)((r >> 32) & 0x7fffffffu); }
 
@@ -568,7 +664,7 @@ int64_t ncf_forward_workspace_bytes(const ncf_layout* lay, int64_t n) {
 }
 
 int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
-                   const float* dlogit, const ncf_step_ctl* ctl, int64_t batch_global, int world, int rank,
+                   const float* dlogit, ncf_step_ctl* ctl, int64_t batch_global, int world, int rank,
                    int dz_mode, void* workspace, int64_t workspace_bytes, float* logits_out, void* stream) {
     if (!lay || !params || !grads || !rows || !ctl || !workspace) return NCF_E_ARG;
     if (batch_global <= 0 || world < 1 || rank < 0 || rank >= world) return NCF_E_ARG;
@@ -684,6 +780,45 @@ int ncf_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(adam_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
                        exp_avg_sq, R, ctl, lr, beta1, beta2, (float)eps, loss_slot, loss_hist, hist_len);
+    return launch_status();
+}
+
+int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* params, float* grads, float* exp_avg,
+                         float* exp_avg_sq, const int64_t* ranges, int nranges, ncf_step_ctl* ctl, double lr,
+                         double beta1, double beta2, double eps, float* loss_hist, int64_t hist_len, void* stream) {
+    if (!lay || !workspace || !params || !grads || !exp_avg || !exp_avg_sq || !ranges || !ctl) return NCF_E_ARG;
+    int err = 0;
+    Ranges R = make_ranges(ranges, nranges, &err);
+    if (err) return NCF_E_ARG;
+    // embedding part of the active ranges: [begin, min(end, tower_begin))
+    int64_t er[16];
+    int ne = 0;
+    for (int i = 0; i < nranges; ++i) {
+        const int64_t b = ranges[2 * i];
+        const int64_t e = ranges[2 * i + 1] < lay->tower_begin ? ranges[2 * i + 1] : lay->tower_begin;
+        if (e > b) {
+            er[2 * ne] = b;
+            er[2 * ne + 1] = e;
+            ++ne;
+        }
+    }
+    Ranges RE;
+    memset(&RE, 0, sizeof(RE));
+    if (ne > 0) {
+        RE = make_ranges(er, ne, &err);
+        if (err) return NCF_E_ARG;
+    }
+    const int stride = (int)ncf_slab_stride(lay);
+    const int lo = lay->model_type == NCF_MODEL_GMF ? (int)(lay->wp - lay->tower_begin) : 0;
+    const int nA = (stride - lo + 63) / 64;
+    const int rows = fused_entry(lay) ? SLAB_ROWS : 1;
+    const int64_t etotal = RE.prefix[RE.n];
+    int64_t nB = (etotal + 255) / 256;
+    if (nB > 2048) nB = 2048;
+    hipLaunchKernelGGL(reduce_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
+                       static_cast<const float*>(workspace), lo, stride, rows, nA, lay->tower_begin, lay->tower_len,
+                       params, grads, exp_avg, exp_avg_sq, R, RE, ctl, lr, beta1, beta2, (float)eps, loss_hist,
+                       hist_len);
     return launch_status();
 }
 

@@ -64,6 +64,13 @@ __device__ __forceinline__ void stamp(const TrainArgs& a, int idx) {
 // embedding-gradient atomics -- at every barrier; nothing here needs that, so
 // only the wave's LDS ops are drained.  The "memory" clobber keeps the compiler
 // from moving LDS accesses across it.
+// Scatter ablations exist only in the diagnostics build (results wrong while set).
+#ifdef NCF_STAMPS
+#define DIAG_ON(a, f) (((a).diag & (f)) != 0)
+#else
+#define DIAG_ON(a, f) false
+#endif
+
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ void set_r(f4& v, int r, float x) {
@@ -118,6 +125,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         base = b0 + lo;
         nloc = hi - lo;
         gb_f = (float)gb;
+        if (blockIdx.x == 0 && tid == 0) {  // step snapshot for ncf_reduce_adam_step (fields no WG reads here)
+            a.ctl->snap_batch = a.ctl->batch;
+            a.ctl->snap_t = a.ctl->adam_t + 1;
+        }
     }
     const int64_t ntiles = (nloc + TILE_ROWS - 1) / TILE_ROWS;
     stamp(a, 0);
@@ -248,7 +259,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                     if (f < DM) sum += scr[row * S_::SCM + f];
                     const bool last = row == 15 || si[wr + row + 1] != it;
                     if (last) {
-                        if (it >= 0 && f < DM) atomicAdd(a.grads + lay.im + (int64_t)it * DM + f, sum);
+                        if (it >= 0 && f < DM && !DIAG_ON(a, DIAG_NO_ITEM_SCATTER)) atomicAdd(a.grads + lay.im + (int64_t)it * DM + f, sum);
                         sum = 0.f;
                     }
                 }
@@ -262,7 +273,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                 if (l < F) sum += sg[row * S_::SCG + l];
                 const bool last = row == 15 || si[wr + row + 1] != it;
                 if (last) {
-                    if (it >= 0 && l < F) atomicAdd(a.grads + lay.ig + (int64_t)it * F + l, sum);
+                    if (it >= 0 && l < F && !DIAG_ON(a, DIAG_NO_GMF_SCATTER)) atomicAdd(a.grads + lay.ig + (int64_t)it * F + l, sum);
                     sum = 0.f;
                 }
             }
@@ -429,7 +440,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                     const float dzq = sdz[q];
                     dWpG += dzq * (ugv[j] * igv[j]);
                     const float dgm = dzq * wpf;
-                    atomicAdd(a.grads + lay.ug + (int64_t)max(su[q], 0) * F + gf, dgm * igv[j]);
+                    if (!DIAG_ON(a, DIAG_NO_GMF_SCATTER)) atomicAdd(a.grads + lay.ug + (int64_t)max(su[q], 0) * F + gf, dgm * igv[j]);
                     gIg[j] = dgm * ugv[j];
                 }
             }
@@ -629,7 +640,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
                                 for (int f0 = 0; f0 < DM; f0 += FPI) {
                                     const int f = f0 + l % FPI;
-                                    atomicAdd(a.grads + lay.um + (int64_t)uu * DM + f, scr[q * S_::SCM + f]);
+                                    if (!DIAG_ON(a, DIAG_NO_USER_SCATTER)) atomicAdd(a.grads + lay.um + (int64_t)uu * DM + f, scr[q * S_::SCM + f]);
                                 }
                             }
                         } else {  // DM == 8: one 16-column tile, lanes c < 8 user, c >= 8 item

@@ -135,50 +135,61 @@ class TrainEngine:
                                      self.ctl.data_ptr(), self.lr, self.lay.loss_slot,
                                      self.loss_hist.data_ptr(), hist_len, st), "ncf_sgd_step")
 
+    @property
+    def _fused_optimizer(self):
+        """Single process + Adam: slab reduction and Adam in one launch
+        (ncf_reduce_adam_step); otherwise reduce, [all-reduce], optimizer."""
+        return self.world_size == 1 and self.optimizer == "adam" and os.environ.get("NCF_FUSED_ADAM", "1") == "1"
+
+    def _train_launch(self):
+        st = L.stream_ptr(self.device)
+        L.check(L.hip().ncf_train_step(ctypes.byref(self.lay), self.flat.data_ptr(), self.grads.data_ptr(),
+                                       self.rows.data_ptr(), None, self.ctl.data_ptr(), self.batch_size,
+                                       self.world_size, self.rank, L.DZ_BCE, self.ws.data_ptr(),
+                                       self.ws.numel() * 4, None, st), "ncf_train_step")
+
+    def _reduce_adam(self):
+        st = L.stream_ptr(self.device)
+        L.check(L.hip().ncf_reduce_adam_step(ctypes.byref(self.lay), self.ws.data_ptr(), self.flat.data_ptr(),
+                                             self.grads.data_ptr(), self.exp_avg.data_ptr(),
+                                             self.exp_avg_sq.data_ptr(), self._ranges, self._nranges,
+                                             self.ctl.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps,
+                                             self.loss_hist.data_ptr(), self.num_batches, st),
+                "ncf_reduce_adam_step")
+
     def _step_body(self):
+        if self._fused_optimizer:
+            self._train_launch()
+            self._reduce_adam()
+            return
         self._compute()
         self._allreduce()
         self._optimize()
 
     def time_kernels(self, n_steps):
-        """Run n_steps eager steps with HIP events around each launch (on the
-        stream the kernels run on) and return mean milliseconds per kernel."""
+        """Run n_steps eager steps with HIP events between the launches (on the
+        stream they run on) and return mean milliseconds per launch group."""
         st = torch.cuda.current_stream(self.device)
-        names = ["ncf_train_step", "ncf_reduce_slab", "allreduce", "optimizer"]
-        acc = {k: 0.0 for k in names}
-        lib = L.hip()
-        lay = ctypes.byref(self.lay)
-        sp = L.stream_ptr(self.device)
+        if self._fused_optimizer:
+            parts = [("ncf_train_step", self._train_launch), ("ncf_reduce_adam_step", self._reduce_adam)]
+        else:
+            parts = [("ncf_train_step", self._train_launch),
+                     ("ncf_reduce_slab", lambda: L.check(L.hip().ncf_reduce_slab(
+                         ctypes.byref(self.lay), self.ws.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(),
+                         L.stream_ptr(self.device)), "ncf_reduce_slab")),
+                     ("allreduce", self._allreduce), ("optimizer", self._optimize)]
+        acc = {k: 0.0 for k, _ in parts}
         evs = []
         for _ in range(n_steps):
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(len(parts) + 1)]
             e[0].record(st)
-            L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.rows.data_ptr(),
-                                       None, self.ctl.data_ptr(),
-                                       self.batch_size, self.world_size, self.rank, L.DZ_BCE,
-                                       self.ws.data_ptr(), self.ws.numel() * 4, None, sp), "ncf_train_step")
-            e[1].record(st)
-            L.check(lib.ncf_reduce_slab(lay, self.ws.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(), sp), "ncf_reduce_slab")
-            e[2].record(st)
-            if self.world_size > 1:
-                import torch.distributed as dist
-                dist.all_reduce(self.grads, group=self.group)
-            e[3].record(st)
-            if self.optimizer == "adam":
-                L.check(lib.ncf_adam_step(self.flat.data_ptr(), self.grads.data_ptr(), self.exp_avg.data_ptr(),
-                                          self.exp_avg_sq.data_ptr(), self._ranges, self._nranges,
-                                          self.ctl.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps,
-                                          self.lay.loss_slot, self.loss_hist.data_ptr(), self.num_batches, sp),
-                        "ncf_adam_step")
-            else:
-                L.check(lib.ncf_sgd_step(self.flat.data_ptr(), self.grads.data_ptr(), self._ranges, self._nranges,
-                                         self.ctl.data_ptr(), self.lr, self.lay.loss_slot,
-                                         self.loss_hist.data_ptr(), self.num_batches, sp), "ncf_sgd_step")
-            e[4].record(st)
+            for k, (_, fn) in enumerate(parts):
+                fn()
+                e[k + 1].record(st)
             evs.append(e)
         torch.cuda.synchronize(self.device)
         for e in evs:
-            for k, name in enumerate(names):
+            for k, (name, _) in enumerate(parts):
                 acc[name] += e[k].elapsed_time(e[k + 1])
         return {k: v / max(1, n_steps) for k, v in acc.items()}
 

@@ -173,7 +173,8 @@ _scratch = _Scratch()
 
 
 def new_ctl(n_total, dev, batch=0, adam_t=0):
-    return torch.tensor([batch, adam_t, n_total, 0], dtype=torch.int64, device=dev)
+    """ncf_step_ctl: batch, adam_t, n_total, reserved, snap_batch, snap_t."""
+    return torch.tensor([batch, adam_t, n_total, 0, 0, 0], dtype=torch.int64, device=dev)
 
 
 class _NCFFunction(torch.autograd.Function):

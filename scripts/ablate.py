@@ -9,6 +9,8 @@ import sys
 import numpy as np
 import torch
 
+os.environ.setdefault("NCF_HIP_LIB", "diag")  # the scatter switches exist in the diag build only
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -24,13 +26,13 @@ def main():
         eng, model, ds, _ = bench.setup_engine(cfg, 1, 0, dev, None, rows)
         eng.run(3, use_graph=False)
         torch.cuda.synchronize()
-        variants = {"full": 0, "no_wgrad": 2}
+        variants = {"full": 0, "no_wgrad": 2, "no_user_scatter": 8, "no_item_scatter": 16,
+                    "no_gmf_scatter": 32, "no_scatter": 8 | 16 | 32}
         times = {k: [] for k in variants}
         for _ in range(5):
             for name, d in variants.items():
                 L.hip().ncf_debug_set_diag(d)
-                kt = eng.time_kernels(10)
-                times[name].append(kt["ncf_train_step"])
+                times[name].append(eng.time_train_kernel(20))
         L.hip().ncf_debug_set_diag(0)
         res[str(rows)] = {k: float(np.median(v)) for k, v in times.items()}
         res[str(rows) + "_other"] = eng.time_kernels(10)

@@ -331,3 +331,30 @@ def test_layered_engine_trajectory_vs_oracle(mt, f, Lyr, use_graph):
     np.testing.assert_allclose(eng.epoch_losses()[:T], losses, rtol=1e-5)
     for (k, v), (k2, v2) in zip(m.state_dict().items(), ref.state_dict().items()):
         np.testing.assert_allclose(v.cpu().numpy(), v2.numpy(), rtol=1e-4, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("mt,f,Lyr", [("NeuMF-end", 16, 3), ("GMF", 8, 1), ("NeuMF-end", 32, 3)])
+def test_fused_reduce_adam_bitwise_equals_separate_kernels(monkeypatch, mt, f, Lyr):
+    """ncf_reduce_adam_step == ncf_reduce_slab + ncf_adam_step (same slab summation
+    order, same Adam arithmetic).  Not bit for bit: the embedding gradients are f32
+    atomics whose order differs between any two runs, so parameters and losses are
+    held to rtol 1e-5; the step counters exactly."""
+    T, B = 15, 700
+    rng = np.random.default_rng(21)
+    users = rng.integers(0, 200, (T, B))
+    items = rng.integers(0, 300, (T, B))
+    labels = (rng.random((T, B)) < 0.2).astype(np.int64)
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("NCF_FUSED_ADAM", fused)
+        _, m, eng = _engine_for(mt, f, Lyr, 200, 300, 6)
+        assert eng._fused_optimizer == (fused == "1")
+        _stream(eng, users, items, labels, B)
+        eng.run(T, use_graph=True)
+        torch.cuda.synchronize()
+        out.append(([v.cpu().numpy().copy() for v in m.state_dict().values()], eng.epoch_losses()[:T].copy(),
+                    eng.ctl.cpu().numpy()[:2].copy()))
+    for a, b in zip(out[0][0], out[1][0]):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(out[0][1], out[1][1], rtol=1e-5)
+    assert np.array_equal(out[0][2], out[1][2]) and out[0][2][1] == T
