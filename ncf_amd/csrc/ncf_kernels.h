@@ -51,6 +51,10 @@ struct Shape {
     static_assert(P <= 128, "predict LDS region");
     __host__ __device__ static constexpr int TPW(int k) { return (MT(k) * KT(k) + NWAVES - 1) / NWAVES; }
     static constexpr int KT0 = MLP ? KT(0) : 1;
+    // Layer-0 wgrad after the embedding scatter (its atomics drain under the wgrad
+    // MFMAs) keeps the wgrad operands live through the dgrad: off where that
+    // exceeds the register file (NeuMF f=64).
+    static constexpr bool WGRAD0_LATE = !(MLP && GMF && F >= 64);
     static_assert(F >= 8 && F <= 64 && (F & (F - 1)) == 0, "factor_num must be 8..64, a power of 2");
     static_assert(L >= 1 && L <= 4, "num_layers must be 1..4");
 };

@@ -495,7 +495,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                         dbAcc[k] += s;
                     }
                     // wgrad: dW_k[out][in] += sum_rows dpre_k[row][out] * H_k[row][in]
-                    if constexpr (k == 0) {
+                    // (layer 0: after the dgrad and the embedding scatter, so the
+                    // scatter atomics drain under these MFMAs)
+                    auto wgrad0 = [&]() {
                         if (w < KT0 && !(a.diag & DIAG_NO_WGRAD)) {
 #pragma unroll
                             for (int mt = 0; mt < MT0; ++mt) {
@@ -520,6 +522,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                                 accW0[mt] = acc0;
                             }
                         }
+                    };
+                    if constexpr (k == 0) {
+                        if constexpr (!S_::WGRAD0_LATE) wgrad0();
+                        // (h) next tile's embedding fragments: before this tile's
+                        // scatter atomics, so the next tile waits on them only
+                        load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
                     } else {
                         constexpr int T = S_::MT(k) * S_::KT(k);
                         constexpr int tpw = S_::TPW(k);
@@ -553,14 +561,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                             }
                         }
                     }
-                    stamp(a, sb + 4 + 3 * (L - 1 - k));
-                    if constexpr (k == 0) {
-                        // (h) next tile's embedding fragments: after the layer-0 wgrad
-                        // (whose operand loads then wait on nothing younger than the
-                        // GMF atomics) and before this tile's scatter atomics (so
-                        // the next tile waits on them only, not on the atomics)
-                        load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
-                    }
+                    if constexpr (k >= 1) stamp(a, sb + 4 + 3 * (L - 1 - k));
                     // dgrad
                     const float* Ws = sW + S_::woff(k);
                     if constexpr (k >= 1) {
@@ -610,6 +611,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                                 __builtin_amdgcn_sched_barrier(0);
                             }
                         }
+                        // The layer-0 wgrad operands (bx, loaded in (d)) must be complete
+                        // before the scatter: consumed here, the wait is a counted one on
+                        // old loads; at their use after the branchy scatter it would
+                        // drain the atomics too.
+                        if constexpr (S_::WGRAD0_LATE) {
+#pragma unroll
+                            for (int i = 0; i < NWAVES * 4; ++i) asm volatile("" ::"v"(bx[i]));
+                        }
+                        stamp(a, sb + 4 + 3 * (L - 1));
                         // item half -> this wave's scratch rows (segment-reduced below);
                         // user half -> unconditional atomics (padding rows add 0 to row 0)
                         float* scr = sstage + w * S_::WAVE_STAGE + S_::R0;
@@ -654,8 +664,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                                 if (c < DM) atomicAdd(a.grads + lay.um + (int64_t)uu * DM + c, lane_get(acc[0], r));
                             }
                         }
+                        stamp(a, sb + 5 + 3 * (L - 1));
+                        if constexpr (S_::WGRAD0_LATE) wgrad0();
                     }
-                    stamp(a, sb + 5 + 3 * (L - 1 - k));
+                    if constexpr (k >= 1) stamp(a, sb + 5 + 3 * (L - 1 - k));
                 });
             } else {
                 // GMF-only model: item-side GMF rows, then publish next indices

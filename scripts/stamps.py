@@ -19,6 +19,8 @@ for t in range(4):
     for j in range(3):
         NAMES.update({b + 3 + 3 * j: f"t{t}:L{2-j}:stage+bar", b + 4 + 3 * j: f"t{t}:L{2-j}:wgrad",
                       b + 5 + 3 * j: f"t{t}:L{2-j}:dgrad"})
+    # layer 0 runs dgrad MFMA, then the scatter, then the wgrad
+    NAMES.update({b + 10: f"t{t}:L0:dgrad_mfma", b + 11: f"t{t}:L0:scatter", b + 13: f"t{t}:L0:wgrad+end-barrier"})
     NAMES[b + 13] = f"t{t}:end-barrier"
 NAMES.update({60: "epilogue:img", 61: "epilogue:store"})
 
