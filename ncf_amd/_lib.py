@@ -17,9 +17,10 @@ import threading
 import torch  # noqa: F401  (must precede loading libncf_hip.so)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# NCF_HIP_LIB=diag selects the diagnostics build (phase stamps compiled in)
-HIP_LIB_PATH = os.path.join(_HERE, "libncf_hip_diag.so" if os.environ.get("NCF_HIP_LIB") == "diag"
-                            else "libncf_hip.so")
+# NCF_HIP_LIB=<variant> selects ncf_amd/libncf_hip_<variant>.so (diag = phase stamps
+# compiled in; other variants are experiment builds of the Makefile's `variant` target)
+_VARIANT = os.environ.get("NCF_HIP_LIB", "")
+HIP_LIB_PATH = os.path.join(_HERE, f"libncf_hip_{_VARIANT}.so" if _VARIANT else "libncf_hip.so")
 SAMPLER_LIB_PATH = os.path.join(_HERE, "libncf_sampler.so")
 
 NCF_OK = 0

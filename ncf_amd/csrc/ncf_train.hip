@@ -551,7 +551,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                                         else
                                             acc0 = MFMA4(av, bv, acc0);
                                     }
+#ifndef NCF_WGRADK_FREE
                                     if (ws & 1) __builtin_amdgcn_sched_barrier(0);
+#endif
                                 }
                                 acc0.x += acc1.x;
                                 acc0.y += acc1.y;

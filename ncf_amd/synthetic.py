@@ -21,6 +21,7 @@ import os
 import numpy as np
 
 SHAPES = {
+    "tiny": (60, 400, 1_800),  # test-sized: script-compatibility tests
     "ml-100k": (943, 1682, 100_000),
     "ml-1m": (6040, 3706, 1_000_209),
     "ml-20m": (138_493, 26_744, 20_000_263),
