@@ -77,6 +77,7 @@ class TrainEngine:
         self.n_total = 0
         self.batch_size = None
         self._graph = None
+        self._graph_k = None
         self._graph_key = None
 
     # ------------------------------------------------------------------ data
@@ -239,12 +240,24 @@ class TrainEngine:
         torch.cuda.current_stream(self.device).wait_stream(s)
         return g
 
+    # steps unrolled into one graph when the collective is captured too (single
+    # process): fewer graph launches, no host work between consecutive steps
+    GRAPH_STEPS = int(os.environ.get("NCF_GRAPH_STEPS", "8"))
+
     def capture(self):
         """Capture the step into hipGraph(s) (after at least one eager step)."""
         if self._capture_collective:
             self._graph = (self._graph_of(self._step_body),)
+            k = self.GRAPH_STEPS
+            self._graph_k = None
+            if k > 1:
+                def body():
+                    for _ in range(k):
+                        self._step_body()
+                self._graph_k = self._graph_of(body)
         else:
             self._graph = (self._graph_of(self._compute), self._graph_of(self._optimize))
+            self._graph_k = None
         self._graph_key = (self.batch_size, self.n_total, self.rows.data_ptr())
         return self._graph
 
@@ -271,7 +284,13 @@ class TrainEngine:
             if n_steps <= 1:
                 return
             self.capture()  # captured launches are recorded, not executed
-        for _ in range(n_steps - done):
+        left = n_steps - done
+        if self._graph_k is not None:
+            k = self.GRAPH_STEPS
+            for _ in range(left // k):
+                self._graph_k.replay()
+            left %= k
+        for _ in range(left):
             self._replay()
 
     def epoch_losses(self):
