@@ -42,7 +42,23 @@ struct Shape {
     static constexpr int SCM = MLP ? DM + 4 : 0;
     static constexpr int SCG = GMF ? F + 4 : 0;
     static constexpr int SCR = 16 * (SCM + SCG);
-    static constexpr int WAVE_STAGE = R0 + (R1 > SCR ? R1 : SCR);
+    static constexpr int STAGE_OLD = R0 + (R1 > SCR ? R1 : SCR);
+    // Odd L: the layer-0 staging and the next tile's first staging (layer L-1) have
+    // the same parity, so without a barrier between tiles a fast wave would overwrite
+    // staging a slow wave still reads.  With two equal halves whose roles alternate
+    // by tile parity the tile-end barrier goes away (if the LDS budget allows).
+    static constexpr int RMAX = R0 > R1 ? R0 : R1;
+    static constexpr int HALF = RMAX > SCR ? RMAX : SCR;
+    static constexpr int STAGE_ALT = 2 * HALF;
+    static constexpr bool ALT_FITS = (W_TOTAL + 10 * TILE_ROWS + NWAVES * STAGE_ALT) * 4 <= LDS_LIMIT_BYTES;
+#ifdef NCF_KEEP_END_BARRIER  // experiment switch: the previous layout + tile-end barrier
+    static constexpr bool ALT = false;
+    static constexpr bool END_BARRIER = true;
+#else
+    static constexpr bool ALT = MLP && (L & 1) && ALT_FITS;
+    static constexpr bool END_BARRIER = !MLP || ((L & 1) && !ALT_FITS);
+#endif
+    static constexpr int WAVE_STAGE = ALT ? STAGE_ALT : STAGE_OLD;
     // su[2], si[2], labels[2] (double-buffered tile indices), zgmf, dz, then
     // 128 floats of biases (each layer's padded to 16*MT) and 128 of predict weights
     static constexpr int MISC = 10 * TILE_ROWS;

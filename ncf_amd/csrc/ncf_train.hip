@@ -97,6 +97,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 
     const int tid = threadIdx.x;
     const int w = tid >> 6;
+    const bool wv_hi = __builtin_amdgcn_readfirstlane(w) >= NWAVES / 2;  // wave-uniform (scalar branch)
     const int l0 = tid & 63;
     const int c0 = l0 & 15;
     const int g0 = l0 >> 4;
@@ -467,7 +468,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                 }
                 static_for<L>([&](auto ii) {
                     constexpr int k = L - 1 - decltype(ii)::value;
-                    constexpr int RK = (k & 1) ? S_::R0 : 0;
+                    // staging region of layer k this tile (alternating halves when ALT)
+                    const int RK = S_::ALT ? ((((k + titer) & 1) != 0) ? S_::HALF : 0) : ((k & 1) ? S_::R0 : 0);
                     float* st = sstage + w * S_::WAVE_STAGE + RK;
 #pragma unroll
                     for (int mt = 0; mt < S_::MT(k); ++mt)
@@ -524,7 +526,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                         }
                     };
                     if constexpr (k == 0) {
-                        if constexpr (!S_::WGRAD0_LATE) wgrad0();
+                        // Waves s and s + 4 share SIMD s: the upper half runs the layer-0
+                        // wgrad first, so each SIMD overlaps one wave's scatter with the
+                        // other's MFMAs (both orders when WGRAD0_LATE; else wgrad first).
+                        if (!S_::WGRAD0_LATE || wv_hi) wgrad0();
                         // (h) next tile's embedding fragments: before this tile's
                         // scatter atomics, so the next tile waits on them only
                         load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
@@ -617,14 +622,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                         // before the scatter: consumed here, the wait is a counted one on
                         // old loads; at their use after the branchy scatter it would
                         // drain the atomics too.
-                        if constexpr (S_::WGRAD0_LATE) {
+                        if (S_::WGRAD0_LATE && !wv_hi) {
 #pragma unroll
                             for (int i = 0; i < NWAVES * 4; ++i) asm volatile("" ::"v"(bx[i]));
                         }
                         stamp(a, sb + 4 + 3 * (L - 1));
                         // item half -> this wave's scratch rows (segment-reduced below);
                         // user half -> unconditional atomics (padding rows add 0 to row 0)
-                        float* scr = sstage + w * S_::WAVE_STAGE + S_::R0;
+                        // scratch: the half / region not holding this tile's layer-0 staging
+                        float* scr = sstage + w * S_::WAVE_STAGE + (S_::ALT ? ((titer & 1) ? 0 : S_::HALF) : S_::R0);
                         if constexpr (DM >= 16) {  // the split is 16-column aligned
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
@@ -667,7 +673,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                             }
                         }
                         stamp(a, sb + 5 + 3 * (L - 1));
-                        if constexpr (S_::WGRAD0_LATE) wgrad0();
+                        if (S_::WGRAD0_LATE && !wv_hi) wgrad0();
                     }
                     if constexpr (k >= 1) stamp(a, sb + 5 + 3 * (L - 1 - k));
                 });
@@ -682,7 +688,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                 lds_barrier();
                 load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
             }
-            lds_barrier();
+            // Tile end: no barrier unless the staging layout needs one (END_BARRIER):
+            // the next tile's first cross-wave staging goes to the other region and
+            // its first barrier resynchronises, so a wave still scattering overlaps
+            // the others' next forward.
+            if constexpr (S_::END_BARRIER) lds_barrier();
             stamp(a, sb + 13);
             ++titer;
         }
