@@ -240,6 +240,19 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     // table -- instead of one per row.  Correct for any row order (unsorted
     // input just yields shorter segments).  scr holds the MLP item rows
     // [16][SCM] (written by the caller); the GMF item rows go to [16][SCG] after it.
+    // The wave's 16 row ids (wave-uniform) into scalar registers: four 16-byte LDS
+    // reads, then readfirstlane, so segment boundaries are scalar branches.
+    auto wave_ids = [&](const int* ids16, int (&ids)[16]) {
+        const int4* p4 = reinterpret_cast<const int4*>(ids16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int4 v = p4[q];
+            ids[4 * q + 0] = v.x;
+            ids[4 * q + 1] = v.y;
+            ids[4 * q + 2] = v.z;
+            ids[4 * q + 3] = v.w;
+        }
+    };
     auto item_segments = [&](float* scr, const TrainArgs& a, const int* su, const int* si, int wr, int l,
                              const float* gIg, int gf, int gq0) {
         (void)su;
@@ -248,19 +261,28 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
             for (int j = 0; j < NI; ++j) sg[(j * RPI + gq0) * S_::SCG + gf] = gIg[j];
         }
+        int ids[16];
+        wave_ids(si + wr, ids);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // same-wave LDS hand-off
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ids[r] = __builtin_amdgcn_readfirstlane(ids[r]);
+        // All 16 rows' values are read before the walk (one LDS wait, not one per row).
         if constexpr (S_::MLP) {
             constexpr int DM = S_::DM;
 #pragma unroll
             for (int f0 = 0; f0 < DM; f0 += 64) {
                 const int f = f0 + l;
+                const int fc = f < DM ? f : DM - 1;
+                float v[16];
+#pragma unroll
+                for (int row = 0; row < 16; ++row) v[row] = scr[row * S_::SCM + fc];
                 float sum = 0.f;
+#pragma unroll
                 for (int row = 0; row < 16; ++row) {
-                    const int it = si[wr + row];
-                    if (f < DM) sum += scr[row * S_::SCM + f];
-                    const bool last = row == 15 || si[wr + row + 1] != it;
-                    if (last) {
-                        if (it >= 0 && f < DM && !DIAG_ON(a, DIAG_NO_ITEM_SCATTER)) atomicAdd(a.grads + lay.im + (int64_t)it * DM + f, sum);
+                    sum += v[row];
+                    if (row == 15 || ids[row + 1] != ids[row]) {
+                        if (ids[row] >= 0 && f < DM && !DIAG_ON(a, DIAG_NO_ITEM_SCATTER))
+                            atomicAdd(a.grads + lay.im + (int64_t)ids[row] * DM + f, sum);
                         sum = 0.f;
                     }
                 }
@@ -268,13 +290,17 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         }
         if constexpr (S_::GMF) {
             const float* sg = scr + 16 * S_::SCM;
+            const int lc = l < F ? l : F - 1;
+            float v[16];
+#pragma unroll
+            for (int row = 0; row < 16; ++row) v[row] = sg[row * S_::SCG + lc];
             float sum = 0.f;
+#pragma unroll
             for (int row = 0; row < 16; ++row) {
-                const int it = si[wr + row];
-                if (l < F) sum += sg[row * S_::SCG + l];
-                const bool last = row == 15 || si[wr + row + 1] != it;
-                if (last) {
-                    if (it >= 0 && l < F && !DIAG_ON(a, DIAG_NO_GMF_SCATTER)) atomicAdd(a.grads + lay.ig + (int64_t)it * F + l, sum);
+                sum += v[row];
+                if (row == 15 || ids[row + 1] != ids[row]) {
+                    if (ids[row] >= 0 && l < F && !DIAG_ON(a, DIAG_NO_GMF_SCATTER))
+                        atomicAdd(a.grads + lay.ig + (int64_t)ids[row] * F + l, sum);
                     sum = 0.f;
                 }
             }
@@ -651,14 +677,24 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                             constexpr int RPW = DM >= 64 ? 1 : 64 / DM;  // rows per wave-instruction
                             constexpr int FPI = DM >= 64 ? 64 : DM;
+                            constexpr int NQ = 16 / RPW, NF = DM / FPI;
+                            // read every value first (one LDS wait), then the atomics back to back
+                            float uv[NQ][NF];
+                            int uid[NQ];
 #pragma unroll
-                            for (int q0 = 0; q0 < 16; q0 += RPW) {
-                                const int q = q0 + l / FPI;
-                                const int uu = max(su[wr + q], 0);
+                            for (int qi = 0; qi < NQ; ++qi) {
+                                const int q = qi * RPW + l / FPI;
+                                uid[qi] = max(su[wr + q], 0);
 #pragma unroll
-                                for (int f0 = 0; f0 < DM; f0 += FPI) {
-                                    const int f = f0 + l % FPI;
-                                    if (!DIAG_ON(a, DIAG_NO_USER_SCATTER)) atomicAdd(a.grads + lay.um + (int64_t)uu * DM + f, scr[q * S_::SCM + f]);
+                                for (int fi = 0; fi < NF; ++fi) uv[qi][fi] = scr[q * S_::SCM + fi * FPI + l % FPI];
+                            }
+#pragma unroll
+                            for (int qi = 0; qi < NQ; ++qi) {
+#pragma unroll
+                                for (int fi = 0; fi < NF; ++fi) {
+                                    const int f = fi * FPI + l % FPI;
+                                    if (!DIAG_ON(a, DIAG_NO_USER_SCATTER))
+                                        atomicAdd(a.grads + lay.um + (int64_t)uid[qi] * DM + f, uv[qi][fi]);
                                 }
                             }
                         } else {  // DM == 8: one 16-column tile, lanes c < 8 user, c >= 8 item
