@@ -527,12 +527,14 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                     // scatter atomics drain under these MFMAs)
                     auto wgrad0 = [&]() {
                         if (w < KT0 && !(a.diag & DIAG_NO_WGRAD)) {
+                            // layer-0 staging region of this tile (see RK below)
+                            const int RK0 = S_::ALT ? ((titer & 1) ? S_::HALF : 0) : 0;
 #pragma unroll
                             for (int mt = 0; mt < MT0; ++mt) {
                                 f4 acc0 = accW0[mt], acc1 = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                                 for (int ws = 0; ws < NWAVES; ++ws) {
-                                    const float* sto = sstage + ws * S_::WAVE_STAGE;
+                                    const float* sto = sstage + ws * S_::WAVE_STAGE + RK0;
 #pragma unroll
                                     for (int s = 0; s < 4; ++s) {
                                         const float av = sto[(4 * g + s) * S_::SD(0) + 16 * mt + c];

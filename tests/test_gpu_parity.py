@@ -108,6 +108,10 @@ def test_engine_trajectory_vs_golden(golden, mt, opt, use_graph):
 ONE_STEP = {  # name: (model_type, f, L, B, expected path)
     "C2": ("NeuMF-end", 8, 3, 1024, 1), "C3": ("NeuMF-end", 16, 3, 8192, 1),
     "default": ("NeuMF-end", 32, 2, 4096, 1),
+    # > 256 tiles of 128 rows: every workgroup of the fused kernel runs 2-3 tiles
+    # (alternating staging halves, no tile-end barrier, prefetch across tiles)
+    "C3-multitile": ("NeuMF-end", 16, 3, 65536 + 3000, 1), "C2-multitile": ("NeuMF-end", 8, 3, 40000, 1),
+    "mlp-multitile": ("MLP", 16, 2, 50000, 1), "gmf-multitile": ("GMF", 16, 1, 70000, 1),
     # layered path: tower too large for LDS, or factor_num without a fused kernel
     "cli-default-32x3": ("NeuMF-end", 32, 3, 4096, 2), "stress-64x4": ("NeuMF-end", 64, 4, 1000, 2),
     "odd-f6": ("NeuMF-end", 6, 3, 3001, 2), "mlp-f11": ("MLP", 11, 2, 777, 2),
@@ -359,3 +363,25 @@ def test_fused_reduce_adam_bitwise_equals_separate_kernels(monkeypatch, mt, f, L
         np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(out[0][1], out[1][1], rtol=1e-5)
     assert np.array_equal(out[0][2], out[1][2]) and out[0][2][1] == T
+
+
+@pytest.mark.parametrize("mt,f,Lyr", [("NeuMF-end", 16, 3), ("NeuMF-end", 8, 2)])
+def test_engine_multitile_trajectory_vs_oracle(mt, f, Lyr):
+    """Batches of 40,000 rows (every workgroup runs 2 tiles per step): 6 engine
+    Adam steps vs torch.optim.Adam on the oracle.  Parameters to atol lr/3: Adam
+    moves a parameter whose gradient is ~0 by up to lr on summation-order noise;
+    a wrong tile (e.g. stale staging) moves whole rows by ~lr every step."""
+    T, B = 6, 40000
+    ref, m, eng = _engine_for(mt, f, Lyr, 3000, 2000, 9)
+    rng = np.random.default_rng(31)
+    users = rng.integers(0, 3000, (T, B))
+    items = np.minimum(rng.zipf(1.3, (T, B)) - 1, 1999)
+    labels = (rng.random((T, B)) < 0.2).astype(np.int64)
+    _stream(eng, users, items, labels, B)
+    eng.run(T, use_graph=True)
+    torch.cuda.synchronize()
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    losses = O.train_steps(ref, opt, users, items, labels)
+    np.testing.assert_allclose(eng.epoch_losses()[:T], losses, rtol=1e-5)
+    for (k, v), (k2, v2) in zip(m.state_dict().items(), ref.state_dict().items()):
+        np.testing.assert_allclose(v.cpu().numpy(), v2.numpy(), rtol=1e-4, atol=3e-4, err_msg=k)
