@@ -396,13 +396,16 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         // predict
         float zt = 0.f;
         if constexpr (S_::MLP) {
+            // sWP is zero-padded past P and H[L] is 0 past F (zero weight rows, zero
+            // bias, ReLU), so no bounds test: one 16-byte LDS read per output tile
 #pragma unroll
             for (int mt = 0; mt < MTL; ++mt) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int o = 16 * mt + 4 * g + r;
-                    if (o < F) zt += sWP[S_::POFF + o] * lane_get(H[L][mt], r);
-                }
+                const f4 wp4 = *reinterpret_cast<const f4*>(sWP + S_::POFF + 16 * mt + 4 * g);
+                const f4 h = H[L][mt];
+                zt += wp4.x * h.x;
+                zt += wp4.y * h.y;
+                zt += wp4.z * h.z;
+                zt += wp4.w * h.w;
             }
             zt += shfl_xor(zt, 16);
             zt += shfl_xor(zt, 32);
@@ -441,6 +444,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                 }
             }
 
+            if (titer < 2) stamp(a, 44 + 3 * titer);  // diag sub-phase: bx gather issued
             // (e) loss + dlogit
             if (a.logits_out != nullptr && g == 0 && valid) a.logits_out[row0 + myq] = z;
             float dz = 0.f;
@@ -457,6 +461,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                 sdz[myq] = dz;
                 dbpAcc += dz;
             }
+            if (titer < 2) stamp(a, 45 + 3 * titer);  // diag sub-phase: loss + dz
             // GMF backward.  User side: unconditional atomics (padding rows add 0
             // to row 0).  Item side: kept for the per-item segment reduction.
             float gIg[NI];

@@ -23,6 +23,8 @@ for t in range(4):
     NAMES.update({b + 10: f"t{t}:L0:dgrad_mfma", b + 11: f"t{t}:L0:scatter", b + 13: f"t{t}:L0:wgrad+end-barrier"})
     NAMES[b + 13] = f"t{t}:end-barrier"
 NAMES.update({60: "epilogue:img", 61: "epilogue:store"})
+for t in range(2):  # sub-phases of loss+gmf_bwd (slots of tiles 3-4, unused at bench size)
+    NAMES.update({44 + 3 * t: f"t{t}:  bx-gather-issued", 45 + 3 * t: f"t{t}:  loss+dz"})
 
 
 def main():
@@ -35,7 +37,7 @@ def main():
     eng.run(5, use_graph=False)
     nwg = L.hip().ncf_slab_rows()
     buf = torch.zeros(nwg * 64, dtype=torch.int64, device=dev)
-    out = {}
+    since = {}
     for rep in range(3):
         buf.zero_()
         L.hip().ncf_debug_set_stamps(buf.data_ptr())
@@ -43,18 +45,18 @@ def main():
         torch.cuda.synchronize()
         L.hip().ncf_debug_set_stamps(None)
         st = buf.view(nwg, 64).cpu().numpy().astype(np.int64)
-        t0 = st[:, 0:1]
-        rel = st - t0
-        for idx, name in sorted(NAMES.items()):
-            col = st[:, idx]
-            ok = col > 0
-            if ok.sum() == 0:
-                continue
-            prev = [i for i in sorted(NAMES) if i < idx and (st[ok, i] > 0).all()]
-            d = (col[ok] - st[ok, prev[-1]]) if prev else col[ok] * 0
-            out.setdefault(name, []).append([float(np.median(d)), float(np.median(rel[ok, idx]))])
-    res = {k: {"delta_cycles_median": np.median([x[0] for x in v]), "since_start": np.median([x[1] for x in v])}
-           for k, v in out.items()}
+        rel = st - st[:, 0:1]
+        for idx, name in NAMES.items():
+            ok = st[:, idx] > 0
+            if ok.sum() > 0:
+                since.setdefault(name, []).append(float(np.median(rel[ok, idx])))
+    # phases in time order; delta = gap to the previous phase's median stamp
+    order = sorted(since.items(), key=lambda kv: np.median(kv[1]))
+    res, prev = {}, 0.0
+    for name, v in order:
+        t = float(np.median(v))
+        res[name] = {"delta_cycles_median": t - prev, "since_start": t}
+        prev = t
     print(json.dumps({"rows": rows, "phases": res}))
 
 
