@@ -27,45 +27,49 @@ struct Shape {
     __host__ __device__ static constexpr int wsize(int k) { return MLP ? 16 * MT(k) * SW(k) : 0; }
     __host__ __device__ static constexpr int woff(int k) { return k == 0 ? 0 : woff(k - 1) + wsize(k - 1); }
     static constexpr int W_TOTAL = woff(L);
-    __host__ __device__ static constexpr int stsize(int k) {
-        return MLP ? 16 * SD(k) + (k >= 1 ? 16 * SH(k) : 0) : 0;
-    }
-    __host__ __device__ static constexpr int rmax(int par, int k) {
-        return k >= L ? 0
-                      : ((k & 1) == par ? (stsize(k) > rmax(par, k + 1) ? stsize(k) : rmax(par, k + 1))
-                                        : rmax(par, k + 1));
-    }
-    static constexpr int R0 = rmax(0, 0), R1 = rmax(1, 0);
-    // Per-wave scratch of the layer-0 phase (item-side gradient rows before the
-    // per-item segment reduction): [16][DM + 4] MLP part, [16][F + 4] GMF part.
-    // It lives in the R1 staging region, free once every wave is past layer 1.
+    // Per-wave LDS: only layer 0 is staged across waves (its wgrad needs every row
+    // of the tile); layers k >= 1 accumulate their wgrad per wave in registers
+    // (see ncf_train.hip), summed over the waves once, in the epilogue.  The
+    // per-wave scratch of the layer-0 phase (item-side rows before the segment
+    // walk): [16][DM + 4] MLP part, [16][F + 4] GMF part.
+    static constexpr int ST0 = MLP ? 16 * SD(0) : 0;
     static constexpr int SCM = MLP ? DM + 4 : 0;
     static constexpr int SCG = GMF ? F + 4 : 0;
     static constexpr int SCR = 16 * (SCM + SCG);
-    static constexpr int STAGE_OLD = R0 + (R1 > SCR ? R1 : SCR);
-    // Odd L: the layer-0 staging and the next tile's first staging (layer L-1) have
-    // the same parity, so without a barrier between tiles a fast wave would overwrite
-    // staging a slow wave still reads.  With two equal halves whose roles alternate
-    // by tile parity the tile-end barrier goes away (if the LDS budget allows).
-    static constexpr int RMAX = R0 > R1 ? R0 : R1;
-    static constexpr int HALF = RMAX > SCR ? RMAX : SCR;
-    static constexpr int STAGE_ALT = 2 * HALF;
-    static constexpr bool ALT_FITS = (W_TOTAL + 10 * TILE_ROWS + NWAVES * STAGE_ALT) * 4 <= LDS_LIMIT_BYTES;
-#ifdef NCF_KEEP_END_BARRIER  // experiment switch: the previous layout + tile-end barrier
-    static constexpr bool ALT = false;
-    static constexpr bool END_BARRIER = true;
-#else
-    static constexpr bool ALT = MLP && (L & 1) && ALT_FITS;
-    static constexpr bool END_BARRIER = !MLP || ((L & 1) && !ALT_FITS);
-#endif
-    static constexpr int WAVE_STAGE = ALT ? STAGE_ALT : STAGE_OLD;
+    // Register accumulators of layers k >= 1: MT(k) x KT(k) 16x16 dW_k tiles and
+    // MT(k) bias partials per lane; kt_off / mb_off index layer k's first one.
+    __host__ __device__ static constexpr int nkt(int k) { return (MLP && k >= 1) ? MT(k) * KT(k) : 0; }
+    __host__ __device__ static constexpr int kt_off(int k) { return k <= 1 ? 0 : kt_off(k - 1) + nkt(k - 1); }
+    __host__ __device__ static constexpr int mb_off(int k) { return k <= 1 ? 0 : mb_off(k - 1) + MT(k - 1); }
+    static constexpr int NKT = MLP ? kt_off(L) : 0;
+    static constexpr int NMB = (MLP && L > 1) ? mb_off(L) : 0;
+    // Epilogue: per-wave LDS image of layer k's partials ([S(k+1)][S(k)] + 4 bias
+    // partials per output) and the per-thread share of their sum over the waves.
+    __host__ __device__ static constexpr int rwk(int k) { return S(k + 1) * S(k) + 4 * S(k + 1); }
+    __host__ __device__ static constexpr int nek(int k) {
+        return (MLP && k >= 1) ? (S(k + 1) * S(k) + S(k + 1) + NWAVES * 64 - 1) / (NWAVES * 64) : 0;
+    }
+    __host__ __device__ static constexpr int ne_off(int k) { return k <= 1 ? 0 : ne_off(k - 1) + nek(k - 1); }
+    static constexpr int NKEEP = MLP ? ne_off(L) : 0;
     // su[2], si[2], labels[2] (double-buffered tile indices), zgmf, dz, then
     // 128 floats of biases (each layer's padded to 16*MT) and 128 of predict weights
     static constexpr int MISC = 10 * TILE_ROWS;
+    // Two halves per wave whose roles (layer-0 staging / scatter scratch) alternate
+    // with tile parity: the next tile's staging never overwrites rows a slow wave
+    // still reads, so there is no tile-end barrier (if the LDS budget allows).
+    static constexpr int HALF0 = ST0 > SCR ? ST0 : SCR;
+    static constexpr bool ALT0_FITS = (W_TOTAL + MISC + NWAVES * 2 * HALF0) * 4 <= LDS_LIMIT_BYTES;
+#ifdef NCF_KEEP_END_BARRIER  // experiment switch: one region + tile-end barrier
+    static constexpr bool ALT0 = false;
+#else
+    static constexpr bool ALT0 = MLP && ALT0_FITS;
+#endif
+    static constexpr bool END_BARRIER = !ALT0;
+    static constexpr int WAVE_STAGE = ALT0 ? 2 * HALF0 : ST0 + SCR;
+    static_assert(!MLP || L < 2 || rwk(1) <= WAVE_STAGE, "epilogue wgrad image exceeds the staging region");
     __host__ __device__ static constexpr int boff(int k) { return k == 0 ? 0 : boff(k - 1) + 16 * MT(k - 1); }
     static_assert(!MLP || boff(L) <= 128, "bias LDS region");
     static_assert(P <= 128, "predict LDS region");
-    __host__ __device__ static constexpr int TPW(int k) { return (MT(k) * KT(k) + NWAVES - 1) / NWAVES; }
     static constexpr int KT0 = MLP ? KT(0) : 1;
     // Layer-0 wgrad after the embedding scatter (its atomics drain under the wgrad
     // MFMAs) keeps the wgrad operands live through the dgrad: off where that

@@ -93,7 +93,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     float* sdz = szg + TILE_ROWS;        // dlogit, per tile row
     float* sB = sdz + TILE_ROWS;         // biases, layer k at boff(k), zero-padded
     float* sWP = sB + 128;               // predict weights, zero-padded
-    float* sstage = sWP + 128;           // union: per-wave staging | slab image
+    float* sstage = sWP + 128;           // union: per-wave staging | epilogue images
 
     const int tid = threadIdx.x;
     const int w = tid >> 6;
@@ -136,9 +136,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 
     // Row prefetch: every thread issues the same loads (clamped row), so the
     // vector-memory stream is straight-line and hipcc can count vmcnt waits
-    // exactly instead of draining everything at a branch merge.
+    // exactly instead of draining everything at a branch merge.  Each wave
+    // loads and publishes its own 16 rows (lanes l < 16 publish): with one
+    // barrier per tile, a fast wave writing tile t+2's ids into the buffer of
+    // tile t must never overwrite rows another wave still reads after tile t's
+    // barrier -- and past that barrier waves read only their own rows.
+    const int prow = 16 * w + (l0 & 15);
+    const bool pub = l0 < 16;
     auto load_idx = [&](int64_t row0, int& u, int& it, float& y) {
-        const int64_t r = row0 + (tid & (TILE_ROWS - 1));
+        const int64_t r = row0 + prow;
         const bool ok = r < nloc;
         const int64_t rc = base + (ok ? r : 0);
         const uint64_t pr = a.rows[rc];
@@ -176,17 +182,19 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     constexpr int MT0 = S_::MLP ? S_::MT(0) : 1;
     constexpr int KT0 = S_::KT0;
     constexpr int MTL = S_::MLP ? S_::MT(L - 1) : 1;
-    constexpr int TPWK = (L > 1 && S_::MLP) ? S_::TPW(1) : 1;  // layers k >= 1 (TPW(k) <= TPW(1))
     f4 accW0[MT0];          // dW_0 tiles (mt, nt = w)
-    f4 accWk[L][TPWK];      // dW_k tiles, k >= 1 (round-robin blocks)
     float dbAcc[L];
     f4 dWpT[MTL];
+    f4 accK[S_::NKT > 0 ? S_::NKT : 1];    // dW_k tiles of layers k >= 1, this wave's rows
+    float dbK[S_::NMB > 0 ? S_::NMB : 1];  // db_k partials (output 16mt + c, rows 4g..4g+3)
     float dWpG = 0.f, dbpAcc = 0.f, lossAcc = 0.f;
+#pragma unroll
+    for (int t = 0; t < S_::NKT; ++t) accK[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < S_::NMB; ++t) dbK[t] = 0.f;
 #pragma unroll
     for (int k = 0; k < L; ++k) {
         dbAcc[k] = 0.f;
-#pragma unroll
-        for (int j = 0; j < TPWK; ++j) accWk[k][j] = f4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int t = 0; t < MT0; ++t) accW0[t] = f4{0.f, 0.f, 0.f, 0.f};
@@ -197,10 +205,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     constexpr int NI = S_::GMF ? 16 / RPI : 1;
     const float bpv = prm[lay.bp];
     const float wpf = S_::GMF ? prm[lay.wp + l0 % F] : 0.f;
-    if (tid < TILE_ROWS) {
-        su2[tid] = nu;
-        si2[tid] = ni;
-        slab2[tid] = nlab;
+    if (pub) {
+        su2[prow] = nu;
+        si2[prow] = ni;
+        slab2[prow] = nlab;
     }
     __syncthreads();
 
@@ -416,9 +424,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 
         if constexpr (FWD_ONLY) {
             if (g == 0 && valid) a.logits_out[base + row0 + myq] = z;
-            if (tid < TILE_ROWS) {
-                su2[(buf ^ 1) * TILE_ROWS + tid] = nu;
-                si2[(buf ^ 1) * TILE_ROWS + tid] = ni;
+            if (pub) {
+                su2[(buf ^ 1) * TILE_ROWS + prow] = nu;
+                si2[(buf ^ 1) * TILE_ROWS + prow] = ni;
             }
             lds_barrier();
             load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
@@ -499,112 +507,44 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                 }
                 static_for<L>([&](auto ii) {
                     constexpr int k = L - 1 - decltype(ii)::value;
-                    // staging region of layer k this tile (alternating halves when ALT)
-                    const int RK = S_::ALT ? ((((k + titer) & 1) != 0) ? S_::HALF : 0) : ((k & 1) ? S_::R0 : 0);
-                    float* st = sstage + w * S_::WAVE_STAGE + RK;
-#pragma unroll
-                    for (int mt = 0; mt < S_::MT(k); ++mt)
-                        *reinterpret_cast<f4*>(st + c * S_::SD(k) + 16 * mt + 4 * g) = D[k][mt];
                     if constexpr (k >= 1) {
-                        float* sh = st + 16 * S_::SD(k);
+                        stamp(a, sb + 3 + 3 * (L - 1 - k));
+                        // wgrad of layer k from this wave's own rows, no staging and no
+                        // barrier: D_k and H_k (orientation A: row on the lane) are
+                        // transposed to orientation B (rows in the K slots) by four
+                        // exact selector MFMAs per 16x16 tile, and each 16x16 block of
+                        // dW_k accumulates four MFMAs over the 16 rows in registers
+                        // (summed over the waves once, in the epilogue); db_k likewise.
+                        if (!(a.diag & DIAG_NO_WGRAD)) {
+                            float sel[4];
 #pragma unroll
-                        for (int t = 0; t < S_::KT(k); ++t)
-                            *reinterpret_cast<f4*>(sh + c * S_::SH(k) + 16 * t + 4 * g) = H[k][t];
-                    } else {
-                        // publish the next tile's indices with the layer-0 barrier
-                        if (tid < TILE_ROWS) {
-                            su2[(buf ^ 1) * TILE_ROWS + tid] = nu;
-                            si2[(buf ^ 1) * TILE_ROWS + tid] = ni;
-                            slab2[(buf ^ 1) * TILE_ROWS + tid] = nlab;
-                        }
-                    }
-                    lds_barrier();
-                    stamp(a, sb + 3 + 3 * (L - 1 - k));
-                    // bias grad: this wave's 16 rows, lane = output feature
-                    if (l < S_::S(k + 1)) {
-                        float s = 0.f;
+                            for (int q = 0; q < 4; ++q) sel[q] = c == 4 * g + q ? 1.f : 0.f;
+                            auto tr16 = [&](const f4& x) {
+                                f4 y = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                        for (int rr = 0; rr < 16; ++rr) s += st[rr * S_::SD(k) + l];
-                        dbAcc[k] += s;
-                    }
-                    // wgrad: dW_k[out][in] += sum_rows dpre_k[row][out] * H_k[row][in]
-                    // (layer 0: after the dgrad and the embedding scatter, so the
-                    // scatter atomics drain under these MFMAs)
-                    auto wgrad0 = [&]() {
-                        if (w < KT0 && !(a.diag & DIAG_NO_WGRAD)) {
-                            // layer-0 staging region of this tile (see RK below)
-                            const int RK0 = S_::ALT ? ((titer & 1) ? S_::HALF : 0) : 0;
+                                for (int q = 0; q < 4; ++q) y = MFMA4(lane_get(x, q), sel[q], y);
+                                return y;
+                            };
+                            f4 DB[S_::MT(k)];
 #pragma unroll
-                            for (int mt = 0; mt < MT0; ++mt) {
-                                f4 acc0 = accW0[mt], acc1 = f4{0.f, 0.f, 0.f, 0.f};
+                            for (int mt = 0; mt < S_::MT(k); ++mt) {
+                                DB[mt] = tr16(D[k][mt]);
+                                dbK[S_::mb_off(k) + mt] += (DB[mt].x + DB[mt].y) + (DB[mt].z + DB[mt].w);
+                            }
 #pragma unroll
-                                for (int ws = 0; ws < NWAVES; ++ws) {
-                                    const float* sto = sstage + ws * S_::WAVE_STAGE + RK0;
+                            for (int t = 0; t < S_::KT(k); ++t) {
+                                const f4 HB = tr16(H[k][t]);
 #pragma unroll
-                                    for (int s = 0; s < 4; ++s) {
-                                        const float av = sto[(4 * g + s) * S_::SD(0) + 16 * mt + c];
-                                        if (ws & 1)
-                                            acc1 = MFMA4(av, bx[ws * 4 + s], acc1);
-                                        else
-                                            acc0 = MFMA4(av, bx[ws * 4 + s], acc0);
-                                    }
-                                    if (ws & 1) __builtin_amdgcn_sched_barrier(0);
+                                for (int mt = 0; mt < S_::MT(k); ++mt) {
+                                    f4& acc = accK[S_::kt_off(k) + mt * S_::KT(k) + t];
+#pragma unroll
+                                    for (int q = 0; q < 4; ++q) acc = MFMA4(lane_get(DB[mt], q), lane_get(HB, q), acc);
                                 }
-                                acc0.x += acc1.x;
-                                acc0.y += acc1.y;
-                                acc0.z += acc1.z;
-                                acc0.w += acc1.w;
-                                accW0[mt] = acc0;
                             }
                         }
-                    };
-                    if constexpr (k == 0) {
-                        // Waves s and s + 4 share SIMD s: the upper half runs the layer-0
-                        // wgrad first, so each SIMD overlaps one wave's scatter with the
-                        // other's MFMAs (both orders when WGRAD0_LATE; else wgrad first).
-                        if (!S_::WGRAD0_LATE || wv_hi) wgrad0();
-                        // (h) next tile's embedding fragments: before this tile's
-                        // scatter atomics, so the next tile waits on them only
-                        load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
-                    } else {
-                        constexpr int T = S_::MT(k) * S_::KT(k);
-                        constexpr int tpw = S_::TPW(k);
-#pragma unroll
-                        for (int jl = 0; jl < tpw; ++jl) {
-                            const int j = w * tpw + jl;
-                            if (j < T && !(a.diag & DIAG_NO_WGRAD)) {
-                                const int mt = j % S_::MT(k);
-                                const int nt = j / S_::MT(k);
-                                f4 acc0 = accWk[k][jl], acc1 = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                                for (int ws = 0; ws < NWAVES; ++ws) {
-                                    const float* sto = sstage + ws * S_::WAVE_STAGE + RK;
-#pragma unroll
-                                    for (int s = 0; s < 4; ++s) {
-                                        const int row = 4 * g + s;
-                                        const float av = sto[row * S_::SD(k) + 16 * mt + c];
-                                        const float bv = sto[16 * S_::SD(k) + row * S_::SH(k) + 16 * nt + c];
-                                        if (ws & 1)
-                                            acc1 = MFMA4(av, bv, acc1);
-                                        else
-                                            acc0 = MFMA4(av, bv, acc0);
-                                    }
-#ifndef NCF_WGRADK_FREE
-                                    if (ws & 1) __builtin_amdgcn_sched_barrier(0);
-#endif
-                                }
-                                acc0.x += acc1.x;
-                                acc0.y += acc1.y;
-                                acc0.z += acc1.z;
-                                acc0.w += acc1.w;
-                                accWk[k][jl] = acc0;
-                            }
-                        }
-                    }
-                    if constexpr (k >= 1) stamp(a, sb + 4 + 3 * (L - 1 - k));
-                    // dgrad
-                    const float* Ws = sW + S_::woff(k);
-                    if constexpr (k >= 1) {
+                        stamp(a, sb + 4 + 3 * (L - 1 - k));
+                        // dgrad
+                        const float* Ws = sW + S_::woff(k);
                         f4 acc[S_::KT(k)];
 #pragma unroll
                         for (int m2 = 0; m2 < S_::KT(k); ++m2) acc[m2] = f4{0.f, 0.f, 0.f, 0.f};
@@ -632,7 +572,66 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                             d.w = h.w > 0.f ? acc[m2].w : 0.f;
                             D[k - 1][m2] = d;
                         }
+                        stamp(a, sb + 5 + 3 * (L - 1 - k));
                     } else {
+                        // layer 0: its wgrad needs every row of the tile -> stage this
+                        // wave's D_0 rows (half titer & 1 when ALT0) and publish the next
+                        // tile's indices with the tile's one barrier
+                        const int RK0s = S_::ALT0 ? ((titer & 1) ? S_::HALF0 : 0) : 0;
+                        float* st = sstage + w * S_::WAVE_STAGE + RK0s;
+#pragma unroll
+                        for (int mt = 0; mt < S_::MT(0); ++mt)
+                            *reinterpret_cast<f4*>(st + c * S_::SD(0) + 16 * mt + 4 * g) = D[0][mt];
+                        if (pub) {
+                            su2[(buf ^ 1) * TILE_ROWS + prow] = nu;
+                            si2[(buf ^ 1) * TILE_ROWS + prow] = ni;
+                            slab2[(buf ^ 1) * TILE_ROWS + prow] = nlab;
+                        }
+                        lds_barrier();
+                        stamp(a, sb + 3 + 3 * (L - 1));
+                        // bias grad: this wave's 16 rows, lane = output feature
+                        if (l < S_::S(1)) {
+                            float s = 0.f;
+#pragma unroll
+                            for (int rr = 0; rr < 16; ++rr) s += st[rr * S_::SD(0) + l];
+                            dbAcc[0] += s;
+                        }
+                    auto wgrad0 = [&]() {
+                        if (w < KT0 && !(a.diag & DIAG_NO_WGRAD)) {
+                            // layer-0 staging region of this tile (see RK below)
+                            const int RK0 = S_::ALT0 ? ((titer & 1) ? S_::HALF0 : 0) : 0;
+#pragma unroll
+                            for (int mt = 0; mt < MT0; ++mt) {
+                                f4 acc0 = accW0[mt], acc1 = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                                for (int ws = 0; ws < NWAVES; ++ws) {
+                                    const float* sto = sstage + ws * S_::WAVE_STAGE + RK0;
+#pragma unroll
+                                    for (int s = 0; s < 4; ++s) {
+                                        const float av = sto[(4 * g + s) * S_::SD(0) + 16 * mt + c];
+                                        if (ws & 1)
+                                            acc1 = MFMA4(av, bx[ws * 4 + s], acc1);
+                                        else
+                                            acc0 = MFMA4(av, bx[ws * 4 + s], acc0);
+                                    }
+                                    if (ws & 1) __builtin_amdgcn_sched_barrier(0);
+                                }
+                                acc0.x += acc1.x;
+                                acc0.y += acc1.y;
+                                acc0.z += acc1.z;
+                                acc0.w += acc1.w;
+                                accW0[mt] = acc0;
+                            }
+                        }
+                    };
+                        // Waves s and s + 4 share SIMD s: the upper half runs the layer-0
+                        // wgrad first, so each SIMD overlaps one wave's scatter with the
+                        // other's MFMAs (both orders when WGRAD0_LATE; else wgrad first).
+                        if (!S_::WGRAD0_LATE || wv_hi) wgrad0();
+                        // (h) next tile's embedding fragments: before this tile's
+                        // scatter atomics, so the next tile waits on them only
+                        load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
+                        const float* Ws = sW + S_::woff(0);
                         // orientation B: C[i = row 4g+r][j = in-feature 16*nt + c]
                         f4 acc[KT0];
 #pragma unroll
@@ -663,7 +662,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                         // item half -> this wave's scratch rows (segment-reduced below);
                         // user half -> unconditional atomics (padding rows add 0 to row 0)
                         // scratch: the half / region not holding this tile's layer-0 staging
-                        float* scr = sstage + w * S_::WAVE_STAGE + (S_::ALT ? ((titer & 1) ? 0 : S_::HALF) : S_::R0);
+                        float* scr = sstage + w * S_::WAVE_STAGE + (S_::ALT0 ? ((titer & 1) ? 0 : S_::HALF0) : S_::ST0);
                         if constexpr (DM >= 16) {  // the split is 16-column aligned
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
@@ -718,15 +717,14 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                         stamp(a, sb + 5 + 3 * (L - 1));
                         if (S_::WGRAD0_LATE && !wv_hi) wgrad0();
                     }
-                    if constexpr (k >= 1) stamp(a, sb + 5 + 3 * (L - 1 - k));
                 });
             } else {
                 // GMF-only model: item-side GMF rows, then publish next indices
-                item_segments(sstage + w * S_::WAVE_STAGE + S_::R0, a, su, si, wr, l, gIg, gf, gq0);
-                if (tid < TILE_ROWS) {
-                    su2[(buf ^ 1) * TILE_ROWS + tid] = nu;
-                    si2[(buf ^ 1) * TILE_ROWS + tid] = ni;
-                    slab2[(buf ^ 1) * TILE_ROWS + tid] = nlab;
+                item_segments(sstage + w * S_::WAVE_STAGE, a, su, si, wr, l, gIg, gf, gq0);
+                if (pub) {
+                    su2[(buf ^ 1) * TILE_ROWS + prow] = nu;
+                    si2[(buf ^ 1) * TILE_ROWS + prow] = ni;
+                    slab2[(buf ^ 1) * TILE_ROWS + prow] = nlab;
                 }
                 lds_barrier();
                 load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
@@ -747,8 +745,100 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         const int lo = S_::MLP ? 0 : (int)(lay.wp - tb);
         const int len = (int)lay.tower_len + 64;  // slab stride (ncf_slab_stride); loss at tower_len
         float* img = sstage;
-        const int l = l0, c = c0, g = g0, gf = l0 % F;
+        const int l = l0, c = c0, g = g0;
+        lds_barrier();  // every wave is past its last tile: the staging is free
+        stamp(a, 62);
+        // Layers k >= 1: each wave writes its register partials to its own LDS
+        // image, then every thread sums its share of the entries over the waves
+        // (plain stores and loads: LDS float atomics run ~2 cycles per lane).
+        float kept[S_::NKEEP > 0 ? S_::NKEEP : 1];
+        if constexpr (S_::MLP) {
+            static_for<L>([&](auto kk) {
+                constexpr int k = decltype(kk)::value;
+                if constexpr (k >= 1) {
+                    constexpr int SK = S_::S(k), SO = S_::S(k + 1);
+                    float* im = sstage + w * S_::WAVE_STAGE;
+#pragma unroll
+                    for (int mt = 0; mt < S_::MT(k); ++mt) {
+#pragma unroll
+                        for (int t = 0; t < S_::KT(k); ++t) {
+                            const f4 v = accK[S_::kt_off(k) + mt * S_::KT(k) + t];
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int o = 16 * mt + 4 * g + r;
+                                if (o < SO) im[o * SK + 16 * t + c] = lane_get(v, r);
+                            }
+                        }
+                        const int o = 16 * mt + c;
+                        if (o < SO) im[SO * SK + g * SO + o] = dbK[S_::mb_off(k) + mt];
+                    }
+                    lds_barrier();
+#pragma unroll
+                    for (int j = 0; j < S_::nek(k); ++j) {
+                        const int e = tid + j * NTHREADS;
+                        float s = 0.f;
+                        if (e < SO * SK) {
+#pragma unroll
+                            for (int ws = 0; ws < NWAVES; ++ws) s += sstage[ws * S_::WAVE_STAGE + e];
+                        } else if (e < SO * SK + SO) {
+#pragma unroll
+                            for (int ws = 0; ws < NWAVES; ++ws)
+#pragma unroll
+                                for (int gg = 0; gg < 4; ++gg) s += sstage[ws * S_::WAVE_STAGE + SO * SK + gg * SO + (e - SO * SK)];
+                        }
+                        kept[S_::ne_off(k) + j] = s;
+                    }
+                    lds_barrier();
+                }
+            });
+        }
+        stamp(a, 58);
+        // Remaining partials (db_0, predict weights, bp, loss): reduced inside the
+        // wave by shuffles, one per-wave LDS image, summed over the waves below.
+        constexpr int S1 = S_::MLP ? S_::S(1) : 0;
+        constexpr int NT = S1 + S_::P + 2;  // [db_0 | wp | bp | loss]
+        static_assert(NT <= S_::WAVE_STAGE && NT <= NTHREADS, "epilogue tail image");
+        {
+            float* tv = sstage + w * S_::WAVE_STAGE;
+            if constexpr (S_::MLP) {
+                if (l < S1) tv[l] = dbAcc[0];
+#pragma unroll
+                for (int mt = 0; mt < MTL; ++mt) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float v = lane_get(dWpT[mt], r);  // row c, predict input 16mt + 4g + r
+#pragma unroll
+                        for (int m = 1; m < 16; m <<= 1) v += shfl_xor(v, m);
+                        const int o = 16 * mt + 4 * g + r;
+                        if (c == 0 && o < F) tv[S1 + S_::POFF + o] = v;
+                    }
+                }
+            }
+            if constexpr (S_::GMF) {
+                float v = dWpG;  // feature l % F, rows l / F
+#pragma unroll
+                for (int m = F; m < 64; m <<= 1) v += shfl_xor(v, m);
+                if (l < F) tv[S1 + l] = v;
+            }
+            float vb = dbpAcc, vl = lossAcc;  // nonzero on g == 0 lanes only
+#pragma unroll
+            for (int m = 1; m < 64; m <<= 1) {
+                vb += shfl_xor(vb, m);
+                vl += shfl_xor(vl, m);
+            }
+            if (l == 0) {
+                tv[S1 + S_::P] = vb;
+                tv[S1 + S_::P + 1] = vl / gb_f;
+            }
+        }
         lds_barrier();
+        float tsum = 0.f;
+        if (tid < NT) {
+#pragma unroll
+            for (int ws = 0; ws < NWAVES; ++ws) tsum += sstage[ws * S_::WAVE_STAGE + tid];
+        }
+        lds_barrier();
+        stamp(a, 59);
         for (int e = lo + tid; e < len; e += NTHREADS) img[e] = 0.f;
         lds_barrier();
         if constexpr (S_::MLP) {
@@ -766,38 +856,24 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
             static_for<L>([&](auto kk) {
                 constexpr int k = decltype(kk)::value;
                 if constexpr (k >= 1) {
-                    constexpr int T = S_::MT(k) * S_::KT(k);
-                    constexpr int tpw = S_::TPW(k);
-                    float* dW = img + (lay.w[k] - tb);
+                    // layers k >= 1: this thread's share of the wave sums
+                    constexpr int SK = S_::S(k), SO = S_::S(k + 1);
 #pragma unroll
-                    for (int jl = 0; jl < tpw; ++jl) {
-                        const int j = w * tpw + jl;
-                        if (j < T) {
-                            const int mt = j % S_::MT(k);
-                            const int nt = j / S_::MT(k);
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                const int o = 16 * mt + 4 * g + r;
-                                if (o < S_::S(k + 1)) dW[o * S_::S(k) + 16 * nt + c] = lane_get(accWk[k][jl], r);
-                            }
-                        }
+                    for (int j = 0; j < S_::nek(k); ++j) {
+                        const int e = tid + j * NTHREADS;
+                        if (e < SO * SK)
+                            img[(lay.w[k] - tb) + e] = kept[S_::ne_off(k) + j];
+                        else if (e < SO * SK + SO)
+                            img[(lay.b[k] - tb) + (e - SO * SK)] = kept[S_::ne_off(k) + j];
                     }
                 }
-                if (l < S_::S(k + 1)) atomicAdd(img + (lay.b[k] - tb) + l, dbAcc[k]);
             });
-#pragma unroll
-            for (int mt = 0; mt < MTL; ++mt) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int o = 16 * mt + 4 * g + r;
-                    if (o < F) atomicAdd(img + (lay.wp - tb) + S_::POFF + o, lane_get(dWpT[mt], r));
-                }
-            }
         }
-        if constexpr (S_::GMF) atomicAdd(img + (lay.wp - tb) + gf, dWpG);
-        if (g == 0) {
-            atomicAdd(img + (lay.bp - tb), dbpAcc);
-            atomicAdd(img + lay.tower_len, lossAcc / gb_f);
+        if (tid < NT) {
+            const int64_t pos = tid < S1 ? (lay.b[0] - tb) + tid
+                              : tid < S1 + S_::P ? (lay.wp - tb) + (tid - S1)
+                              : tid == S1 + S_::P ? (lay.bp - tb) : (int64_t)lay.tower_len;
+            img[pos] = tsum;
         }
         lds_barrier();
         stamp(a, 60);

@@ -22,7 +22,7 @@ for t in range(4):
     # layer 0 runs dgrad MFMA, then the scatter, then the wgrad
     NAMES.update({b + 10: f"t{t}:L0:dgrad_mfma", b + 11: f"t{t}:L0:scatter", b + 13: f"t{t}:L0:wgrad+end-barrier"})
     NAMES[b + 13] = f"t{t}:end-barrier"
-NAMES.update({60: "epilogue:img", 61: "epilogue:store"})
+NAMES.update({62: "epilogue:first barrier", 58: "epilogue:wgrad-k sums", 59: "epilogue:tail sums", 60: "epilogue:img", 61: "epilogue:store"})
 for t in range(2):  # sub-phases of loss+gmf_bwd (slots of tiles 3-4, unused at bench size)
     NAMES.update({44 + 3 * t: f"t{t}:  bx-gather-issued", 45 + 3 * t: f"t{t}:  loss+dz"})
 
