@@ -44,13 +44,11 @@ struct Shape {
     static constexpr int NKT = MLP ? kt_off(L) : 0;
     static constexpr int NMB = (MLP && L > 1) ? mb_off(L) : 0;
     // Epilogue: per-wave LDS image of layer k's partials ([S(k+1)][S(k)] + 4 bias
-    // partials per output) and the per-thread share of their sum over the waves.
+    // partials per output) and the entries of their sum over the waves per thread.
     __host__ __device__ static constexpr int rwk(int k) { return S(k + 1) * S(k) + 4 * S(k + 1); }
     __host__ __device__ static constexpr int nek(int k) {
         return (MLP && k >= 1) ? (S(k + 1) * S(k) + S(k + 1) + NWAVES * 64 - 1) / (NWAVES * 64) : 0;
     }
-    __host__ __device__ static constexpr int ne_off(int k) { return k <= 1 ? 0 : ne_off(k - 1) + nek(k - 1); }
-    static constexpr int NKEEP = MLP ? ne_off(L) : 0;
     // su[2], si[2], labels[2] (double-buffered tile indices), zgmf, dz, then
     // 128 floats of biases (each layer's padded to 16*MT) and 128 of predict weights
     static constexpr int MISC = 10 * TILE_ROWS;

@@ -740,19 +740,95 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     }
 
     if constexpr (!FWD_ONLY) {
-        // ---- this workgroup's tower/predict partial: assemble in LDS, store once
+        // ---- this workgroup's tower/predict partial -> its slab row, stored straight
+        // from registers (sums over the waves through per-wave LDS images).  Every
+        // slab entry in [lo, len) is written exactly once, the alignment gaps with 0.
         const int64_t tb = lay.tower_begin;
-        const int lo = S_::MLP ? 0 : (int)(lay.wp - tb);
         const int len = (int)lay.tower_len + 64;  // slab stride (ncf_slab_stride); loss at tower_len
-        float* img = sstage;
+        float* out = a.slab + (int64_t)blockIdx.x * len;
         const int l = l0, c = c0, g = g0;
+        // layer-0 wgrad: this wave's 16-column block, already summed over the rows
+        if constexpr (S_::MLP) {
+            if (w < KT0) {
+#pragma unroll
+                for (int mt = 0; mt < MT0; ++mt) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int o = 16 * mt + 4 * g + r;
+                        if (o < S_::S(1)) out[(lay.w[0] - tb) + o * S_::S(0) + 16 * w + c] = lane_get(accW0[mt], r);
+                    }
+                }
+            }
+        }
+        // Tail partials [db_0 | wp | bp | loss]: reduced inside the wave by shuffles
+        // (before the barrier), then one per-wave LDS image like the layers k >= 1.
+        constexpr int S1 = S_::MLP ? S_::S(1) : 0;
+        constexpr int NT = S1 + S_::P + 2;
+        // the tail rides with the last layer's round where both images fit
+        constexpr bool TAIL_MERGED = S_::MLP && L >= 2 && S_::rwk(L - 1) + NT <= S_::WAVE_STAGE;
+        constexpr int TOFF = TAIL_MERGED ? S_::rwk(L - 1) : 0;
+        static_assert(TOFF + NT <= S_::WAVE_STAGE && NT <= NTHREADS, "epilogue tail image");
+        float tw[MTL][4];  // predict-weight partials summed over the wave's rows (lanes c == 0)
+        if constexpr (S_::MLP) {
+#pragma unroll
+            for (int mt = 0; mt < MTL; ++mt) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float v = lane_get(dWpT[mt], r);  // row c, predict input 16mt + 4g + r
+#pragma unroll
+                    for (int m = 1; m < 16; m <<= 1) v += shfl_xor(v, m);
+                    tw[mt][r] = v;
+                }
+            }
+        }
+        float vg = dWpG;  // GMF: feature l % F, rows l / F
+        if constexpr (S_::GMF) {
+#pragma unroll
+            for (int m = F; m < 64; m <<= 1) vg += shfl_xor(vg, m);
+        }
+        float vb = dbpAcc, vl = lossAcc;  // nonzero on g == 0 lanes only
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) {
+            vb += shfl_xor(vb, m);
+            vl += shfl_xor(vl, m);
+        }
+        auto write_tail = [&]() {
+            float* tv = sstage + w * S_::WAVE_STAGE + TOFF;
+            if constexpr (S_::MLP) {
+                if (l < S1) tv[l] = dbAcc[0];
+#pragma unroll
+                for (int mt = 0; mt < MTL; ++mt) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int o = 16 * mt + 4 * g + r;
+                        if (c == 0 && o < F) tv[S1 + S_::POFF + o] = tw[mt][r];
+                    }
+                }
+            }
+            if constexpr (S_::GMF)
+                if (l < F) tv[S1 + l] = vg;
+            if (l == 0) {
+                tv[S1 + S_::P] = vb;
+                tv[S1 + S_::P + 1] = vl / gb_f;
+            }
+        };
+        auto sum_tail = [&]() {
+            if (tid < NT) {
+                float ts = 0.f;
+#pragma unroll
+                for (int ws = 0; ws < NWAVES; ++ws) ts += sstage[ws * S_::WAVE_STAGE + TOFF + tid];
+                const int64_t pos = tid < S1 ? (lay.b[0] - tb) + tid
+                                  : tid < S1 + S_::P ? (lay.wp - tb) + (tid - S1)
+                                  : tid == S1 + S_::P ? (lay.bp - tb) : (int64_t)lay.tower_len;
+                out[pos] = ts;
+            }
+        };
         lds_barrier();  // every wave is past its last tile: the staging is free
         stamp(a, 62);
-        // Layers k >= 1: each wave writes its register partials to its own LDS
-        // image, then every thread sums its share of the entries over the waves
-        // (plain stores and loads: LDS float atomics run ~2 cycles per lane).
-        float kept[S_::NKEEP > 0 ? S_::NKEEP : 1];
-        if constexpr (S_::MLP) {
+        if constexpr (S_::MLP && L >= 2) {
+            // Layers k >= 1: each wave writes its register partials to its own LDS
+            // image, then every thread sums its share of the entries over the waves
+            // (plain stores and loads: LDS float atomics run ~2 cycles per lane).
             static_for<L>([&](auto kk) {
                 constexpr int k = decltype(kk)::value;
                 if constexpr (k >= 1) {
@@ -772,113 +848,53 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                         const int o = 16 * mt + c;
                         if (o < SO) im[SO * SK + g * SO + o] = dbK[S_::mb_off(k) + mt];
                     }
+                    if constexpr (TAIL_MERGED && k == L - 1) write_tail();
                     lds_barrier();
 #pragma unroll
                     for (int j = 0; j < S_::nek(k); ++j) {
                         const int e = tid + j * NTHREADS;
-                        float s = 0.f;
                         if (e < SO * SK) {
+                            float s = 0.f;
 #pragma unroll
                             for (int ws = 0; ws < NWAVES; ++ws) s += sstage[ws * S_::WAVE_STAGE + e];
+                            out[(lay.w[k] - tb) + e] = s;
                         } else if (e < SO * SK + SO) {
+                            float s = 0.f;
 #pragma unroll
                             for (int ws = 0; ws < NWAVES; ++ws)
 #pragma unroll
                                 for (int gg = 0; gg < 4; ++gg) s += sstage[ws * S_::WAVE_STAGE + SO * SK + gg * SO + (e - SO * SK)];
+                            out[(lay.b[k] - tb) + (e - SO * SK)] = s;
                         }
-                        kept[S_::ne_off(k) + j] = s;
                     }
-                    lds_barrier();
+                    if constexpr (TAIL_MERGED && k == L - 1)
+                        sum_tail();
+                    else
+                        lds_barrier();
                 }
             });
         }
-        stamp(a, 58);
-        // Remaining partials (db_0, predict weights, bp, loss): reduced inside the
-        // wave by shuffles, one per-wave LDS image, summed over the waves below.
-        constexpr int S1 = S_::MLP ? S_::S(1) : 0;
-        constexpr int NT = S1 + S_::P + 2;  // [db_0 | wp | bp | loss]
-        static_assert(NT <= S_::WAVE_STAGE && NT <= NTHREADS, "epilogue tail image");
-        {
-            float* tv = sstage + w * S_::WAVE_STAGE;
-            if constexpr (S_::MLP) {
-                if (l < S1) tv[l] = dbAcc[0];
-#pragma unroll
-                for (int mt = 0; mt < MTL; ++mt) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float v = lane_get(dWpT[mt], r);  // row c, predict input 16mt + 4g + r
-#pragma unroll
-                        for (int m = 1; m < 16; m <<= 1) v += shfl_xor(v, m);
-                        const int o = 16 * mt + 4 * g + r;
-                        if (c == 0 && o < F) tv[S1 + S_::POFF + o] = v;
-                    }
-                }
-            }
-            if constexpr (S_::GMF) {
-                float v = dWpG;  // feature l % F, rows l / F
-#pragma unroll
-                for (int m = F; m < 64; m <<= 1) v += shfl_xor(v, m);
-                if (l < F) tv[S1 + l] = v;
-            }
-            float vb = dbpAcc, vl = lossAcc;  // nonzero on g == 0 lanes only
-#pragma unroll
-            for (int m = 1; m < 64; m <<= 1) {
-                vb += shfl_xor(vb, m);
-                vl += shfl_xor(vl, m);
-            }
-            if (l == 0) {
-                tv[S1 + S_::P] = vb;
-                tv[S1 + S_::P + 1] = vl / gb_f;
-            }
+        if constexpr (!TAIL_MERGED) {
+            write_tail();
+            lds_barrier();
+            sum_tail();
         }
-        lds_barrier();
-        float tsum = 0.f;
-        if (tid < NT) {
-#pragma unroll
-            for (int ws = 0; ws < NWAVES; ++ws) tsum += sstage[ws * S_::WAVE_STAGE + tid];
-        }
-        lds_barrier();
-        stamp(a, 59);
-        for (int e = lo + tid; e < len; e += NTHREADS) img[e] = 0.f;
-        lds_barrier();
+        stamp(a, 60);
+        // alignment gaps of the 64-float segments (ncf_layout_init)
+        auto zero_gap = [&](int64_t seg, int n) {
+            const int gap = ((n + 63) & ~63) - n;
+            if (tid < gap) out[(seg - tb) + n + tid] = 0.f;
+        };
         if constexpr (S_::MLP) {
-            if (w < KT0) {
-                float* dW = img + (lay.w[0] - tb);
-#pragma unroll
-                for (int mt = 0; mt < MT0; ++mt) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int o = 16 * mt + 4 * g + r;
-                        if (o < S_::S(1)) dW[o * S_::S(0) + 16 * w + c] = lane_get(accW0[mt], r);
-                    }
-                }
-            }
             static_for<L>([&](auto kk) {
                 constexpr int k = decltype(kk)::value;
-                if constexpr (k >= 1) {
-                    // layers k >= 1: this thread's share of the wave sums
-                    constexpr int SK = S_::S(k), SO = S_::S(k + 1);
-#pragma unroll
-                    for (int j = 0; j < S_::nek(k); ++j) {
-                        const int e = tid + j * NTHREADS;
-                        if (e < SO * SK)
-                            img[(lay.w[k] - tb) + e] = kept[S_::ne_off(k) + j];
-                        else if (e < SO * SK + SO)
-                            img[(lay.b[k] - tb) + (e - SO * SK)] = kept[S_::ne_off(k) + j];
-                    }
-                }
+                zero_gap(lay.w[k], S_::S(k + 1) * S_::S(k));
+                zero_gap(lay.b[k], S_::S(k + 1));
             });
         }
-        if (tid < NT) {
-            const int64_t pos = tid < S1 ? (lay.b[0] - tb) + tid
-                              : tid < S1 + S_::P ? (lay.wp - tb) + (tid - S1)
-                              : tid == S1 + S_::P ? (lay.bp - tb) : (int64_t)lay.tower_len;
-            img[pos] = tsum;
-        }
-        lds_barrier();
-        stamp(a, 60);
-        float* out = a.slab + (int64_t)blockIdx.x * len;
-        for (int e = lo + tid; e < len; e += NTHREADS) out[e] = img[e];
+        zero_gap(lay.wp, S_::P);
+        zero_gap(lay.bp, 1);
+        zero_gap(tb + lay.tower_len, 1);
 #ifdef NCF_STAMPS
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif

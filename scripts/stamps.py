@@ -22,7 +22,7 @@ for t in range(4):
     # layer 0 runs dgrad MFMA, then the scatter, then the wgrad
     NAMES.update({b + 10: f"t{t}:L0:dgrad_mfma", b + 11: f"t{t}:L0:scatter", b + 13: f"t{t}:L0:wgrad+end-barrier"})
     NAMES[b + 13] = f"t{t}:end-barrier"
-NAMES.update({62: "epilogue:first barrier", 58: "epilogue:wgrad-k sums", 59: "epilogue:tail sums", 60: "epilogue:img", 61: "epilogue:store"})
+NAMES.update({62: "epilogue:first barrier", 60: "epilogue:sums+stores", 61: "epilogue:drain"})
 for t in range(2):  # sub-phases of loss+gmf_bwd (slots of tiles 3-4, unused at bench size)
     NAMES.update({44 + 3 * t: f"t{t}:  bx-gather-issued", 45 + 3 * t: f"t{t}:  loss+dz"})
 
@@ -38,6 +38,7 @@ def main():
     nwg = L.hip().ncf_slab_rows()
     buf = torch.zeros(nwg * 64, dtype=torch.int64, device=dev)
     since = {}
+    spread = []
     for rep in range(3):
         buf.zero_()
         L.hip().ncf_debug_set_stamps(buf.data_ptr())
@@ -46,6 +47,9 @@ def main():
         L.hip().ncf_debug_set_stamps(None)
         st = buf.view(nwg, 64).cpu().numpy().astype(np.int64)
         rel = st - st[:, 0:1]
+        dur = rel[:, 61][st[:, 61] > 0]
+        if dur.size:  # per-workgroup duration: the kernel ends with the slowest one
+            spread.append([float(np.percentile(dur, q)) for q in (0, 10, 50, 90, 100)])
         for idx, name in NAMES.items():
             ok = st[:, idx] > 0
             if ok.sum() > 0:
@@ -57,7 +61,9 @@ def main():
         t = float(np.median(v))
         res[name] = {"delta_cycles_median": t - prev, "since_start": t}
         prev = t
-    print(json.dumps({"rows": rows, "phases": res}))
+    sp = np.median(np.array(spread), axis=0).tolist() if spread else []
+    print(json.dumps({"rows": rows, "phases": res,
+                      "wg_duration_cycles_p0_p10_p50_p90_max": sp}))
 
 
 if __name__ == "__main__":
