@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 4
+#define NCF_ABI_VERSION 5
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -134,6 +134,12 @@ int ncf_forward(const ncf_layout *lay, const float *params, const uint64_t *rows
  * label tensors the reference DataLoader yields, datasets.py:72-78). */
 int ncf_pack_rows(const int32_t *users, const int32_t *items, const float *labels, int64_t n,
                   uint64_t *rows_out, void *stream);
+
+/* p[0 .. n) = 0 with a kernel (no memset node in a captured graph); p 16-byte aligned,
+ * n a multiple of 4.  Zeroes the local gradient bucket after the data-parallel
+ * reduce-scatter (the replacement of optimizer.zero_grad, train_neumf.py:111, on
+ * the sharded optimizer path). */
+int ncf_zero_f32(float *p, int64_t n, void *stream);
 
 /* grads[tower_begin + j] = sum_w slab[w][j] over the slab rows at the start of the
  * train workspace (loss slot included), in a fixed order (bitwise reproducible).  If

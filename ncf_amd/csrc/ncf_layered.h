@@ -24,6 +24,9 @@ struct LyrArgs {
     float* logits_out;       // optional per-row logits
 };
 
+// p[0 .. n) = 0 (n % 4 == 0, p 16-byte aligned) on stream st.
+int launch_zero_f32(float* p, int64_t n, hipStream_t st);
+
 // Workspace floats for `rows` rows per launch (slab row + activations [+ dY buffers]).
 int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train);
 

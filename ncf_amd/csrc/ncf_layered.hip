@@ -463,7 +463,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             Db = ws + off;
         }
     }
-    if (train && hipMemsetAsync(slab, 0, (size_t)(lay.tower_len + 64) * 4, st) != hipSuccess) return NCF_E_LAUNCH;
+    if (train && launch_zero_f32(slab, lay.tower_len + 64, st) != NCF_OK) return NCF_E_LAUNCH;
     const unsigned mt = (unsigned)((R + GBM - 1) / GBM);
     if (mlp) {
         for (int k = 0; k < L; ++k) {

@@ -259,6 +259,11 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
 }
 
 // ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void zero_f32_kernel(f4* __restrict__ p, int64_t n4) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x)
+        p[q] = f4{0.f, 0.f, 0.f, 0.f};
+}
+
 // Packed rows (include/ncf_hip.h NCF_ROW_PACK): u | item << 32 | label << 63.
 __device__ __forceinline__ int row_item(uint64_t r) { return (int)((r >> 32) & 0x7fffffffu); }
 
@@ -587,6 +592,15 @@ static int ensure_lds(const void* fn, int64_t bytes) {
     return NCF_OK;
 }
 
+int launch_zero_f32(float* p, int64_t n, hipStream_t st) {
+    if (!p || n < 0 || (n & 3) || (reinterpret_cast<uintptr_t>(p) & 15)) return NCF_E_ARG;
+    if (n == 0) return NCF_OK;
+    int64_t grid = (n / 4 + 255) / 256;
+    if (grid > 2048) grid = 2048;
+    hipLaunchKernelGGL(zero_f32_kernel, dim3((int)grid), dim3(256), 0, st, reinterpret_cast<f4*>(p), n / 4);
+    return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
+}
+
 }  // namespace ncf
 
 using namespace ncf;
@@ -836,6 +850,8 @@ int ncf_sgd_step(float* params, float* grads, const int64_t* ranges, int nranges
                        loss_slot, loss_hist, hist_len);
     return launch_status();
 }
+
+int ncf_zero_f32(float* p, int64_t n, void* stream) { return launch_zero_f32(p, n, (hipStream_t)stream); }
 
 int ncf_pack_rows(const int32_t* users, const int32_t* items, const float* labels, int64_t n, uint64_t* rows_out,
                   void* stream) {

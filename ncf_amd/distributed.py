@@ -1,10 +1,19 @@
 """Data-parallel helpers (one process per GPU, torch.distributed over RCCL).
 
-The reference is single-device; the build adds exactly one strategy (SURVEY.md
-8e): every rank computes the same global stream from the same seeds and takes a
-contiguous shard of each global batch; the gradient exchange is one all-reduce
-of the flat gradient bucket (dense tower grads + dense embedding grads), which
-keeps dense-Adam parity with the single-device run.
+The reference is single-device; the build adds one strategy:
+every rank computes the same global stream from the same seeds and takes a
+contiguous shard of each global batch.  The gradient exchange has two forms
+(``TrainEngine(dp_mode=...)``):
+
+* ``"zero1"`` (default for world > 1): the flat gradient bucket (dense
+  embedding tables + tower + predict, zero padded to world x shard floats) is
+  reduce-scattered, each rank runs Adam on its own contiguous shard of the
+  flat parameters (its moments are shard-sized), and the updated parameters
+  are all-gathered in place.  Same bytes on the wire as one all-reduce, 1/W
+  of the optimizer's HBM traffic and moment memory per rank.
+* ``"allreduce"``: one all-reduce of the flat gradient bucket, replicated Adam.
+
+Both keep dense-Adam parity with the single-device run (Adam is elementwise).
 """
 from __future__ import annotations
 
@@ -12,6 +21,8 @@ import os
 
 import torch
 import torch.distributed as dist
+
+ALIGN = 64  # floats: flat-buffer segments and shards start 256-byte aligned
 
 
 def shard_range(global_rows: int, world: int, rank: int):
@@ -22,10 +33,65 @@ def shard_range(global_rows: int, world: int, rank: int):
     return lo, min(lo + per, global_rows)
 
 
+def shard_floats(total: int, world: int, align: int = ALIGN) -> int:
+    """Floats per rank of the flat buffer under the sharded optimizer: the
+    smallest multiple of `align` with world * shard >= total."""
+    per = (int(total) + world - 1) // world
+    return max(align, (per + align - 1) // align * align)
+
+
+def shard_ranges(ranges, world: int, rank: int, shard: int):
+    """Active [begin, end) float ranges of the flat buffer that fall inside rank's
+    shard [rank*shard, (rank+1)*shard), shifted to shard-local offsets."""
+    lo, hi = rank * shard, (rank + 1) * shard
+    out = []
+    for b, e in ranges:
+        b2, e2 = max(int(b), lo), min(int(e), hi)
+        if e2 > b2:
+            out.append([b2 - lo, e2 - lo])
+    return out
+
+
+def _native_ok(t: torch.Tensor, group) -> bool:
+    """reduce_scatter_tensor / all_gather_into_tensor straight on the backend:
+    always for RCCL ('nccl'); gloo only for host tensors.  gloo with device
+    tensors (the single-GPU multi-rank test) goes through exact all-reduce
+    forms instead."""
+    if os.environ.get("NCF_DP_EMULATE", "0") == "1":
+        return False
+    return dist.get_backend(group) != "gloo" or t.device.type == "cpu"
+
+
 def allreduce_flat_grads(flat: torch.Tensor, group=None):
     """Sum the flat gradient bucket over ranks (in place)."""
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    return flat
+
+
+def reduce_scatter_flat(out: torch.Tensor, inp: torch.Tensor, rank: int, group=None):
+    """out[:] = (sum over ranks of inp)[rank*S:(rank+1)*S], S = out.numel()."""
+    s = out.numel()
+    if _native_ok(inp, group):
+        dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group)
+    else:
+        dist.all_reduce(inp, op=dist.ReduceOp.SUM, group=group)
+        out.copy_(inp[rank * s:(rank + 1) * s])
+    return out
+
+
+def all_gather_flat(flat: torch.Tensor, rank: int, shard: int, group=None, scratch=None):
+    """In-place all-gather: every rank contributes flat[rank*S:(rank+1)*S]."""
+    mine = flat[rank * shard:(rank + 1) * shard]
+    if _native_ok(flat, group):
+        dist.all_gather_into_tensor(flat, mine, group=group)
+    else:
+        # exact: every other contribution is +0.0
+        tmp = scratch if scratch is not None else torch.empty_like(flat)
+        tmp.zero_()
+        tmp[rank * shard:(rank + 1) * shard].copy_(mine)
+        dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=group)
+        flat.copy_(tmp)
     return flat
 
 

@@ -9,10 +9,12 @@ with the all-reduce issued between them, see ``_capture_collective``):
                          bwd / embedding scatter-add   (models.py:97-118,
                          train_neumf.py:111-114)
   2. ``ncf_reduce_slab`` per-workgroup tower grads -> flat grad buffer
-  3. RCCL all-reduce of the flat grad buffer (world > 1 only; one bucket)
-  4. ``ncf_adam_step``   dense Adam over every active parameter + grad zeroing +
-                         loss bookkeeping + batch/step counters
+  3. world > 1, dp_mode "zero1" (default): RCCL reduce-scatter of the flat grad
+     buffer; dp_mode "allreduce": RCCL all-reduce of it
+  4. ``ncf_adam_step``   dense Adam over the active parameters (zero1: of this
+                         rank's shard only) + grad zeroing + loss bookkeeping
                          (train_neumf.py:90,115)
+  5. zero1 only: RCCL all-gather of the updated parameter shards (in place)
 
 Data parallelism: every rank holds the same epoch stream (same seeds, same
 sampler, same permutation); rank r processes rows [r*ceil(gb/W), ...) of each
@@ -27,6 +29,7 @@ import os
 import torch
 
 from . import _lib as L
+from . import distributed as D
 from . import ops
 
 
@@ -52,26 +55,56 @@ def _active_ranges(model, lay):
 
 class TrainEngine:
     def __init__(self, model, lr=1e-3, optimizer="adam", betas=(0.9, 0.999), eps=1e-8,
-                 world_size=1, rank=0, process_group=None, max_batches=1 << 16):
+                 world_size=1, rank=0, process_group=None, max_batches=1 << 16, dp_mode=None):
         self.model = model
-        self.flat, self.lay = ops.ensure_flat(model)
+        self.world_size, self.rank, self.group = int(world_size), int(rank), process_group
+        if dp_mode is None:
+            dp_mode = os.environ.get("NCF_DP_MODE", "zero1") if self.world_size > 1 else "single"
+        if self.world_size == 1:
+            dp_mode = "single"
+        if dp_mode not in ("single", "zero1", "allreduce"):
+            raise ValueError(f"dp_mode {dp_mode!r}")
+        self.dp_mode = dp_mode
+        lay = L.layout(model.user_num, model.item_num, model.factor_num, model.num_layers, model.model_type)
+        if dp_mode == "zero1":
+            # flat buffers padded to world x shard floats; rank r owns [r*S, (r+1)*S)
+            self.shard = D.shard_floats(int(lay.total), self.world_size)
+            n = self.shard * self.world_size
+        else:
+            self.shard = None
+            n = int(lay.total)
+        self.flat, self.lay = ops.ensure_flat(model, n)
         dev = self.flat.device
         self.device = dev
-        n = int(self.lay.total)
+        n = self.flat.numel()
         self.grads = torch.zeros(n, dtype=torch.float32, device=dev)
         self.optimizer = optimizer
+        n_opt = self.shard if dp_mode == "zero1" else n
         if optimizer == "adam":
-            self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
-            self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+            self.exp_avg = torch.zeros(n_opt, dtype=torch.float32, device=dev)
+            self.exp_avg_sq = torch.zeros(n_opt, dtype=torch.float32, device=dev)
         elif optimizer != "sgd":
             raise ValueError(optimizer)
         self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
         self.ws = None  # ncf_train_step workspace, sized by set_epoch_stream
         self.ctl = ops.new_ctl(0, dev)
-        self.world_size, self.rank, self.group = int(world_size), int(rank), process_group
         rng = _active_ranges(model, self.lay)
         self._ranges = (ctypes.c_int64 * (2 * len(rng)))(*[x for r in rng for x in r])
         self._nranges = len(rng)
+        self._loss_slot = int(self.lay.loss_slot)
+        self._opt_ptrs = (self.flat.data_ptr(), self.grads.data_ptr())
+        if dp_mode == "zero1":
+            S, r = self.shard, self.rank
+            self.gshard = torch.zeros(S, dtype=torch.float32, device=dev)
+            # an empty [0, 0) range when no active parameter falls in the shard: the
+            # launch still records the loss if this rank owns the loss slot
+            srng = D.shard_ranges(rng, self.world_size, r, S) or [[0, 0]]
+            self._sranges = (ctypes.c_int64 * (2 * len(srng)))(*[x for q in srng for x in q])
+            self._nsranges = len(srng)
+            self.loss_owner = self._loss_slot // S
+            self._loss_slot = self._loss_slot - r * S
+            self._opt_ptrs = (self.flat.data_ptr() + 4 * r * S, self.gshard.data_ptr())
+            self._ag_scratch = None
         self.loss_hist = torch.zeros(max_batches, dtype=torch.float32, device=dev)
         self.rows = None
         self.n_total = 0
@@ -115,26 +148,48 @@ class TrainEngine:
         L.check(lib.ncf_reduce_slab(lay, self.ws.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(), st), "ncf_reduce_slab")
 
     def _allreduce(self):
-        """Launch 3 (world > 1): sum of the flat gradient over ranks (RCCL on ROCm)."""
-        if self.world_size > 1:
-            import torch.distributed as dist
-            dist.all_reduce(self.grads, group=self.group)
+        """Launch 3 (world > 1): gradient exchange over ranks (RCCL on ROCm).
+        zero1: reduce-scatter of the flat gradient into this rank's shard;
+        allreduce: in-place sum of the whole flat gradient."""
+        if self.world_size == 1:
+            return
+        if self.dp_mode == "zero1":
+            D.reduce_scatter_flat(self.gshard, self.grads, self.rank, self.group)
+        else:
+            D.allreduce_flat_grads(self.grads, self.group)
+
+    def _allgather(self):
+        """Launch 5 (zero1): every rank's updated parameter shard to every rank."""
+        if self.dp_mode == "zero1":
+            if self._ag_scratch is None and not D._native_ok(self.flat, self.group):
+                self._ag_scratch = torch.empty_like(self.flat)
+            D.all_gather_flat(self.flat, self.rank, self.shard, self.group, self._ag_scratch)
 
     def _optimize(self):
-        """Launch 4: dense Adam / SGD + grad zeroing + loss bookkeeping."""
+        """Launch 4: dense Adam / SGD + grad zeroing + loss bookkeeping (zero1: over
+        this rank's shard; the full local gradient buffer is zeroed for the next
+        step's accumulation, and only the loss slot's owner records the loss)."""
         st = L.stream_ptr(self.device)
         lib = L.hip()
         hist_len = self.num_batches
+        if self.dp_mode == "zero1":
+            L.check(lib.ncf_zero_f32(self.grads.data_ptr(), self.grads.numel(), st), "ncf_zero_f32")
+            ranges, nr = self._sranges, self._nsranges
+            hist = self.loss_hist.data_ptr() if self.rank == self.loss_owner else None
+        else:
+            ranges, nr = self._ranges, self._nranges
+            hist = self.loss_hist.data_ptr()
+        p, g = self._opt_ptrs
         if self.optimizer == "adam":
-            L.check(lib.ncf_adam_step(self.flat.data_ptr(), self.grads.data_ptr(), self.exp_avg.data_ptr(),
-                                      self.exp_avg_sq.data_ptr(), self._ranges, self._nranges,
+            L.check(lib.ncf_adam_step(p, g, self.exp_avg.data_ptr(),
+                                      self.exp_avg_sq.data_ptr(), ranges, nr,
                                       self.ctl.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps,
-                                      self.lay.loss_slot, self.loss_hist.data_ptr(), hist_len, st),
+                                      self._loss_slot, hist, hist_len, st),
                     "ncf_adam_step")
         else:
-            L.check(lib.ncf_sgd_step(self.flat.data_ptr(), self.grads.data_ptr(), self._ranges, self._nranges,
-                                     self.ctl.data_ptr(), self.lr, self.lay.loss_slot,
-                                     self.loss_hist.data_ptr(), hist_len, st), "ncf_sgd_step")
+            L.check(lib.ncf_sgd_step(p, g, ranges, nr,
+                                     self.ctl.data_ptr(), self.lr, self._loss_slot,
+                                     hist, hist_len, st), "ncf_sgd_step")
 
     @property
     def _fused_optimizer(self):
@@ -166,6 +221,7 @@ class TrainEngine:
         self._compute()
         self._allreduce()
         self._optimize()
+        self._allgather()
 
     def time_kernels(self, n_steps):
         """Run n_steps eager steps with HIP events between the launches (on the
@@ -178,7 +234,10 @@ class TrainEngine:
                      ("ncf_reduce_slab", lambda: L.check(L.hip().ncf_reduce_slab(
                          ctypes.byref(self.lay), self.ws.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(),
                          L.stream_ptr(self.device)), "ncf_reduce_slab")),
-                     ("allreduce", self._allreduce), ("optimizer", self._optimize)]
+                     ("allreduce" if self.dp_mode != "zero1" else "reduce_scatter", self._allreduce),
+                     ("optimizer", self._optimize)]
+            if self.dp_mode == "zero1":
+                parts.append(("all_gather", self._allgather))
         acc = {k: 0.0 for k, _ in parts}
         evs = []
         for _ in range(n_steps):
@@ -268,6 +327,7 @@ class TrainEngine:
             self._graph[0].replay()
             self._allreduce()
             self._graph[1].replay()
+            self._allgather()
 
     def run(self, n_steps, use_graph=True):
         """n_steps consecutive optimizer steps (batches advance on device)."""
@@ -294,7 +354,18 @@ class TrainEngine:
             self._replay()
 
     def epoch_losses(self):
-        """Per-batch mean BCE of the last epoch (host copy)."""
+        """Per-batch mean BCE of the last epoch (host copy).  zero1: the rank owning
+        the loss slot recorded it; it is broadcast to the others (a collective: every
+        rank calls this)."""
+        if self.dp_mode == "zero1":
+            import torch.distributed as dist
+            h = self.loss_hist[: self.num_batches].clone()
+            if D._native_ok(h, self.group):
+                dist.broadcast(h, src=self.loss_owner, group=self.group)
+            else:
+                h = h.cpu()
+                dist.broadcast(h, src=self.loss_owner, group=self.group)
+            return h.double().cpu().numpy()
         return self.loss_hist[: self.num_batches].double().cpu().numpy()
 
     def state_step(self):

@@ -39,15 +39,17 @@ def active_mask(model):
     return [True] * (4 + n_tower + 2)
 
 
-def ensure_flat(model):
-    """Return (flat, layout) for a HIP-resident NCF, (re)packing if needed."""
+def ensure_flat(model, min_floats=0):
+    """Return (flat, layout) for a HIP-resident NCF, (re)packing if needed.
+    ``min_floats``: the flat buffer is at least this long (zero padding after
+    ``lay.total``; the sharded data-parallel optimizer needs world * shard floats)."""
     lay = getattr(model, "_ncf_layout", None)
     flat = getattr(model, "_ncf_flat", None)
     dev = model.embed_user_GMF.weight.device
     if lay is None:
         lay = L.layout(model.user_num, model.item_num, model.factor_num, model.num_layers, model.model_type)
         model._ncf_layout = lay
-    if flat is not None and flat.device == dev:
+    if flat is not None and flat.device == dev and flat.numel() >= min_floats:
         ok = all(p.data_ptr() == flat.data_ptr() + 4 * off for p, off in _segments(model, lay))
         if ok:
             return flat, lay
@@ -55,7 +57,7 @@ def ensure_flat(model):
         raise NotImplementedError(
             f"no HIP path for model_type={model.model_type} factor_num={model.factor_num} "
             f"num_layers={model.num_layers}")
-    flat = torch.zeros(int(lay.total), dtype=torch.float32, device=dev)
+    flat = torch.zeros(max(int(lay.total), int(min_floats)), dtype=torch.float32, device=dev)
     with torch.no_grad():
         for p, off in _segments(model, lay):
             n = p.numel()

@@ -91,3 +91,102 @@ def test_gloo_two_ranks_equal_single_process_gradient():
     _, _, grads = O.forward_backward(m, u[perm[:B]], i[perm[:B]], y[perm[:B]].astype(np.int64))
     ref = torch.cat([grads[k].reshape(-1) for k, _ in m.named_parameters()]).numpy()
     np.testing.assert_allclose(g0, ref, rtol=1e-5, atol=1e-9)
+
+
+# ---------------------------------------------------------------------------
+# zero1: reduce-scatter -> Adam on the own shard -> in-place all-gather
+# (ncf_amd.engine.TrainEngine(dp_mode="zero1"), the default for world > 1)
+
+def test_shard_floats_and_ranges_cover_active_params():
+    from ncf_amd.distributed import shard_floats, shard_ranges
+    active = [[0, 640], [1024, 1088], [4096, 9000]]
+    for total in (64, 1000, 9001, 790_737):
+        for W in (1, 2, 3, 4, 8):
+            S = shard_floats(total, W)
+            assert S % 64 == 0 and S * W >= total and (S - 64) * W < total
+            got = []
+            for r in range(W):
+                for b, e in shard_ranges(active, W, r, S):
+                    assert 0 <= b < e <= S and b % 4 == 0 and e % 4 == 0
+                    got.append([b + r * S, e + r * S])
+            covered = sorted(x for b, e in got for x in range(b, e))
+            want = sorted(x for b, e in active for x in range(b, min(e, S * W)))
+            assert covered == want
+
+
+def _zero1_worker(rank, world, port, emulate, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["NCF_DP_EMULATE"] = "1" if emulate else "0"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import ncf_oracle as O
+    from ncf_amd.distributed import all_gather_flat, reduce_scatter_flat, shard_floats, shard_range
+    torch.manual_seed(5)
+    m = O.OracleNCF(40, 60, 8, 3, 0.0, "NeuMF-end")
+    params = list(m.parameters())
+    n = sum(p.numel() for p in params)
+    S = shard_floats(n, world)
+    flat = torch.zeros(S * world)
+    flat[:n] = torch.cat([p.detach().reshape(-1) for p in params])
+    shard = torch.nn.Parameter(flat[rank * S:(rank + 1) * S].clone())
+    opt = torch.optim.Adam([shard], lr=1e-2)
+    rng = np.random.default_rng(2)
+    B = 257
+    for _ in range(3):
+        u, i = rng.integers(0, 40, B), rng.integers(0, 60, B)
+        y = (rng.random(B) < 0.3).astype(np.float32)
+        off = 0  # the gathered flat parameters back into the model
+        with torch.no_grad():
+            for p in params:
+                p.copy_(flat[off:off + p.numel()].view_as(p))
+                off += p.numel()
+        m.zero_grad()
+        lo, hi = shard_range(B, world, rank)
+        logit = m(torch.as_tensor(u[lo:hi]), torch.as_tensor(i[lo:hi]))
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(logit, torch.as_tensor(y[lo:hi]),
+                                                                    reduction="sum") / B
+        loss.backward()
+        g = torch.zeros(S * world)
+        g[:n] = torch.cat([p.grad.reshape(-1) for p in params])
+        gs = torch.zeros(S)
+        reduce_scatter_flat(gs, g, rank)
+        shard.grad = gs
+        opt.step()
+        with torch.no_grad():
+            flat[rank * S:(rank + 1) * S].copy_(shard)
+        all_gather_flat(flat, rank, S)
+    q.put((rank, flat[:n].numpy().copy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,emulate", [(2, False), (3, False), (2, True)])
+def test_gloo_zero1_matches_single_process_adam(world, emulate):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + (os.getpid() % 1000) + 10 * world + int(emulate)
+    procs = [ctx.Process(target=_zero1_worker, args=(r, world, port, emulate, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, f in res[1:]:
+        assert np.array_equal(f, res[0][1]), "ranks hold different parameters after the all-gather"
+    # single process, full-batch mean gradient, dense Adam over every parameter
+    from oracle import ncf_oracle as O
+    torch.manual_seed(5)
+    m = O.OracleNCF(40, 60, 8, 3, 0.0, "NeuMF-end")
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+    rng = np.random.default_rng(2)
+    B = 257
+    for _ in range(3):
+        u, i = rng.integers(0, 40, B), rng.integers(0, 60, B)
+        y = (rng.random(B) < 0.3).astype(np.float32)
+        opt.zero_grad()
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(m(torch.as_tensor(u), torch.as_tensor(i)),
+                                                                    torch.as_tensor(y))
+        loss.backward()
+        opt.step()
+    ref = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).numpy()
+    np.testing.assert_allclose(res[0][1], ref, rtol=1e-4, atol=1e-6)

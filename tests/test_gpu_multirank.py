@@ -1,13 +1,16 @@
 """Data-parallel engine on the GPU: two ranks (gloo, both on cuda:0, spawned
 processes) run TrainEngine with world_size=2 -- row shards inside
-ncf_train_step, the flat-gradient all-reduce between the compute and optimizer
-graphs, replicated Adam -- and must (a) stay bitwise identical to each other
+ncf_train_step, the gradient exchange between the compute and optimizer graphs
+(zero1: reduce-scatter, Adam on the rank's shard, in-place all-gather of the
+parameters; allreduce: all-reduce, replicated Adam) -- and must (a) stay
+bitwise identical to each other
 and (b) match a single-rank run over the same global batches (per-step loss
 rtol 1e-5; parameters rtol 1e-4 / atol 1e-6: the summed shard gradients differ
 from the full-batch gradient only in fp32 summation order).
 
 RCCL needs one GPU per rank, which the single-GPU test box does not have; gloo
-all-reduces the same device buffer through the host, so everything but the
+moves the same device buffers through the host (reduce-scatter / all-gather in
+their exact all-reduce forms, ncf_amd.distributed), so everything but the
 transport is the bench's N>1 path."""
 import os
 import socket
@@ -31,13 +34,13 @@ def _batches():
     return users, items, labels
 
 
-def _run(world, rank, group, mt, f, nl, use_graph):
+def _run(world, rank, group, mt, f, nl, use_graph, dp_mode=None):
     from ncf_amd import ops
     from ncf_amd.engine import TrainEngine
     from ncf_amd.models import NCF
     torch.manual_seed(3)
     m = NCF(U, I, f, nl, 0.0, mt).to("cuda:0")
-    eng = TrainEngine(m, lr=1e-3, world_size=world, rank=rank, process_group=group)
+    eng = TrainEngine(m, lr=1e-3, world_size=world, rank=rank, process_group=group, dp_mode=dp_mode)
     u, i, y = _batches()
     rows = torch.as_tensor(ops.pack_rows_host(u, i, y), device="cuda:0")
     eng.set_epoch_stream(rows, B)
@@ -47,13 +50,13 @@ def _run(world, rank, group, mt, f, nl, use_graph):
     return flat, eng.epoch_losses()[:T].copy()
 
 
-def _worker(rank, world, port, mt, f, nl, use_graph, q):
+def _worker(rank, world, port, mt, f, nl, use_graph, dp_mode, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
-    flat, losses = _run(world, rank, dist.group.WORLD, mt, f, nl, use_graph)
+    flat, losses = _run(world, rank, dist.group.WORLD, mt, f, nl, use_graph, dp_mode)
     q.put((rank, flat, losses))
     dist.barrier()
     dist.destroy_process_group()
@@ -65,14 +68,18 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("mt,f,nl,use_graph", [("NeuMF-end", 16, 3, True), ("NeuMF-end", 16, 3, False),
-                                               ("NeuMF-end", 32, 3, True)])
-def test_two_ranks_match_single_rank(mt, f, nl, use_graph):
+@pytest.mark.parametrize("mt,f,nl,use_graph,dp_mode", [("NeuMF-end", 16, 3, True, "zero1"),
+                                                       ("NeuMF-end", 16, 3, False, "zero1"),
+                                                       ("NeuMF-end", 16, 3, True, "allreduce"),
+                                                       ("NeuMF-end", 32, 3, True, "zero1"),
+                                                       ("GMF", 16, 3, True, "zero1")])
+def test_two_ranks_match_single_rank(mt, f, nl, use_graph, dp_mode):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mt, f, nl, use_graph, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mt, f, nl, use_graph, dp_mode, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {}
