@@ -31,7 +31,10 @@ def test_library_exports_every_declared_symbol(header, lib):
 
 def test_abi_version_and_layout():
     import ncf_amd._lib as L
-    assert L.hip().ncf_abi_version() == L.ABI_VERSION == 4
+    import re
+    hdr = open(os.path.join(ROOT, "include", "ncf_hip.h")).read()
+    want = int(re.search(r"#define NCF_ABI_VERSION (\d+)", hdr).group(1))
+    assert L.hip().ncf_abi_version() == L.ABI_VERSION == want
     for U, I, f, nl, mt in ((944, 1683, 8, 3, "NeuMF-end"), (6041, 3707, 16, 3, "NeuMF-end"), (50, 80, 8, 1, "GMF")):
         lay = L.layout(U, I, f, nl, mt)
         from ncf_amd.models import NCF
