@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 5
+#define NCF_ABI_VERSION 6
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -48,6 +48,7 @@ extern "C" {
 /* dz_mode of ncf_train_step */
 #define NCF_DZ_BCE 0    /* fused nn.BCEWithLogitsLoss() (mean) from labels (train_neumf.py:86,113) */
 #define NCF_DZ_DLOGIT 1 /* upstream dL/dlogit given per row (autograd backward of NCF.forward) */
+#define NCF_DZ_KD 2     /* distillation: w_task * BCE + w_resp * response term (ncf_train_step_kd) */
 
 /* Flat parameter buffer layout, offsets in floats.  Order and shapes follow the
  * reference state_dict (models.py:11-34): embed_user_GMF [U,f], embed_item_GMF [I,f],
@@ -124,6 +125,44 @@ int ncf_train_step(const ncf_layout *lay, const float *params, float *grads, con
                    const float *dlogit, ncf_step_ctl *ctl, int64_t batch_global, int world,
                    int rank, int dz_mode, void *workspace, int64_t workspace_bytes,
                    float *logits_out, void *stream);
+
+/*
+ * Distillation step of the student (src/distillation/base.py:36-50,
+ * response.py:15-32, feature.py:125-147, attention.py:81-102): ncf_train_step with
+ * dz_mode NCF_DZ_KD, i.e. per row of the global batch B
+ *   loss_i = w_task * bce(z_i, y_i) + w_resp * r_i,   loss = sum_i loss_i / B
+ *   temperature <= 0:  r_i = (z_i - t_i)^2                    (response.py:28-32)
+ *   temperature T > 0: r_i = T^2 (sigmoid(z_i/T) - sigmoid(t_i/T))^2   (base.py:27-34)
+ *   dL/dz_i = (w_task * (sigmoid(z_i) - y_i) + w_resp * dr_i/dz_i) / B
+ * teacher_logits[row]: the teacher's logit per row of the epoch stream (same indexing
+ * as rows; ncf_forward of the teacher over the stream).  Feature terms are added by
+ * ncf_kd_feature_step.
+ */
+int ncf_train_step_kd(const ncf_layout *lay, const float *params, float *grads, const uint64_t *rows,
+                      const float *teacher_logits, ncf_step_ctl *ctl, int64_t batch_global, int world,
+                      int rank, float w_task, float w_resp, float temperature, void *workspace,
+                      int64_t workspace_bytes,
+                      float *logits_out, void *stream);
+
+/*
+ * Feature distillation terms (src/distillation/feature.py:51-123) of the same batch
+ * as the preceding ncf_train_step[_kd] launch (reads ctl->batch; run it before
+ * ncf_reduce_slab / ncf_reduce_adam_step).  Two feature keys:
+ *   key 0 "gmf_features": x = Ug_s[u] * Ig_s[i] (f_s),   teacher Ug_t[u] * Ig_t[i] (f_t)
+ *   key 1 "mlp_input":    x = [Um_s[u] | Im_s[i]] (2dm_s), teacher [Um_t[u] | Im_t[i]] (2dm_t)
+ * a = A x + c (adapter nn.Linear [T, S] + bias [T]; A == NULL: identity, S == T);
+ * loss += coef_k / (B * T_k) * sum_o (a_o - x_t,o)^2 with coef_k = beta / count (0 skips
+ * the key); dL/dx = A^T (2 coef_k / (B T_k) (a - x_t)) is scatter-added into the student
+ * embedding gradients (GMF through the product rule).  The loss term is added to the
+ * loss column of slab row 0 of `workspace` (the student's train workspace).
+ * Limits: f_s, f_t <= 64; 2dm_s <= 1024; 2dm_t <= 2048.
+ */
+int ncf_kd_feature_step(const ncf_layout *student, const float *s_params, float *s_grads,
+                        const ncf_layout *teacher, const float *t_params, const uint64_t *rows,
+                        const ncf_step_ctl *ctl, int64_t batch_global, int world, int rank,
+                        const float *gmf_w, const float *gmf_b, float gmf_coef,
+                        const float *mlp_w, const float *mlp_b, float mlp_coef,
+                        void *workspace, void *stream);
 
 /* Forward only (NCF.forward under no_grad, metrics.py:11-12): logits[n] of rows[n].
  * workspace: ncf_forward_workspace_bytes(lay, n) bytes (may be NULL when that is 0). */

@@ -28,8 +28,8 @@ NCF_E_UNSUPPORTED = -1
 NCF_E_ARG = -2
 NCF_E_LAUNCH = -3
 MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
-DZ_BCE, DZ_DLOGIT = 0, 1
-ABI_VERSION = 5  # include/ncf_hip.h NCF_ABI_VERSION
+DZ_BCE, DZ_DLOGIT, DZ_KD = 0, 1, 2
+ABI_VERSION = 6  # include/ncf_hip.h NCF_ABI_VERSION
 PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
 
@@ -62,6 +62,12 @@ _HIP_PROTOS = {
     "ncf_slab_rows": (ctypes.c_int, []),
     "ncf_train_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_i64, c_vp, c_vp]),
+    "ncf_train_step_kd": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp,
+                                         c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                         ctypes.c_float, c_vp, c_i64, c_vp, c_vp]),
+    "ncf_kd_feature_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, ctypes.POINTER(NcfLayout), c_vp,
+                                           c_vp, c_vp, c_i64, ctypes.c_int, ctypes.c_int,
+                                           c_vp, c_vp, ctypes.c_float, c_vp, c_vp, ctypes.c_float, c_vp, c_vp]),
     "ncf_forward": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "ncf_workspace_bytes": (c_i64, [ctypes.POINTER(NcfLayout), c_i64]),
     "ncf_forward_workspace_bytes": (c_i64, [ctypes.POINTER(NcfLayout), c_i64]),

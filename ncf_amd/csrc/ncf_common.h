@@ -28,3 +28,17 @@ __device__ __forceinline__ float bce_loss(float x, float y) {
     return (1.0f - y) * x + m + logf(expf(-m) + expf(-x - m));
 }
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// Distillation response term of one row (src/distillation/base.py:27-34 with T > 0,
+// response.py:28-32 with T <= 0): *r = its per-row loss, returns d r / d z.
+__device__ __forceinline__ float kd_response(float z, float t, float T, float* r) {
+    if (T > 0.f) {
+        const float ss = sigmoidf_(z / T), st = sigmoidf_(t / T);
+        const float d = ss - st;
+        *r = d * d * (T * T);
+        return 2.f * T * d * (ss * (1.f - ss));
+    }
+    const float d = z - t;
+    *r = d * d;
+    return 2.f * d;
+}

@@ -86,6 +86,7 @@ struct TrainArgs {
     ncf_step_ctl* ctl;
     int64_t batch_global;
     int world, rank, dz_mode;
+    float kd_wt, kd_wr, kd_temp;  // NCF_DZ_KD: task / response weights, temperature (<= 0: logit MSE)
     float* slab;
     float* logits_out;
     int64_t fwd_n;  // FWD_ONLY: number of rows

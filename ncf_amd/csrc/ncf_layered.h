@@ -20,6 +20,7 @@ struct LyrArgs {
     ncf_step_ctl* ctl;       // train: batch selection; nullptr = forward over fwd_n rows
     int64_t batch_global, fwd_n;
     int world, rank, dz_mode;
+    float kd_wt, kd_wr, kd_temp;  // NCF_DZ_KD: task / response weights, temperature; dlogit = teacher logits
     float* slab;             // one row [tower_len + 64] of tower/predict partials (+ loss)
     float* logits_out;       // optional per-row logits
 };

@@ -377,6 +377,12 @@ __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float
                     const float y = (float)(uint32_t)(rw >> 63);
                     dz = (sigmoidf_(z) - y) / s.gb;
                     if (gl == 0) accL += bce_loss(z, y) / s.gb;
+                } else if (a.dz_mode == NCF_DZ_KD) {
+                    const float y = (float)(uint32_t)(rw >> 63);
+                    float rl;
+                    const float rg = kd_response(z, a.dlogit[s.base + m], a.kd_temp, &rl);
+                    dz = (a.kd_wt * (sigmoidf_(z) - y) + a.kd_wr * rg) / s.gb;
+                    if (gl == 0) accL += (a.kd_wt * bce_loss(z, y) + a.kd_wr * rl) / s.gb;
                 } else {
                     dz = a.dlogit[s.base + m];
                 }

@@ -592,6 +592,133 @@ static int ensure_lds(const void* fn, int64_t bytes) {
     return NCF_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Feature distillation terms (reference src/distillation/feature.py:51-123): one
+// wave per row of this rank's shard of the current global batch.  Per feature key:
+// the student feature x goes to the wave's LDS row, phase 1 (lanes over adapter
+// outputs o) forms a_o = c_o + A[o,:] x, the teacher feature and the loss, and
+// stores da_o = 2 coef (a_o - t_o) / (B T); phase 2 (lanes over inputs s) forms
+// dx_s = sum_o A[o,s] da_o and scatter-adds it into the student's embedding rows.
+// The adapters are small (at most [2048 x 1024]) and read through L1/L2.
+struct KdKey {
+    const float* A;  // [T][S] nn.Linear weight, nullptr = identity
+    const float* c;  // [T] bias
+    float coef;      // beta / count; 0 = key not matched
+    int S, T;
+};
+struct KdFeatArgs {
+    ncf_layout sl, tl;
+    const float* sp;
+    float* sg;
+    const float* tp;
+    const uint64_t* rows;
+    const ncf_step_ctl* ctl;
+    int64_t batch_global;
+    int world, rank;
+    KdKey key[2];
+    float* loss_out;
+};
+constexpr int KD_MAXS = 1024, KD_MAXT = 2048, KD_WAVES = 4;
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(256) void kd_feature_kernel(KdFeatArgs a) {
+    __shared__ float sx[KD_WAVES][KD_MAXS];
+    __shared__ float sd[KD_WAVES][KD_MAXT];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    // rows of this rank: the selection of ncf_train_step (ncf_train.hip)
+    const int64_t ntot = a.ctl->n_total;
+    const int64_t nbatch = (ntot + a.batch_global - 1) / a.batch_global;
+    const int64_t b = nbatch > 0 ? a.ctl->batch % nbatch : 0;
+    const int64_t b0 = b * a.batch_global;
+    int64_t gb = ntot - b0;
+    if (gb > a.batch_global) gb = a.batch_global;
+    if (gb < 0) gb = 0;
+    const int64_t per = (gb + a.world - 1) / a.world;
+    int64_t lo = (int64_t)a.rank * per, hi = lo + per;
+    if (lo > gb) lo = gb;
+    if (hi > gb) hi = gb;
+    const float gbf = (float)gb;
+    const ncf_layout& sl = a.sl;
+    const ncf_layout& tl = a.tl;
+    float lossw = 0.f;
+    for (int64_t r = lo + (int64_t)blockIdx.x * KD_WAVES + w; r < hi; r += (int64_t)gridDim.x * KD_WAVES) {
+        const uint64_t pr = a.rows[b0 + r];
+        const int u = (int)(uint32_t)pr;
+        const int it = (int)((pr >> 32) & 0x7fffffffu);
+        if (u < 0) continue;  // padding row (wave-uniform)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const KdKey K = a.key[k];
+            if (K.coef == 0.f) continue;
+            const int S = K.S, T = K.T;
+            const float scale = K.coef / (gbf * (float)T);
+            float us = 0.f, is = 0.f;
+            if (k == 0) {  // gmf_features = embed_user_GMF(u) * embed_item_GMF(i)  (feature.py:56-59)
+                if (l < S) {
+                    us = a.sp[sl.ug + (int64_t)u * S + l];
+                    is = a.sp[sl.ig + (int64_t)it * S + l];
+                    sx[w][l] = us * is;
+                }
+            } else {  // mlp_input = cat(embed_user_MLP(u), embed_item_MLP(i))  (feature.py:61-65)
+                const int dms = S / 2;
+                for (int s = l; s < S; s += 64)
+                    sx[w][s] = s < dms ? a.sp[sl.um + (int64_t)u * dms + s] : a.sp[sl.im + (int64_t)it * dms + (s - dms)];
+            }
+            wave_sync_lds();
+            for (int o = l; o < T; o += 64) {
+                float av;
+                if (K.A != nullptr) {  // adapter nn.Linear (feature.py:36-46, 97-100)
+                    const float* Ar = K.A + (int64_t)o * S;
+                    av = 0.f;
+                    for (int s = 0; s < S; ++s) av += Ar[s] * sx[w][s];
+                    av += K.c[o];
+                } else {
+                    av = sx[w][o];
+                }
+                float xt;
+                if (k == 0) {
+                    xt = a.tp[tl.ug + (int64_t)u * T + o] * a.tp[tl.ig + (int64_t)it * T + o];
+                } else {
+                    const int dmt = T / 2;
+                    xt = o < dmt ? a.tp[tl.um + (int64_t)u * dmt + o] : a.tp[tl.im + (int64_t)it * dmt + (o - dmt)];
+                }
+                const float d = av - xt;
+                lossw += scale * (d * d);     // F.mse_loss(student_feat, teacher_feat), feature.py:110
+                sd[w][o] = 2.f * scale * d;
+            }
+            wave_sync_lds();
+            for (int s = l; s < S; s += 64) {
+                float dx;
+                if (K.A != nullptr) {
+                    dx = 0.f;
+                    for (int o = 0; o < T; ++o) dx += K.A[(int64_t)o * S + s] * sd[w][o];
+                } else {
+                    dx = sd[w][s];
+                }
+                if (k == 0) {
+                    atomicAdd(a.sg + sl.ug + (int64_t)u * S + s, dx * is);
+                    atomicAdd(a.sg + sl.ig + (int64_t)it * S + s, dx * us);
+                } else {
+                    const int dms = S / 2;
+                    if (s < dms)
+                        atomicAdd(a.sg + sl.um + (int64_t)u * dms + s, dx);
+                    else
+                        atomicAdd(a.sg + sl.im + (int64_t)it * dms + (s - dms), dx);
+                }
+            }
+            wave_sync_lds();
+        }
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) lossw += __shfl_xor(lossw, m, 64);
+    if (l == 0 && lossw != 0.f) atomicAdd(a.loss_out, lossw);
+}
+
 int launch_zero_f32(float* p, int64_t n, hipStream_t st) {
     if (!p || n < 0 || (n & 3) || (reinterpret_cast<uintptr_t>(p) & 15)) return NCF_E_ARG;
     if (n == 0) return NCF_OK;
@@ -677,13 +804,15 @@ int64_t ncf_forward_workspace_bytes(const ncf_layout* lay, int64_t n) {
     return lyr_workspace_floats(lay, n, false) * 4;
 }
 
-int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
-                   const float* dlogit, ncf_step_ctl* ctl, int64_t batch_global, int world, int rank,
-                   int dz_mode, void* workspace, int64_t workspace_bytes, float* logits_out, void* stream) {
+static int train_step_impl(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
+                           const float* dlogit, ncf_step_ctl* ctl, int64_t batch_global, int world, int rank,
+                           int dz_mode, float kd_wt, float kd_wr, float kd_temp, void* workspace,
+                           int64_t workspace_bytes,
+                           float* logits_out, void* stream) {
     if (!lay || !params || !grads || !rows || !ctl || !workspace) return NCF_E_ARG;
     if (batch_global <= 0 || world < 1 || rank < 0 || rank >= world) return NCF_E_ARG;
-    if (dz_mode != NCF_DZ_BCE && dz_mode != NCF_DZ_DLOGIT) return NCF_E_ARG;
-    if (dz_mode == NCF_DZ_DLOGIT && !dlogit) return NCF_E_ARG;
+    if (dz_mode != NCF_DZ_BCE && dz_mode != NCF_DZ_DLOGIT && dz_mode != NCF_DZ_KD) return NCF_E_ARG;
+    if (dz_mode != NCF_DZ_BCE && !dlogit) return NCF_E_ARG;
     const int64_t rows_max = (batch_global + world - 1) / world;
     if (workspace_bytes < ncf_workspace_bytes(lay, rows_max)) return NCF_E_ARG;
     float* slab = static_cast<float*>(workspace);
@@ -701,6 +830,9 @@ int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, con
         la.world = world;
         la.rank = rank;
         la.dz_mode = dz_mode;
+        la.kd_wt = kd_wt;
+        la.kd_wr = kd_wr;
+        la.kd_temp = kd_temp;
         la.logits_out = logits_out;
         return lyr_run(la, slab, rows_max, true, (hipStream_t)stream);
     }
@@ -714,12 +846,15 @@ int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, con
     a.grads = grads;
     a.rows = rows;
     // BCE mode: point dlogit at the rows so the per-row load stays unconditional
-    a.dlogit = dz_mode == NCF_DZ_DLOGIT ? dlogit : reinterpret_cast<const float*>(rows);
+    a.dlogit = dz_mode != NCF_DZ_BCE ? dlogit : reinterpret_cast<const float*>(rows);
     a.ctl = ctl;
     a.batch_global = batch_global;
     a.world = world;
     a.rank = rank;
     a.dz_mode = dz_mode;
+    a.kd_wt = kd_wt;
+    a.kd_wr = kd_wr;
+    a.kd_temp = kd_temp;
     a.diag = g_diag;
     a.stamps = g_stamps;
     a.slab = slab;
@@ -728,6 +863,62 @@ int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, con
     if (hipLaunchKernel(e->train, dim3(SLAB_ROWS), dim3(NTHREADS), args, (size_t)lds, (hipStream_t)stream) !=
         hipSuccess)
         return NCF_E_LAUNCH;
+    return launch_status();
+}
+
+int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
+                   const float* dlogit, ncf_step_ctl* ctl, int64_t batch_global, int world, int rank,
+                   int dz_mode, void* workspace, int64_t workspace_bytes, float* logits_out, void* stream) {
+    if (dz_mode == NCF_DZ_KD) return NCF_E_ARG;  // ncf_train_step_kd carries the weights
+    return train_step_impl(lay, params, grads, rows, dlogit, ctl, batch_global, world, rank, dz_mode, 0.f, 0.f, 0.f,
+                           workspace, workspace_bytes, logits_out, stream);
+}
+
+int ncf_train_step_kd(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
+                      const float* teacher_logits, ncf_step_ctl* ctl, int64_t batch_global, int world, int rank,
+                      float w_task, float w_resp, float temperature, void* workspace, int64_t workspace_bytes,
+                      float* logits_out, void* stream) {
+    if (!teacher_logits) return NCF_E_ARG;
+    return train_step_impl(lay, params, grads, rows, teacher_logits, ctl, batch_global, world, rank, NCF_DZ_KD,
+                           w_task, w_resp, temperature, workspace, workspace_bytes, logits_out, stream);
+}
+
+int ncf_kd_feature_step(const ncf_layout* student, const float* s_params, float* s_grads, const ncf_layout* teacher,
+                        const float* t_params, const uint64_t* rows, const ncf_step_ctl* ctl, int64_t batch_global,
+                        int world, int rank, const float* gmf_w, const float* gmf_b, float gmf_coef,
+                        const float* mlp_w, const float* mlp_b, float mlp_coef, void* workspace, void* stream) {
+    if (!student || !s_params || !s_grads || !teacher || !t_params || !rows || !ctl || !workspace) return NCF_E_ARG;
+    if (batch_global <= 0 || world < 1 || rank < 0 || rank >= world) return NCF_E_ARG;
+    KdFeatArgs a;
+    memset(&a, 0, sizeof(a));
+    a.sl = *student;
+    a.tl = *teacher;
+    a.sp = s_params;
+    a.sg = s_grads;
+    a.tp = t_params;
+    a.rows = rows;
+    a.ctl = ctl;
+    a.batch_global = batch_global;
+    a.world = world;
+    a.rank = rank;
+    const int fs = student->factor_num, ft = teacher->factor_num;
+    const int ms = 2 * (student->factor_num << (student->num_layers - 1));
+    const int mt = 2 * (teacher->factor_num << (teacher->num_layers - 1));
+    a.key[0] = KdKey{gmf_w, gmf_b, gmf_coef, fs, ft};
+    a.key[1] = KdKey{mlp_w, mlp_b, mlp_coef, ms, mt};
+    for (int k = 0; k < 2; ++k) {
+        const KdKey& K = a.key[k];
+        if (K.coef == 0.f) continue;
+        if (K.A == nullptr && K.S != K.T) return NCF_E_ARG;   // identity needs equal widths
+        if (K.A != nullptr && K.c == nullptr) return NCF_E_ARG;
+        if (K.S > (k == 0 ? 64 : KD_MAXS) || K.T > (k == 0 ? 64 : KD_MAXT)) return NCF_E_UNSUPPORTED;
+    }
+    a.loss_out = static_cast<float*>(workspace) + student->tower_len;  // slab row 0, loss column
+    const int64_t per = (batch_global + world - 1) / world;
+    int64_t grid = (per + KD_WAVES - 1) / KD_WAVES;
+    if (grid > 2048) grid = 2048;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(kd_feature_kernel, dim3((unsigned)grid), dim3(64 * KD_WAVES), 0, (hipStream_t)stream, a);
     return launch_status();
 }
 

@@ -461,6 +461,13 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                     const float y = slab_[myq];
                     dz = (sigmoidf_(z) - y) / gb_f;
                     if (g == 0) lossAcc += bce_loss(z, y);
+                } else if (a.dz_mode == NCF_DZ_KD) {
+                    // distillation (base.py:40-50; response term: kd_response)
+                    const float y = slab_[myq];
+                    float rl;
+                    const float rg = kd_response(z, a.dlogit[base + row0 + myq], a.kd_temp, &rl);
+                    dz = (a.kd_wt * (sigmoidf_(z) - y) + a.kd_wr * rg) / gb_f;
+                    if (g == 0) lossAcc += a.kd_wt * bce_loss(z, y) + a.kd_wr * rl;
                 } else {
                     dz = slab_[myq];  // labels[] carries dL/dlogit
                 }

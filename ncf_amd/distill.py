@@ -1,0 +1,375 @@
+"""Knowledge distillation (config C5): the reference's ``src/distillation``
+classes with the same constructors, attributes, printed messages and loss
+arithmetic, plus the device plan that runs the student's training step fused.
+
+Reference (src/distillation/, paths relative to the reference root):
+  * ``BaseDistillation``       base.py:5-50   -- freezes the teacher; task loss
+    BCE-with-logits; kd(s, t) = MSE(sigmoid(s/T), sigmoid(t/T)) * T^2
+  * ``ResponseDistillation``   response.py:6-32   -- kd overridden by the logit MSE
+  * ``SoftTargetDistillation`` response.py:34-61
+  * ``FeatureDistillation``    feature.py:6-147   -- nn.Linear adapters per mismatched
+    key (created in __init__, so they consume the torch generator like the reference)
+  * ``AttentionDistillation``  attention.py:6-102
+  * ``UnifiedDistillation``    -- the reference file src/distillation/unified.py is EMPTY
+    (0 bytes) although scripts/train_student.py:19,120-127 imports and constructs it.
+    Defined here as alpha*task + max(0, 1-alpha-beta-gamma)*kd + beta*feature +
+    gamma*attention (parity unpinned: no reference output exists).
+
+Two ways to run them:
+  * ``module(user, item, label) -> loss`` (the reference's API): the teacher and
+    student forwards go through ``NCF.forward`` -- on a HIP device that is the
+    fused forward kernel and, for the student, its autograd backward -- and the
+    small loss terms are torch ops.
+  * ``module.device_plan()`` -> ``DeviceDistillPlan`` for ``TrainEngine(distill=...)``
+    (what ``scripts/train_student.py`` uses): the teacher's logits for the whole
+    epoch stream come from one ``ncf_forward`` launch per epoch; each step is
+    ``ncf_train_step_kd`` (BCE + response term fused into the student's step) +
+    ``ncf_kd_feature_step`` (feature terms) + the usual reduce/Adam launches.
+    The attention term is identically zero (below) and contributes nothing on the
+    device path.
+
+Why attention is zero: ``compute_attention_map`` (attention.py:16-28) takes the
+L2 norm of an L2-normalised row -- 1 for every non-zero row -- and softmaxes it
+over the batch, so both maps are uniform and the KL term is 0 up to rounding
+(~1e-16 here), with a gradient of the same order.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib as L
+from . import ops
+
+
+class BaseDistillation(nn.Module):
+    """base.py:5-50."""
+
+    def __init__(self, teacher_model, student_model, temperature=2.0, alpha=0.5):
+        super().__init__()
+        self.teacher_model = teacher_model
+        self.student_model = student_model
+        self.temperature = temperature
+        self.alpha = alpha
+        for param in self.teacher_model.parameters():
+            param.requires_grad = False
+        self.teacher_model.eval()
+
+    def forward(self, user, item, label):
+        raise NotImplementedError("Subclasses must implement forward method")
+
+    def knowledge_distillation_loss(self, teacher_logits, student_logits):
+        teacher_probs = torch.sigmoid(teacher_logits / self.temperature)
+        student_probs = torch.sigmoid(student_logits / self.temperature)
+        return F.mse_loss(student_probs, teacher_probs) * (self.temperature ** 2)
+
+    def task_loss(self, predictions, labels):
+        return F.binary_cross_entropy_with_logits(predictions, labels)
+
+    def combined_loss(self, teacher_logits, student_logits, labels):
+        task_loss = self.task_loss(student_logits, labels)
+        kd_loss = self.knowledge_distillation_loss(teacher_logits, student_logits)
+        return self.alpha * task_loss + (1 - self.alpha) * kd_loss
+
+    # ---- device plan: subclasses set the weights of the fused step
+    _temperature_kd = True  # response term: kd() (True) or the logit MSE (False)
+
+    def _weights(self):
+        """(w_task, w_resp, beta) of the loss as a function of the student logit."""
+        return self.alpha, 1 - self.alpha, 0.0
+
+    def device_plan(self):
+        wt, wr, beta = self._weights()
+        return DeviceDistillPlan(self.teacher_model, self.student_model, wt, wr,
+                                 self.temperature if self._temperature_kd else 0.0, beta,
+                                 getattr(self, "adaptation_layers", None))
+
+
+class ResponseDistillation(BaseDistillation):
+    """response.py:6-32: alpha * BCE + (1 - alpha) * MSE(student_logits, teacher_logits)."""
+
+    _temperature_kd = False
+
+    def __init__(self, teacher_model, student_model, temperature=2.0, alpha=0.5):
+        super().__init__(teacher_model, student_model, temperature, alpha)
+
+    def forward(self, user, item, label):
+        with torch.no_grad():
+            teacher_logits = self.teacher_model(user, item)
+        student_logits = self.student_model(user, item)
+        return self.combined_loss(teacher_logits, student_logits, label)
+
+    def knowledge_distillation_loss(self, teacher_logits, student_logits):
+        return F.mse_loss(student_logits, teacher_logits)
+
+
+class SoftTargetDistillation(BaseDistillation):
+    """response.py:34-61."""
+
+    def __init__(self, teacher_model, student_model, temperature=4.0, alpha=0.7):
+        super().__init__(teacher_model, student_model, temperature, alpha)
+
+    def forward(self, user, item, label):
+        with torch.no_grad():
+            teacher_logits = self.teacher_model(user, item)
+        student_logits = self.student_model(user, item)
+        teacher_soft = torch.sigmoid(teacher_logits / self.temperature)
+        student_soft = torch.sigmoid(student_logits / self.temperature)
+        soft_loss = F.mse_loss(student_soft, teacher_soft)
+        hard_loss = self.task_loss(student_logits, label)
+        return self.alpha * hard_loss + (1 - self.alpha) * soft_loss * (self.temperature ** 2)
+
+
+def extract_features(model, user, item):
+    """feature.py:51-81 (features of every model: all four tables always exist)."""
+    features = {}
+    if hasattr(model, "embed_user_GMF"):
+        features["gmf_features"] = model.embed_user_GMF(user) * model.embed_item_GMF(item)
+    if hasattr(model, "embed_user_MLP"):
+        concat = torch.cat((model.embed_user_MLP(user), model.embed_item_MLP(item)), -1)
+        features["mlp_input"] = concat
+        if hasattr(model, "MLP_layers"):
+            x = concat
+            layer_idx = 0
+            for layer in model.MLP_layers:
+                if isinstance(layer, nn.Linear):
+                    x = layer(x)
+                    features[f"mlp_linear_{layer_idx}"] = x
+                    layer_idx += 1
+                elif isinstance(layer, nn.ReLU):
+                    x = layer(x)
+                    features[f"mlp_relu_{layer_idx - 1}"] = x
+    return features
+
+
+def _feature_dims(model):
+    """Widths of the feature keys of extract_features without running it."""
+    dm = model.factor_num * 2 ** (model.num_layers - 1)
+    d = {"gmf_features": model.factor_num, "mlp_input": 2 * dm}
+    w = 2 * dm
+    for k in range(model.num_layers):
+        w //= 2
+        d[f"mlp_linear_{k}"] = w
+        d[f"mlp_relu_{k}"] = w
+    return d
+
+
+class FeatureDistillation(BaseDistillation):
+    """feature.py:6-147."""
+
+    def __init__(self, teacher_model, student_model, temperature=2.0, alpha=0.5, beta=0.3):
+        super().__init__(teacher_model, student_model, temperature, alpha)
+        self.beta = beta
+        self.adaptation_layers = nn.ModuleDict()
+        self._setup_adaptation_layers()
+
+    def _setup_adaptation_layers(self):
+        teacher_gmf_dim = self.teacher_model.embed_user_GMF.embedding_dim
+        student_gmf_dim = self.student_model.embed_user_GMF.embedding_dim
+        teacher_mlp_user_dim = self.teacher_model.embed_user_MLP.embedding_dim
+        student_mlp_user_dim = self.student_model.embed_user_MLP.embedding_dim
+        teacher_mlp_item_dim = self.teacher_model.embed_item_MLP.embedding_dim
+        student_mlp_item_dim = self.student_model.embed_item_MLP.embedding_dim
+        print(f"Teacher dims: GMF={teacher_gmf_dim}, MLP_user={teacher_mlp_user_dim}")
+        print(f"Student dims: GMF={student_gmf_dim}, MLP_user={student_mlp_user_dim}")
+        if teacher_gmf_dim != student_gmf_dim:
+            self.adaptation_layers["gmf_features"] = nn.Linear(student_gmf_dim, teacher_gmf_dim)
+            print(f"Created GMF adapter: {student_gmf_dim} -> {teacher_gmf_dim}")
+        teacher_mlp_concat_dim = teacher_mlp_user_dim + teacher_mlp_item_dim
+        student_mlp_concat_dim = student_mlp_user_dim + student_mlp_item_dim
+        if teacher_mlp_concat_dim != student_mlp_concat_dim:
+            self.adaptation_layers["mlp_input"] = nn.Linear(student_mlp_concat_dim, teacher_mlp_concat_dim)
+            print(f"Created MLP input adapter: {student_mlp_concat_dim} -> {teacher_mlp_concat_dim}")
+
+    def extract_features(self, model, user, item):
+        return extract_features(model, user, item)
+
+    def feature_matching_loss(self, teacher_features, student_features):
+        total_loss = 0
+        count = 0
+        teacher_feat = None
+        for key in teacher_features:
+            if key in student_features:
+                teacher_feat = teacher_features[key]
+                student_feat = student_features[key]
+                if teacher_feat.shape != student_feat.shape:
+                    if key in self.adaptation_layers:
+                        student_feat = self.adaptation_layers[key](student_feat)
+                    else:
+                        print(f"Warning: Skipping {key} - no adapter available "
+                              f"(teacher: {teacher_feat.shape}, student: {student_feat.shape})")
+                        continue
+                total_loss += F.mse_loss(student_feat, teacher_feat)
+                count += 1
+        if count == 0:
+            print("Warning: No features could be matched!")
+            return torch.tensor(0.0, device=teacher_feat.device if teacher_feat is not None else "cpu")
+        return total_loss / count
+
+    def forward(self, user, item, label):
+        with torch.no_grad():
+            teacher_features = self.extract_features(self.teacher_model, user, item)
+            teacher_logits = self.teacher_model(user, item)
+        student_features = self.extract_features(self.student_model, user, item)
+        student_logits = self.student_model(user, item)
+        task_loss = self.task_loss(student_logits, label)
+        response_loss = self.knowledge_distillation_loss(teacher_logits, student_logits)
+        feature_loss = self.feature_matching_loss(teacher_features, student_features)
+        remaining_weight = max(0, 1 - self.alpha - self.beta)
+        return self.alpha * task_loss + remaining_weight * response_loss + self.beta * feature_loss
+
+    def _weights(self):
+        return self.alpha, max(0, 1 - self.alpha - self.beta), self.beta
+
+
+class AttentionDistillation(BaseDistillation):
+    """attention.py:6-102."""
+
+    def __init__(self, teacher_model, student_model, temperature=2.0, alpha=0.5, gamma=0.2):
+        super().__init__(teacher_model, student_model, temperature, alpha)
+        self.gamma = gamma
+
+    def compute_attention_map(self, features):
+        features_norm = F.normalize(features, p=2, dim=-1)
+        attention = torch.norm(features_norm, p=2, dim=-1, keepdim=True)
+        return F.softmax(attention, dim=0)
+
+    def extract_attention_features(self, model, user, item):
+        out = {}
+        if hasattr(model, "embed_user_GMF"):
+            out["gmf_attention"] = self.compute_attention_map(model.embed_user_GMF(user) * model.embed_item_GMF(item))
+        if hasattr(model, "embed_user_MLP"):
+            concat = torch.cat((model.embed_user_MLP(user), model.embed_item_MLP(item)), -1)
+            out["mlp_attention"] = self.compute_attention_map(concat)
+        return out
+
+    def attention_transfer_loss(self, teacher_attention, student_attention):
+        total_loss = 0
+        count = 0
+        for key in teacher_attention:
+            if key in student_attention:
+                eps = 1e-8
+                t = teacher_attention[key].view(-1) + eps
+                s = student_attention[key].view(-1) + eps
+                t = t / t.sum()
+                s = s / s.sum()
+                total_loss += F.kl_div(torch.log(s), t, reduction="batchmean")
+                count += 1
+        return total_loss / max(count, 1)
+
+    def forward(self, user, item, label):
+        with torch.no_grad():
+            teacher_attention = self.extract_attention_features(self.teacher_model, user, item)
+            teacher_logits = self.teacher_model(user, item)
+        student_attention = self.extract_attention_features(self.student_model, user, item)
+        student_logits = self.student_model(user, item)
+        task_loss = self.task_loss(student_logits, label)
+        response_loss = self.knowledge_distillation_loss(teacher_logits, student_logits)
+        attention_loss = self.attention_transfer_loss(teacher_attention, student_attention)
+        return (self.alpha * task_loss + (1 - self.alpha - self.gamma) * response_loss
+                + self.gamma * attention_loss)
+
+    def _weights(self):
+        return self.alpha, 1 - self.alpha - self.gamma, 0.0
+
+
+class UnifiedDistillation(FeatureDistillation):
+    """Referenced by scripts/train_student.py:19,120-127; the reference's
+    src/distillation/unified.py is empty.  This build's definition (unpinned):
+    alpha * task + max(0, 1 - alpha - beta - gamma) * kd + beta * feature + gamma * attention."""
+
+    def __init__(self, teacher_model, student_model, temperature=2.0, alpha=0.5, beta=0.3, gamma=0.2):
+        super().__init__(teacher_model, student_model, temperature, alpha, beta)
+        self.gamma = gamma
+
+    compute_attention_map = AttentionDistillation.compute_attention_map
+    extract_attention_features = AttentionDistillation.extract_attention_features
+    attention_transfer_loss = AttentionDistillation.attention_transfer_loss
+
+    def forward(self, user, item, label):
+        with torch.no_grad():
+            tf = self.extract_features(self.teacher_model, user, item)
+            ta = self.extract_attention_features(self.teacher_model, user, item)
+            teacher_logits = self.teacher_model(user, item)
+        sf = self.extract_features(self.student_model, user, item)
+        sa = self.extract_attention_features(self.student_model, user, item)
+        student_logits = self.student_model(user, item)
+        rest = max(0, 1 - self.alpha - self.beta - self.gamma)
+        return (self.alpha * self.task_loss(student_logits, label)
+                + rest * self.knowledge_distillation_loss(teacher_logits, student_logits)
+                + self.beta * self.feature_matching_loss(tf, sf)
+                + self.gamma * self.attention_transfer_loss(ta, sa))
+
+    def _weights(self):
+        return self.alpha, max(0, 1 - self.alpha - self.beta - self.gamma), self.beta
+
+
+# ---------------------------------------------------------------------------
+class DeviceDistillPlan:
+    """What TrainEngine(distill=plan) launches per student step (see module doc).
+
+    Feature keys on the device: 'gmf_features' and 'mlp_input' (adapter or identity).
+    The tower keys (mlp_linear_k / mlp_relu_k) match only when teacher and student
+    MLP widths agree (dm_t == dm_s), which the scripts' shapes never produce
+    (student factor_num = teacher's / 2, num_layers = teacher's - 1); that case
+    needs gradients into the student's tower activations and raises
+    NotImplementedError here."""
+
+    def __init__(self, teacher, student, w_task, w_resp, temperature, beta, adapters):
+        self.teacher, self.student = teacher, student
+        self.w_task, self.w_resp, self.temperature = float(w_task), float(w_resp), float(temperature)
+        self.beta = float(beta)
+        dev = student.embed_user_GMF.weight.device
+        if teacher.embed_user_GMF.weight.device != dev:
+            raise ValueError("teacher and student must be on the same device")
+        self.t_flat, self.t_lay = ops.ensure_flat(teacher)
+        self.tlog = None
+        self.keys = {}
+        self.active_extra = None
+        if self.beta != 0.0:
+            td, sd = _feature_dims(teacher), _feature_dims(student)
+            matched = [k for k in td if k in sd and (td[k] == sd[k] or k in (adapters or {}))]
+            tower = [k for k in matched if k.startswith("mlp_linear") or k.startswith("mlp_relu")]
+            if tower:
+                raise NotImplementedError(f"feature distillation through matched tower features {tower} "
+                                          "(teacher and student MLP widths equal) has no device path")
+            coef = self.beta / len(matched)
+            for k in ("gmf_features", "mlp_input"):
+                if k not in matched:
+                    continue
+                lin = adapters[k] if adapters is not None and k in adapters else None
+                if lin is not None:
+                    w = lin.weight.detach().to(dev, torch.float32).contiguous()
+                    b = lin.bias.detach().to(dev, torch.float32).contiguous()
+                    self.keys[k] = (w, b, coef)
+                else:
+                    self.keys[k] = (None, None, coef)
+            # the feature terms reach every student embedding table (feature.py:56-65)
+            self.active_extra = [True] * 4 + [False] * (2 * student.num_layers + 2)
+
+    def teacher_logits(self, rows):
+        n = rows.numel()
+        if self.tlog is None or self.tlog.numel() != n:
+            self.tlog = torch.empty(n, dtype=torch.float32, device=rows.device)
+        with torch.no_grad():
+            ops.forward_logits(self.t_flat, self.t_lay, rows, out=self.tlog, ws_owner=self.teacher)
+
+    def launch(self, eng, st):
+        lib = L.hip()
+        L.check(lib.ncf_train_step_kd(ctypes.byref(eng.lay), eng.flat.data_ptr(), eng.grads.data_ptr(),
+                                      eng.rows.data_ptr(), self.tlog.data_ptr(), eng.ctl.data_ptr(),
+                                      eng.batch_size, eng.world_size, eng.rank, self.w_task, self.w_resp,
+                                      self.temperature, eng.ws.data_ptr(), eng.ws.numel() * 4, None, st),
+                "ncf_train_step_kd")
+        if self.keys:
+            g = self.keys.get("gmf_features", (None, None, 0.0))
+            m = self.keys.get("mlp_input", (None, None, 0.0))
+            ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+            L.check(lib.ncf_kd_feature_step(ctypes.byref(eng.lay), eng.flat.data_ptr(), eng.grads.data_ptr(),
+                                            ctypes.byref(self.t_lay), self.t_flat.data_ptr(), eng.rows.data_ptr(),
+                                            eng.ctl.data_ptr(), eng.batch_size, eng.world_size, eng.rank,
+                                            ptr(g[0]), ptr(g[1]), g[2], ptr(m[0]), ptr(m[1]), m[2],
+                                            eng.ws.data_ptr(), st), "ncf_kd_feature_step")

@@ -33,15 +33,20 @@ from . import distributed as D
 from . import ops
 
 
-def _active_ranges(model, lay):
-    """Merged [begin, end) float ranges of the parameters that get gradients."""
+def _active_ranges(model, lay, extra=None):
+    """Merged [begin, end) float ranges of the parameters that get gradients
+    (``extra``: per-parameter mask OR-ed in, e.g. the embedding tables that the
+    feature-distillation terms reach)."""
     segs = []
     sizes = [p.numel() for p in model.ordered_params()]
     offs = [lay.ug, lay.ig, lay.um, lay.im]
     for k in range(model.num_layers):
         offs += [lay.w[k], lay.b[k]]
     offs += [lay.wp, lay.bp]
-    for off, n, act in zip(offs, sizes, ops.active_mask(model)):
+    mask = ops.active_mask(model)
+    if extra is not None:
+        mask = [a or b for a, b in zip(mask, extra)]
+    for off, n, act in zip(offs, sizes, mask):
         if act:
             segs.append([int(off), int(off + (n + 63) // 64 * 64)])
     merged = []
@@ -55,8 +60,12 @@ def _active_ranges(model, lay):
 
 class TrainEngine:
     def __init__(self, model, lr=1e-3, optimizer="adam", betas=(0.9, 0.999), eps=1e-8,
-                 world_size=1, rank=0, process_group=None, max_batches=1 << 16, dp_mode=None):
+                 world_size=1, rank=0, process_group=None, max_batches=1 << 16, dp_mode=None, distill=None):
+        """distill: an ``ncf_amd.distill.DeviceDistillPlan`` -- the student step then
+        runs ncf_train_step_kd (teacher logits of the epoch stream computed once per
+        epoch by ncf_forward) plus ncf_kd_feature_step for the feature terms."""
         self.model = model
+        self.distill = distill
         self.world_size, self.rank, self.group = int(world_size), int(rank), process_group
         if dp_mode is None:
             dp_mode = os.environ.get("NCF_DP_MODE", "zero1") if self.world_size > 1 else "single"
@@ -88,7 +97,7 @@ class TrainEngine:
         self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
         self.ws = None  # ncf_train_step workspace, sized by set_epoch_stream
         self.ctl = ops.new_ctl(0, dev)
-        rng = _active_ranges(model, self.lay)
+        rng = _active_ranges(model, self.lay, None if distill is None else distill.active_extra)
         self._ranges = (ctypes.c_int64 * (2 * len(rng)))(*[x for r in rng for x in r])
         self._nranges = len(rng)
         self._loss_slot = int(self.lay.loss_slot)
@@ -130,6 +139,10 @@ class TrainEngine:
         self.ctl[0] = 0
         self.ctl[2] = n
         self.ctl[3] = 0
+        if self.distill is not None:
+            # the frozen teacher's logit for every row of the epoch stream (one
+            # forward launch per epoch instead of one no_grad forward per step)
+            self.distill.teacher_logits(rows)
 
     @property
     def num_batches(self):
@@ -139,13 +152,9 @@ class TrainEngine:
     def _compute(self):
         """Launches 1-2: fused (or layered) step + slab reduction (advances ctl)."""
         st = L.stream_ptr(self.device)
-        lib = L.hip()
-        lay = ctypes.byref(self.lay)
-        L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.rows.data_ptr(),
-                                   None, self.ctl.data_ptr(),
-                                   self.batch_size, self.world_size, self.rank, L.DZ_BCE,
-                                   self.ws.data_ptr(), self.ws.numel() * 4, None, st), "ncf_train_step")
-        L.check(lib.ncf_reduce_slab(lay, self.ws.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(), st), "ncf_reduce_slab")
+        self._train_launch()
+        L.check(L.hip().ncf_reduce_slab(ctypes.byref(self.lay), self.ws.data_ptr(), self.grads.data_ptr(),
+                                        self.ctl.data_ptr(), st), "ncf_reduce_slab")
 
     def _allreduce(self):
         """Launch 3 (world > 1): gradient exchange over ranks (RCCL on ROCm).
@@ -199,6 +208,9 @@ class TrainEngine:
 
     def _train_launch(self):
         st = L.stream_ptr(self.device)
+        if self.distill is not None:
+            self.distill.launch(self, st)
+            return
         L.check(L.hip().ncf_train_step(ctypes.byref(self.lay), self.flat.data_ptr(), self.grads.data_ptr(),
                                        self.rows.data_ptr(), None, self.ctl.data_ptr(), self.batch_size,
                                        self.world_size, self.rank, L.DZ_BCE, self.ws.data_ptr(),

@@ -35,7 +35,9 @@ from .metrics import evaluate_arrays
 class Trainer:
     def __init__(self, model, train_dataset: NCFData, test_loader=None, *, batch_size=256, lr=1e-3,
                  optimizer="adam", top_k=10, device=None, world_size=1, rank=0, process_group=None,
-                 use_graph=True, save_path=None, verbose=True, test_batch=None):
+                 use_graph=True, save_path=None, verbose=True, test_batch=None, distill=None):
+        """distill: a distillation module (ncf_amd.distill) whose student is `model`:
+        every step then trains the student on that module's loss (device plan)."""
         self.model = model
         self.ds = train_dataset
         self.test_loader = test_loader
@@ -47,8 +49,11 @@ class Trainer:
         if model.embed_user_GMF.weight.device != self.device:
             model.to(self.device)
         self.world_size, self.rank = int(world_size), int(rank)
+        if distill is not None and distill.student_model is not model:
+            raise ValueError("distill.student_model must be the model being trained")
+        plan = distill.device_plan() if distill is not None else None
         self.engine = TrainEngine(model, lr=lr, optimizer=optimizer, world_size=world_size, rank=rank,
-                                  process_group=process_group)
+                                  process_group=process_group, distill=plan)
         self.use_graph = use_graph
         self.save_path = save_path
         self.verbose = verbose and self.rank == 0

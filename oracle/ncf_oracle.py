@@ -209,3 +209,107 @@ def metrics_np(logits, items, batch_size, top_k):
 
 def flat_state(model):
     return {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+
+
+# ---------------------------------------------------------------------------
+# Knowledge distillation (config C5): restatement of src/distillation/*.py as
+# stock torch CPU ops.  Pinned by tests/golden/G8_distill.npz (reference run).
+
+class OracleDistill(nn.Module):
+    """``strategy`` in {"response", "feature", "attention", "unified"}.
+
+    * task loss      F.binary_cross_entropy_with_logits        (base.py:36-38)
+    * kd(s, t)       MSE(sigmoid(s / T), sigmoid(t / T)) * T^2   (base.py:27-34; Feature- and
+                     AttentionDistillation inherit it)
+    * response       alpha * task + (1 - alpha) * MSE(s, t)      (base.py:40-50; response.py:28-32
+                     overrides kd with the plain logit MSE)
+    * feature        alpha * task + max(0, 1 - alpha - beta) * kd(s, t) + beta * mean over
+                     matched keys of MSE(adapter(student feature), teacher feature)
+                     (feature.py:12-147; adapters nn.Linear(S, T) built in key order, :36-46;
+                     unmatched keys skipped, :97-106)
+    * attention      alpha * task + (1 - alpha - gamma) * kd(s, t) + gamma * mean over keys of
+                     KL(softmax_batch(||normalize(f)||) ...)      (attention.py:16-102)
+    * unified        the reference file is empty (src/distillation/unified.py, 0 bytes):
+                     alpha * task + max(0, 1 - alpha - beta - gamma) * kd + beta * feature
+                     + gamma * attention -- this build's definition, parity unpinned.
+    """
+
+    def __init__(self, teacher, student, strategy="response", temperature=2.0, alpha=0.5, beta=0.3, gamma=0.2):
+        super().__init__()
+        self.teacher, self.student = teacher, student
+        self.strategy, self.temperature = strategy, temperature
+        self.alpha, self.beta, self.gamma = alpha, beta, gamma
+        for p in teacher.parameters():
+            p.requires_grad = False
+        teacher.eval()
+        self.adaptation_layers = nn.ModuleDict()
+        if strategy in ("feature", "unified"):
+            tg, sg = teacher.embed_user_GMF.embedding_dim, student.embed_user_GMF.embedding_dim
+            if tg != sg:
+                self.adaptation_layers["gmf_features"] = nn.Linear(sg, tg)
+            tm = teacher.embed_user_MLP.embedding_dim + teacher.embed_item_MLP.embedding_dim
+            sm = student.embed_user_MLP.embedding_dim + student.embed_item_MLP.embedding_dim
+            if tm != sm:
+                self.adaptation_layers["mlp_input"] = nn.Linear(sm, tm)
+
+    @staticmethod
+    def features(model, u, i):
+        f = {"gmf_features": model.embed_user_GMF(u) * model.embed_item_GMF(i)}
+        x = torch.cat((model.embed_user_MLP(u), model.embed_item_MLP(i)), -1)
+        f["mlp_input"] = x
+        k = 0
+        for layer in model.MLP_layers:
+            if isinstance(layer, nn.Linear):
+                x = layer(x)
+                f[f"mlp_linear_{k}"] = x
+                k += 1
+            elif isinstance(layer, nn.ReLU):
+                x = layer(x)
+                f[f"mlp_relu_{k - 1}"] = x
+        return f
+
+    def feature_loss(self, tf, sf):
+        tot, cnt = 0, 0
+        for key, t in tf.items():
+            if key not in sf:
+                continue
+            s = sf[key]
+            if t.shape != s.shape:
+                if key not in self.adaptation_layers:
+                    continue
+                s = self.adaptation_layers[key](s)
+            tot = tot + torch.nn.functional.mse_loss(s, t)
+            cnt += 1
+        return tot / cnt if cnt else torch.tensor(0.0)
+
+    @staticmethod
+    def attention_loss(tf, sf):
+        def att(x):
+            a = torch.norm(torch.nn.functional.normalize(x, p=2, dim=-1), p=2, dim=-1, keepdim=True)
+            return torch.nn.functional.softmax(a, dim=0)
+        tot, cnt = 0, 0
+        for key in ("gmf_features", "mlp_input"):
+            ta, sa = att(tf[key]).view(-1) + 1e-8, att(sf[key]).view(-1) + 1e-8
+            ta, sa = ta / ta.sum(), sa / sa.sum()
+            tot = tot + torch.nn.functional.kl_div(torch.log(sa), ta, reduction="batchmean")
+            cnt += 1
+        return tot / max(cnt, 1)
+
+    def forward(self, u, i, y):
+        with torch.no_grad():
+            tl = self.teacher(u, i)
+            tf = self.features(self.teacher, u, i)
+        sl = self.student(u, i)
+        task = torch.nn.functional.binary_cross_entropy_with_logits(sl, y)
+        a, b, g = self.alpha, self.beta, self.gamma
+        if self.strategy == "response":
+            return a * task + (1 - a) * torch.nn.functional.mse_loss(sl, tl)
+        T = self.temperature
+        resp = torch.nn.functional.mse_loss(torch.sigmoid(sl / T), torch.sigmoid(tl / T)) * (T ** 2)
+        sf = self.features(self.student, u, i)
+        if self.strategy == "feature":
+            return a * task + max(0, 1 - a - b) * resp + b * self.feature_loss(tf, sf)
+        if self.strategy == "attention":
+            return a * task + (1 - a - g) * resp + g * self.attention_loss(tf, sf)
+        return (a * task + max(0, 1 - a - b - g) * resp + b * self.feature_loss(tf, sf)
+                + g * self.attention_loss(tf, sf))

@@ -149,3 +149,51 @@ def test_metrics_small_batch_raises(golden):
     assert bool(g["bs7_k10_raises"])
     with pytest.raises(RuntimeError):
         O.metrics_np(g["logits"], g["test_pairs"][:, 1], 7, 10)
+
+
+# ---------------------------------------------------------------------------
+# G8: distillation (config C5) -- the oracle's restatement of src/distillation/*
+# against the reference's own outputs (tests/golden/make_golden_kd.py)
+KD_CASES = {"c5": ((16, 3, "NeuMF-end"), (8, 2, "MLP")),
+            "cli": ((32, 2, "NeuMF-end"), (16, 1, "NeuMF-end")),
+            "same": ((8, 2, "GMF"), (8, 2, "GMF"))}
+
+
+@pytest.mark.parametrize("case", list(KD_CASES))
+@pytest.mark.parametrize("strategy", ["response", "feature", "attention"])
+def test_oracle_distillation_vs_reference(golden, case, strategy):
+    g = golden("G8_distill")
+    tag = f"{case}_{strategy}"
+    (tf, tl, tm), (sf, sl, sm) = KD_CASES[case]
+    torch.manual_seed(7)
+    teacher = O.OracleNCF(50, 80, tf, tl, 0.0, tm)
+    student = O.OracleNCF(50, 80, sf, sl, 0.0, sm)
+    dist = O.OracleDistill(teacher, student, strategy, 2.0, 0.5, 0.3, 0.2)
+    # same construction order -> bit-identical initial weights and adapters
+    for k, v in teacher.state_dict().items():
+        assert np.array_equal(v.numpy(), g[f"{tag}::teacher::{k}"]), k
+    for k, v in student.state_dict().items():
+        assert np.array_equal(v.numpy(), g[f"{tag}::student0::{k}"]), k
+    for k, v in dist.adaptation_layers.state_dict().items():
+        assert np.array_equal(v.numpy(), g[f"{tag}::adapter::{k}"]), k
+    opt = torch.optim.Adam(student.parameters(), lr=1e-3)
+    losses = []
+    for s in range(g["users"].shape[0]):
+        u, i = torch.from_numpy(g["users"][s]), torch.from_numpy(g["items"][s])
+        y = torch.from_numpy(g["labels"][s])
+        opt.zero_grad()
+        loss = dist(u, i, y)
+        loss.backward()
+        if s == 0:
+            np.testing.assert_allclose(loss.item(), float(g[f"{tag}::loss0"]), rtol=1e-6)
+            for k, p in student.named_parameters():
+                key = f"{tag}::grad0::{k}"
+                assert (p.grad is not None) == (key in g.files), k
+                if p.grad is not None:
+                    np.testing.assert_allclose(p.grad.numpy(), g[key], rtol=1e-5,
+                                               atol=1e-7 * float(np.abs(g[key]).max() or 1), err_msg=k)
+        opt.step()
+        losses.append(loss.item())
+    np.testing.assert_allclose(losses, g[f"{tag}::losses"], rtol=1e-6)
+    for k, v in student.state_dict().items():
+        np.testing.assert_allclose(v.numpy(), g[f"{tag}::student_t5::{k}"], rtol=1e-5, atol=1e-7, err_msg=k)
