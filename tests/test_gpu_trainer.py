@@ -74,3 +74,52 @@ def test_script_stdout_matches_reference(golden, ml100k_dir):
         assert abs(h1 - h2) <= 0.01 and abs(n1 - n2) <= 0.01, (got, ref)
     assert "Parameters: 107841" in out.stdout and "--- RESULTS ---" in out.stdout
     assert os.path.exists(os.path.join(str(ml100k_dir), "results", "models", "NeuMF_end_3l_8f_best.pth"))
+
+
+def _parse_student(lines):
+    out = []
+    for ln in lines:
+        m = re.match(r"(\d+) - Loss: ([\d.]+), HR: ([\d.]+), NDCG: ([\d.]+)", str(ln))
+        if m:
+            out.append((int(m.group(1)), float(m.group(2)), float(m.group(3)), float(m.group(4))))
+    return out
+
+
+@pytest.mark.parametrize("strategy", ["response", "feature"])
+def test_student_script_matches_reference_loop(golden, ml100k_dir, strategy):
+    """scripts/train_student.py (config C5 shapes: teacher NCF(16,3) -> student
+    NCF(8,2,MLP)) against the reference's train_student loop run with the
+    reference's own objects (tests/golden/G9_student_loop.npz): same seeds, same
+    negatives/batches/init, loss within 1e-3 relative, HR/NDCG within 0.01."""
+    from ncf_amd.data import load_all
+    from ncf_amd.models import NCF
+    g = golden("G9_student_loop")
+    ref = _parse_student(g[f"{strategy}_stdout"])
+    _, _, U, I, _ = load_all()
+    torch.manual_seed(123)  # the teacher checkpoint the golden run loaded
+    sd = NCF(U, I, 16, 3, 0.0, "NeuMF-end").state_dict()
+    os.makedirs("results/models", exist_ok=True)
+    torch.save(sd, "results/models/teacher_NeuMF-end_best.pth")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "train_student.py"), "--epochs", "1",
+                          "--factor_num", "8", "--num_layers", "2", "--student_model", "MLP",
+                          "--teacher_model", "NeuMF-end", "--distillation", strategy, "--seed", "0"],
+                         capture_output=True, text=True, timeout=600, cwd=str(ml100k_dir))
+    assert out.returncode == 0, out.stderr[-2000:]
+    got = _parse_student(out.stdout.splitlines())
+    assert len(got) == 1, out.stdout[-2000:]
+    (e1, l1, h1, n1), (e2, l2, h2, n2) = got[0], ref[0]
+    assert e1 == e2
+    assert abs(l1 - l2) <= 1e-3 * l2, (got, ref)
+    assert abs(h1 - h2) <= 0.01 and abs(n1 - n2) <= 0.01, (got, ref)
+    assert "End. Best epoch 000" in out.stdout
+    assert os.path.exists(os.path.join(str(ml100k_dir), "results", "models", "student_MLP_best.pth"))
+
+
+def test_teacher_script_runs(ml100k_dir):
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "train_teacher.py"), "--epochs", "1",
+                          "--factor_num", "16", "--num_layers", "3", "--seed", "0"],
+                         capture_output=True, text=True, timeout=600, cwd=str(ml100k_dir))
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert re.search(r"Epoch 001: Loss=[\d.]+, HR=[\d.]+, NDCG=[\d.]+, Time=\d\d:\d\d:\d\d", out.stdout), out.stdout
+    assert re.search(r"Best Epoch 000: Loss=", out.stdout), out.stdout
+    assert os.path.exists(os.path.join(str(ml100k_dir), "results", "models", "teacher_NeuMF-end_best.pth"))
