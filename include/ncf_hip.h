@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 6
+#define NCF_ABI_VERSION 7
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -173,6 +173,22 @@ int ncf_forward(const ncf_layout *lay, const float *params, const uint64_t *rows
  * label tensors the reference DataLoader yields, datasets.py:72-78). */
 int ncf_pack_rows(const int32_t *users, const int32_t *items, const float *labels, int64_t n,
                   uint64_t *rows_out, void *stream);
+
+/*
+ * Second half of the backward on the factored path (MLP shapes with a fused kernel
+ * and user_num + item_num <= 32768; a no-op returning NCF_OK for every other
+ * layout).  There ncf_train_step scatter-adds, per row, the layer-0 pre-activation
+ * gradient D0 (width dm) into the user and item rows of grads[um] / grads[im] instead
+ * of forming the layer-0 weight and data gradients per row; this call turns those
+ * row sums into the true gradients (all from the same params the step used):
+ *   dUm = G W0[:, :dm],  dIm = H W0[:, dm:]   (in place),
+ *   dW0 = [G^T Um | H^T Im]                   (stored into grads[w0]).
+ * workspace: the train workspace of the step (its tail holds per-block dW0 partials,
+ * summed in a fixed order: bitwise reproducible).
+ * Call sequence per step: ncf_train_step[_kd] -> ncf_expand_grads ->
+ * [ncf_kd_feature_step] -> ncf_reduce_slab or ncf_reduce_adam_step.
+ */
+int ncf_expand_grads(const ncf_layout *lay, const float *params, float *grads, void *workspace, void *stream);
 
 /* p[0 .. n) = 0 with a kernel (no memset node in a captured graph); p 16-byte aligned,
  * n a multiple of 4.  Zeroes the local gradient bucket after the data-parallel

@@ -29,7 +29,7 @@ NCF_E_ARG = -2
 NCF_E_LAUNCH = -3
 MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
 DZ_BCE, DZ_DLOGIT, DZ_KD = 0, 1, 2
-ABI_VERSION = 6  # include/ncf_hip.h NCF_ABI_VERSION
+ABI_VERSION = 7  # include/ncf_hip.h NCF_ABI_VERSION
 PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
 
@@ -73,6 +73,7 @@ _HIP_PROTOS = {
     "ncf_forward_workspace_bytes": (c_i64, [ctypes.POINTER(NcfLayout), c_i64]),
     "ncf_pack_rows": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "ncf_zero_f32": (ctypes.c_int, [c_vp, c_i64, c_vp]),
+    "ncf_expand_grads": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp]),
     "ncf_reduce_slab": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp]),
     "ncf_slab_stride": (c_i64, [ctypes.POINTER(NcfLayout)]),
     "ncf_debug_set_diag": (ctypes.c_int, [ctypes.c_int]),

@@ -108,6 +108,7 @@ struct KernelEntry {
     int mode, F, L;
     const void* train;
     const void* fwd;
+    const void* train_fact;  // factored layer 0 (MLP shapes; see ncf_train.hip), else nullptr
     int w_total, misc, stage8;  // LDS floats
 };
 

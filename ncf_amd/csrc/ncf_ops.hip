@@ -719,12 +719,227 @@ __global__ __launch_bounds__(256) void kd_feature_kernel(KdFeatArgs a) {
     if (l == 0 && lossw != 0.f) atomicAdd(a.loss_out, lossw);
 }
 
+// ---------------------------------------------------------------------------
+// Factored layer 0 (ncf_train.hip, FACT): the step left G_u = sum of the D0 rows
+// of user u in grads[um] and H_i in grads[im] (width DM = S(1)).  fact_expand_kernel
+// turns them into the true gradients; one block per FX_CH-row chunk of one table X
+// (X = Um with koff = 0, or Im with koff = DM), its G and X rows staged in LDS once:
+//   dX = G W0[:, koff : koff + DM]   per 16-row tile (one wave each), written over G
+//   P_b = G^T X                       the block's partial of dW0[:, koff : koff + DM]
+//                                     (each wave owns NT of the NT x NT output tiles),
+//                                     plain stores to partials[b][DM][DM]
+// fact_w0_reduce_kernel then sums the partials of each half in block order
+// (deterministic, no atomics: every block's partial covers the same 16 KB of W0, so
+// float atomics would serialise on those lines).  v_mfma_f32_16x16x4_f32 throughout:
+// (U + I)/16 tile GEMMs per step in place of the per-row layer-0 dgrad / wgrad of B/16.
+constexpr int FX_WAVES = 4;
+constexpr int FX_CH = 64;  // rows per block = FX_WAVES row tiles of 16
+
+template <int DM>
+__global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout lay, const float* __restrict__ prm,
+                                                                     float* __restrict__ grads,
+                                                                     float* __restrict__ partials, int nbu) {
+    constexpr int S0 = 2 * DM, SWS = S0 + 4, ST = DM + 4, NT = (DM + 15) / 16, Q4 = DM / 4;
+    extern __shared__ __attribute__((aligned(16))) float fsm[];
+    float* sW = fsm;                  // W0 [DM][2DM], row stride SWS
+    float* sG = sW + DM * SWS;        // G rows [FX_CH][ST]
+    float* sX = sG + FX_CH * ST;      // X rows [FX_CH][ST]
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, c = l & 15, g = l >> 4;
+    const bool user = (int)blockIdx.x < nbu;
+    const int64_t nrows = user ? lay.user_num : lay.item_num;
+    const int64_t xoff = user ? lay.um : lay.im;
+    const int koff = user ? 0 : DM;
+    const int64_t r0 = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * FX_CH;
+    {   // W0, then the chunk's G and X rows -> LDS: each thread's loads issued together
+        constexpr int NW4 = DM * S0 / 4, PW = (NW4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
+        constexpr int NR4 = FX_CH * Q4, PR = (NR4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
+        f4 wv[PW], gv[PR], xv[PR];
+#pragma unroll
+        for (int q = 0; q < PW; ++q) {
+            const int e4 = tid + q * FX_WAVES * 64;
+            wv[q] = e4 < NW4 ? *reinterpret_cast<const f4*>(prm + lay.w[0] + 4 * e4) : f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int q = 0; q < PR; ++q) {
+            const int e4 = tid + q * FX_WAVES * 64;
+            const int row = e4 / Q4, qq = e4 - row * Q4;
+            const bool ok = e4 < NR4 && r0 + row < nrows;
+            gv[q] = ok ? *reinterpret_cast<const f4*>(grads + xoff + (r0 + row) * DM + 4 * qq) : f4{0.f, 0.f, 0.f, 0.f};
+            xv[q] = ok ? *reinterpret_cast<const f4*>(prm + xoff + (r0 + row) * DM + 4 * qq) : f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int q = 0; q < PW; ++q) {
+            const int e4 = tid + q * FX_WAVES * 64;
+            if (e4 < NW4) {
+                const int j = (4 * e4) / S0, k = 4 * e4 - j * S0;
+                *reinterpret_cast<f4*>(sW + j * SWS + k) = wv[q];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < PR; ++q) {
+            const int e4 = tid + q * FX_WAVES * 64;
+            const int row = e4 / Q4, qq = e4 - row * Q4;
+            if (e4 < NR4) {
+                *reinterpret_cast<f4*>(sG + row * ST + 4 * qq) = gv[q];
+                *reinterpret_cast<f4*>(sX + row * ST + 4 * qq) = xv[q];
+            }
+        }
+    }
+    __syncthreads();
+    // dW0 partial: wave w owns output tiles (mt, nt) with (mt * NT + nt) % FX_WAVES == w.
+    // A[i = j][k = row] = G[row][j],  B[k = row][n = k'] = X[row][k'].
+    for (int tt = w; tt < NT * NT; tt += FX_WAVES) {
+        const int mt = tt / NT, nt = tt - mt * NT;
+        const bool jok = 16 * mt + c < DM, kok = 16 * nt + c < DM;
+        f4 a0 = f4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+#pragma unroll 4
+        for (int s4 = 0; s4 < FX_CH / 4; s4 += 2) {
+            const int ra = 4 * s4 + g, rb = ra + 4;
+            a0 = MFMA4(jok ? sG[ra * ST + 16 * mt + c] : 0.f, kok ? sX[ra * ST + 16 * nt + c] : 0.f, a0);
+            a1 = MFMA4(jok ? sG[rb * ST + 16 * mt + c] : 0.f, kok ? sX[rb * ST + 16 * nt + c] : 0.f, a1);
+        }
+        a0.x += a1.x; a0.y += a1.y; a0.z += a1.z; a0.w += a1.w;
+        float* pb = partials + (int64_t)blockIdx.x * DM * DM;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = 16 * mt + 4 * g + q;
+            if (j < DM && kok) pb[j * DM + 16 * nt + c] = lane_get(a0, q);
+        }
+    }
+    // dX = G W0h for row tile w: A[i = row][k = j] = G[row][j],  B[k = j][n = k'] = W0[j][koff + k']
+    const float* gt = sG + 16 * w * ST;
+    f4 d[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) d[nt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < DM / 4; ++kk) {
+        const float av = gt[c * ST + 4 * kk + g];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const float bv = (16 * nt + c < DM) ? sW[(4 * kk + g) * SWS + koff + 16 * nt + c] : 0.f;
+            d[nt] = MFMA4(av, bv, d[nt]);
+        }
+    }
+    __syncthreads();  // every wave is done reading sX (dW0) before tile w's dX goes there
+    float* dt = sX + 16 * w * ST;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (16 * nt + c < DM) dt[(4 * g + q) * ST + 16 * nt + c] = lane_get(d[nt], q);
+    wave_sync_lds();
+    for (int e = l; e < 16 * Q4; e += 64) {
+        const int row = e / Q4, q = e - row * Q4;
+        const int64_t rr = r0 + 16 * w + row;
+        if (rr < nrows)
+            *reinterpret_cast<f4*>(grads + xoff + rr * DM + 4 * q) = *reinterpret_cast<const f4*>(dt + row * ST + 4 * q);
+    }
+}
+
+// grads[w0][j][koff + k] = sum over the half's blocks of partials[b][j][k], in a fixed
+// order: one block per 64 partial columns of one half; 16 row groups x 16 float4
+// columns per block, each thread summing every 16th block's partial (16-byte
+// loads, unrolled), then the 16 group sums combined in LDS in group order.
+template <int DM>
+__global__ __launch_bounds__(256) void fact_w0_reduce_kernel(ncf_layout lay, const float* __restrict__ partials,
+                                                              float* __restrict__ grads, int nbu, int nblk) {
+    __shared__ f4 part[16][16];
+    constexpr int CB = (DM * DM + 63) / 64;  // 64-column chunks per half
+    const bool user = (int)blockIdx.x < CB;
+    const int chunk = user ? blockIdx.x : blockIdx.x - CB;
+    const int b0 = user ? 0 : nbu, b1 = user ? nbu : nblk;
+    const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
+    const int col = chunk * 64 + 4 * c4;  // element of the [DM][DM] partial
+    f4 sum = f4{0.f, 0.f, 0.f, 0.f};
+    if (col < DM * DM) {
+#pragma unroll 8
+        for (int b = b0 + rg; b < b1; b += 16) {
+            const f4 v = *reinterpret_cast<const f4*>(partials + (int64_t)b * DM * DM + col);
+            sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+        }
+    }
+    part[rg][c4] = sum;
+    __syncthreads();
+    if (rg == 0 && col < DM * DM) {
+        f4 t = part[0][c4];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) {
+            const f4 v = part[q][c4];
+            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+        }
+        const int j = col / DM, k = col - j * DM;  // 4 | DM: the f4 stays in one row
+        *reinterpret_cast<f4*>(grads + lay.w[0] + (int64_t)j * 2 * DM + (user ? 0 : DM) + k) = t;
+    }
+}
+
 int launch_zero_f32(float* p, int64_t n, hipStream_t st) {
     if (!p || n < 0 || (n & 3) || (reinterpret_cast<uintptr_t>(p) & 15)) return NCF_E_ARG;
     if (n == 0) return NCF_OK;
     int64_t grid = (n / 4 + 255) / 256;
     if (grid > 2048) grid = 2048;
     hipLaunchKernelGGL(zero_f32_kernel, dim3((int)grid), dim3(256), 0, st, reinterpret_cast<f4*>(p), n / 4);
+    return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
+}
+
+// Factored layer 0 for this layout?  Fused MLP shapes whose two embedding tables
+// have fewer rows than FACT_MAX_ROWS (the expand pass works on U + I rows per step,
+// the per-row layer-0 gradients on B rows: at ml-1m 9.7K vs 65K; at ml-20m the
+// tables have 165K rows and the per-row form stays).
+constexpr int64_t FACT_MAX_ROWS = 32768;
+// Fused kernel for this layout, or nullptr (then the layered path runs).
+static const KernelEntry* fused_entry(const ncf_layout* lay) {
+    const KernelEntry* e = find_entry(lay->model_type, lay->factor_num, lay->num_layers);
+    if (!e) return nullptr;
+    return train_lds_floats(e, lay) * 4 <= LDS_LIMIT_BYTES ? e : nullptr;
+}
+static bool fact_mode(const ncf_layout* lay) {
+    const KernelEntry* e = fused_entry(lay);
+    return e != nullptr && e->train_fact != nullptr && lay->model_type != NCF_MODEL_GMF &&
+           (int64_t)lay->user_num + lay->item_num <= FACT_MAX_ROWS;
+}
+
+// First slab column (relative to tower_begin) the step writes: GMF models have no
+// tower; the factored path leaves W0's columns to ncf_expand_grads.
+static int slab_lo(const ncf_layout* lay) {
+    if (lay->model_type == NCF_MODEL_GMF) return (int)(lay->wp - lay->tower_begin);
+    if (fact_mode(lay)) return (int)(lay->b[0] - lay->tower_begin);
+    return 0;
+}
+
+static int fact_blocks(const ncf_layout* lay, int* nbu) {
+    const int bu = (int)((lay->user_num + FX_CH - 1) / FX_CH), bi = (int)((lay->item_num + FX_CH - 1) / FX_CH);
+    *nbu = bu;
+    return bu + bi;
+}
+
+static int64_t fact_partials_floats(const ncf_layout* lay) {
+    int nbu;
+    const int64_t DM = (int64_t)lay->factor_num << (lay->num_layers - 1);
+    return (int64_t)fact_blocks(lay, &nbu) * DM * DM;
+}
+
+static int launch_fact_expand(const ncf_layout* lay, const float* params, float* grads, float* partials,
+                              hipStream_t st) {
+    const int DM = lay->factor_num << (lay->num_layers - 1);
+    const void *fe, *fr;
+    switch (DM) {
+#define NCF_FX(D) case D: fe = reinterpret_cast<const void*>(&fact_expand_kernel<D>); \
+                          fr = reinterpret_cast<const void*>(&fact_w0_reduce_kernel<D>); break;
+        NCF_FX(8) NCF_FX(16) NCF_FX(32) NCF_FX(64)
+#undef NCF_FX
+        default: return NCF_E_UNSUPPORTED;
+    }
+    ncf_layout l = *lay;
+    int nbu;
+    int nblk = fact_blocks(lay, &nbu);
+    const int64_t lds = ((int64_t)DM * (2 * DM + 4) + 2LL * FX_CH * (DM + 4)) * 4;
+    if (ensure_lds(fe, lds) != NCF_OK) return NCF_E_LAUNCH;
+    void* ae[] = {&l, (void*)&params, (void*)&grads, (void*)&partials, &nbu};
+    if (hipLaunchKernel(fe, dim3((unsigned)nblk), dim3(FX_WAVES * 64), ae, (size_t)lds, st) != hipSuccess)
+        return NCF_E_LAUNCH;
+    void* ar[] = {&l, (void*)&partials, (void*)&grads, &nbu, &nblk};
+    const unsigned br = (unsigned)(2 * ((DM * DM + 63) / 64));
+    if (hipLaunchKernel(fr, dim3(br), dim3(256), ar, 0, st) != hipSuccess) return NCF_E_LAUNCH;
     return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
 }
 
@@ -778,13 +993,6 @@ int ncf_layout_init(int U, int I, int F, int L, int mode, ncf_layout* o) {
     return NCF_OK;
 }
 
-// Fused kernel for this layout, or nullptr (then the layered path runs).
-static const KernelEntry* fused_entry(const ncf_layout* lay) {
-    const KernelEntry* e = find_entry(lay->model_type, lay->factor_num, lay->num_layers);
-    if (!e) return nullptr;
-    return train_lds_floats(e, lay) * 4 <= LDS_LIMIT_BYTES ? e : nullptr;
-}
-
 int ncf_supported(int mode, int F, int L) {
     ncf_layout lay;
     if (ncf_layout_init(1, 1, F, L, mode, &lay) != NCF_OK) return 0;
@@ -794,7 +1002,8 @@ int ncf_supported(int mode, int F, int L) {
 
 int64_t ncf_workspace_bytes(const ncf_layout* lay, int64_t rows) {
     if (!lay || rows < 0) return -1;
-    if (fused_entry(lay)) return (int64_t)SLAB_ROWS * ncf_slab_stride(lay) * 4;
+    if (fused_entry(lay))
+        return ((int64_t)SLAB_ROWS * ncf_slab_stride(lay) + (fact_mode(lay) ? fact_partials_floats(lay) : 0)) * 4;
     return lyr_workspace_floats(lay, rows, true) * 4;
 }
 
@@ -838,7 +1047,8 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
     }
     const int64_t lds = train_lds_floats(e, lay) * 4;
     if (lds > LDS_LIMIT_BYTES) return NCF_E_UNSUPPORTED;
-    if (ensure_lds(e->train, lds) != NCF_OK) return NCF_E_LAUNCH;
+    const void* fn = fact_mode(lay) ? e->train_fact : e->train;
+    if (ensure_lds(fn, lds) != NCF_OK) return NCF_E_LAUNCH;
     TrainArgs a;
     memset(&a, 0, sizeof(a));
     a.lay = *lay;
@@ -860,7 +1070,7 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
     a.slab = slab;
     a.logits_out = logits_out;
     void* args[] = {&a};
-    if (hipLaunchKernel(e->train, dim3(SLAB_ROWS), dim3(NTHREADS), args, (size_t)lds, (hipStream_t)stream) !=
+    if (hipLaunchKernel(fn, dim3(SLAB_ROWS), dim3(NTHREADS), args, (size_t)lds, (hipStream_t)stream) !=
         hipSuccess)
         return NCF_E_LAUNCH;
     return launch_status();
@@ -964,7 +1174,7 @@ int ncf_reduce_slab(const ncf_layout* lay, const void* workspace, float* grads, 
     if (!lay || !workspace || !grads) return NCF_E_ARG;
     const float* slab = static_cast<const float*>(workspace);
     const int stride = (int)ncf_slab_stride(lay);
-    const int lo = lay->model_type == NCF_MODEL_GMF ? (int)(lay->wp - lay->tower_begin) : 0;
+    const int lo = slab_lo(lay);
     const int blocks = (stride - lo + 63) / 64;
     const int rows = fused_entry(lay) ? SLAB_ROWS : 1;  // the layered path accumulates into one row
     hipLaunchKernelGGL(reduce_slab_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab,
@@ -995,12 +1205,15 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
     int err = 0;
     Ranges R = make_ranges(ranges, nranges, &err);
     if (err) return NCF_E_ARG;
-    // embedding part of the active ranges: [begin, min(end, tower_begin))
+    // plain-Adam part of the active ranges: [begin, min(end, tower_begin + lo)): the
+    // embedding tables, and W0 on the factored path (its gradient is in grads, formed
+    // by ncf_expand_grads, not in the slab)
+    const int64_t plain_end = lay->tower_begin + slab_lo(lay) * (fact_mode(lay) ? 1 : 0);
     int64_t er[16];
     int ne = 0;
     for (int i = 0; i < nranges; ++i) {
         const int64_t b = ranges[2 * i];
-        const int64_t e = ranges[2 * i + 1] < lay->tower_begin ? ranges[2 * i + 1] : lay->tower_begin;
+        const int64_t e = ranges[2 * i + 1] < plain_end ? ranges[2 * i + 1] : plain_end;
         if (e > b) {
             er[2 * ne] = b;
             er[2 * ne + 1] = e;
@@ -1014,7 +1227,7 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
         if (err) return NCF_E_ARG;
     }
     const int stride = (int)ncf_slab_stride(lay);
-    const int lo = lay->model_type == NCF_MODEL_GMF ? (int)(lay->wp - lay->tower_begin) : 0;
+    const int lo = slab_lo(lay);
     const int nA = (stride - lo + 63) / 64;
     const int rows = fused_entry(lay) ? SLAB_ROWS : 1;
     const int64_t etotal = RE.prefix[RE.n];
@@ -1043,6 +1256,14 @@ int ncf_sgd_step(float* params, float* grads, const int64_t* ranges, int nranges
 }
 
 int ncf_zero_f32(float* p, int64_t n, void* stream) { return launch_zero_f32(p, n, (hipStream_t)stream); }
+
+int ncf_expand_grads(const ncf_layout* lay, const float* params, float* grads, void* workspace, void* stream) {
+    if (!lay || !params || !grads) return NCF_E_ARG;
+    if (!fact_mode(lay)) return NCF_OK;
+    if (!workspace) return NCF_E_ARG;
+    float* partials = static_cast<float*>(workspace) + (int64_t)SLAB_ROWS * ncf_slab_stride(lay);
+    return launch_fact_expand(lay, params, grads, partials, (hipStream_t)stream);
+}
 
 int ncf_pack_rows(const int32_t* users, const int32_t* items, const float* labels, int64_t n, uint64_t* rows_out,
                   void* stream) {

@@ -80,9 +80,18 @@ __device__ __forceinline__ void set_r(f4& v, int r, float x) {
     else v.w = x;
 }
 
-template <int F, int L, int MODE, bool FWD_ONLY>
+// FACT (factored layer 0, MLP shapes): the step does not form the layer-0 weight
+// and data gradients per row.  With W0 = [W0u | W0i] and X0 = [Um[u] | Im[i]],
+//   dUm[u] = (sum over the batch rows r of user u of D0_r) W0u,   dW0u = sum_u G_u^T Um[u]
+// (G_u = that row sum), likewise for items: the step scatter-adds D0_r (width
+// S(1) = DM) into the user and item rows of the gradient buffer and
+// fact_expand_kernel (ncf_ops.hip) turns those sums into dUm, dIm, dW0 with
+// (U + I) / 16 tile GEMMs instead of B / 16.  Every wave then touches only its own
+// rows of LDS after the weight prologue, so tiles need no workgroup barrier.
+template <int F, int L, int MODE, bool FWD_ONLY, bool FACT>
 __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     using S_ = Shape<F, L, MODE>;
+    static_assert(!FACT || S_::MLP, "factored layer 0 needs the MLP tower");
     static_assert(!S_::MLP || S_::KT(0) <= NWAVES, "layer-0 wgrad: one 16-column block per wave");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* sW = smem;
@@ -162,18 +171,36 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 
     // ---- tower weights, biases, predict weights -> LDS (zero-padded) ---------
     if constexpr (S_::MLP) {
+        // every layer's loads first (one memory round trip for the whole prologue),
+        // then the LDS stores
+        constexpr int PERMAX = (16 * S_::MT(0) * (S_::S(0) / 4) + NTHREADS - 1) / NTHREADS;
+        f4 wreg[L][PERMAX];
+        float breg[L];
         static_for<L>([&](auto kk) {
             constexpr int k = decltype(kk)::value;
             constexpr int rows = 16 * S_::MT(k), cols4 = S_::S(k) / 4, outs = S_::S(k + 1);
+            constexpr int PER = (rows * cols4 + NTHREADS - 1) / NTHREADS;
             const f4* Wg = reinterpret_cast<const f4*>(prm + lay.w[k]);
-            float* Ws = sW + S_::woff(k);
-            for (int e = tid; e < rows * cols4; e += NTHREADS) {
-                const int o = e / cols4, i4 = e - o * cols4;
-                const f4 v = o < outs ? Wg[e] : f4{0.f, 0.f, 0.f, 0.f};
-                *reinterpret_cast<f4*>(Ws + o * S_::SW(k) + 4 * i4) = v;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const int e = tid + q * NTHREADS;
+                const int o = e / cols4;
+                wreg[k][q] = (e < rows * cols4 && o < outs) ? Wg[e] : f4{0.f, 0.f, 0.f, 0.f};
             }
-            for (int e = tid; e < 16 * S_::MT(k); e += NTHREADS)
-                sB[S_::boff(k) + e] = e < outs ? prm[lay.b[k] + e] : 0.f;
+            breg[k] = tid < outs ? prm[lay.b[k] + tid] : 0.f;  // 16 * MT(k) <= 128 < NTHREADS
+        });
+        static_for<L>([&](auto kk) {
+            constexpr int k = decltype(kk)::value;
+            constexpr int rows = 16 * S_::MT(k), cols4 = S_::S(k) / 4;
+            constexpr int PER = (rows * cols4 + NTHREADS - 1) / NTHREADS;
+            float* Ws = sW + S_::woff(k);
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const int e = tid + q * NTHREADS;
+                const int o = e / cols4, i4 = e - o * cols4;
+                if (e < rows * cols4) *reinterpret_cast<f4*>(Ws + o * S_::SW(k) + 4 * i4) = wreg[k][q];
+            }
+            if (tid < 16 * S_::MT(k)) sB[S_::boff(k) + tid] = breg[k];
         });
     }
     for (int e = tid; e < 128; e += NTHREADS) sWP[e] = e < S_::P ? prm[lay.wp + e] : 0.f;
@@ -435,9 +462,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         } else {
             // (d) layer-0 wgrad operand: X0 rows of the whole tile, columns 16*nt + c
             constexpr int DM = S_::DM;
-            float bx[S_::MLP ? NWAVES * 4 : 1];
+            float bx[S_::MLP && !FACT ? NWAVES * 4 : 1];
             const int nt0 = w < KT0 ? w : KT0 - 1;
-            if constexpr (S_::MLP) {
+            if constexpr (S_::MLP && !FACT) {
                 const int fj = 16 * nt0 + c;
                 const bool isu = fj < DM;
                 const int64_t tab = isu ? lay.um + fj : lay.im + (fj - DM);
@@ -580,6 +607,54 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                             D[k - 1][m2] = d;
                         }
                         stamp(a, sb + 5 + 3 * (L - 1 - k));
+                    } else if constexpr (FACT) {
+                        // layer 0, factored: stage this wave's D0 rows row-major in its
+                        // scratch, publish its next-tile ids (own rows only: no barrier),
+                        // db0, next tile's embedding fragments, then scatter-add the D0
+                        // rows into the user and the item rows of the gradient buffer.
+                        float* scr = sstage + w * S_::WAVE_STAGE;
+#pragma unroll
+                        for (int mt = 0; mt < S_::MT(0); ++mt)
+                            if (16 * mt + 4 * g < S_::S(1))
+                                *reinterpret_cast<f4*>(scr + c * S_::SCM + 16 * mt + 4 * g) = D[0][mt];
+                        if (pub) {
+                            su2[(buf ^ 1) * TILE_ROWS + prow] = nu;
+                            si2[(buf ^ 1) * TILE_ROWS + prow] = ni;
+                            slab2[(buf ^ 1) * TILE_ROWS + prow] = nlab;
+                        }
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // same-wave LDS hand-off
+                        stamp(a, sb + 3 + 3 * (L - 1));
+                        if (l < S_::S(1)) {
+                            float s = 0.f;
+#pragma unroll
+                            for (int rr = 0; rr < 16; ++rr) s += scr[rr * S_::SCM + l];
+                            dbAcc[0] += s;
+                        }
+                        load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
+                        stamp(a, sb + 4 + 3 * (L - 1));
+                        item_segments(scr, a, su, si, wr, l, gIg, gf, gq0);
+                        constexpr int RPW = DM >= 64 ? 1 : 64 / DM;  // rows per wave-instruction
+                        constexpr int FPI = DM >= 64 ? 64 : DM;
+                        constexpr int NQ = 16 / RPW, NF = (DM + FPI - 1) / FPI;
+                        float uv[NQ][NF];
+                        int uid[NQ];
+#pragma unroll
+                        for (int qi = 0; qi < NQ; ++qi) {
+                            const int q = qi * RPW + l / FPI;
+                            uid[qi] = max(su[wr + q], 0);
+#pragma unroll
+                            for (int fi = 0; fi < NF; ++fi) uv[qi][fi] = scr[q * S_::SCM + fi * FPI + l % FPI];
+                        }
+#pragma unroll
+                        for (int qi = 0; qi < NQ; ++qi) {
+#pragma unroll
+                            for (int fi = 0; fi < NF; ++fi) {
+                                const int f = fi * FPI + l % FPI;
+                                if (!DIAG_ON(a, DIAG_NO_USER_SCATTER))
+                                    atomicAdd(a.grads + lay.um + (int64_t)uid[qi] * DM + f, uv[qi][fi]);
+                            }
+                        }
+                        stamp(a, sb + 5 + 3 * (L - 1));
                     } else {
                         // layer 0: its wgrad needs every row of the tile -> stage this
                         // wave's D_0 rows (half titer & 1 when ALT0) and publish the next
@@ -740,7 +815,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
             // the next tile's first cross-wave staging goes to the other region and
             // its first barrier resynchronises, so a wave still scattering overlaps
             // the others' next forward.
-            if constexpr (S_::END_BARRIER) lds_barrier();
+            if constexpr (S_::END_BARRIER && !FACT) lds_barrier();
             stamp(a, sb + 13);
             ++titer;
         }
@@ -755,7 +830,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         float* out = a.slab + (int64_t)blockIdx.x * len;
         const int l = l0, c = c0, g = g0;
         // layer-0 wgrad: this wave's 16-column block, already summed over the rows
-        if constexpr (S_::MLP) {
+        // (FACT: formed after the step by fact_expand_kernel; its slab columns unused)
+        if constexpr (S_::MLP && !FACT) {
             if (w < KT0) {
 #pragma unroll
                 for (int mt = 0; mt < MT0; ++mt) {
@@ -895,7 +971,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         if constexpr (S_::MLP) {
             static_for<L>([&](auto kk) {
                 constexpr int k = decltype(kk)::value;
-                zero_gap(lay.w[k], S_::S(k + 1) * S_::S(k));
+                if (!FACT || k > 0) zero_gap(lay.w[k], S_::S(k + 1) * S_::S(k));
                 zero_gap(lay.b[k], S_::S(k + 1));
             });
         }
@@ -918,8 +994,12 @@ static KernelEntry make_entry() {
     e.mode = MODE;
     e.F = F;
     e.L = L;
-    e.train = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false>);
-    e.fwd = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, true>);
+    e.train = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, false>);
+    e.fwd = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, true, false>);
+    if constexpr (S_::MLP)
+        e.train_fact = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, true>);
+    else
+        e.train_fact = nullptr;
     e.w_total = S_::W_TOTAL;
     e.misc = S_::MISC;
     e.stage8 = NWAVES * S_::WAVE_STAGE;

@@ -364,6 +364,7 @@ class DeviceDistillPlan:
                                       eng.batch_size, eng.world_size, eng.rank, self.w_task, self.w_resp,
                                       self.temperature, eng.ws.data_ptr(), eng.ws.numel() * 4, None, st),
                 "ncf_train_step_kd")
+        eng._expand(st)  # before the feature terms add plain embedding gradients
         if self.keys:
             g = self.keys.get("gmf_features", (None, None, 0.0))
             m = self.keys.get("mlp_input", (None, None, 0.0))

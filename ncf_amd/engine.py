@@ -7,7 +7,8 @@ with the all-reduce issued between them, see ``_capture_collective``):
 
   1. ``ncf_train_step``  fused gather / GMF / MFMA tower fwd / BCE / MFMA tower
                          bwd / embedding scatter-add   (models.py:97-118,
-                         train_neumf.py:111-114)
+                         train_neumf.py:111-114), then ``ncf_expand_grads``
+                         (factored layer 0: per-user/item sums -> dUm, dIm, dW0)
   2. ``ncf_reduce_slab`` per-workgroup tower grads -> flat grad buffer
   3. world > 1, dp_mode "zero1" (default): RCCL reduce-scatter of the flat grad
      buffer; dp_mode "allreduce": RCCL all-reduce of it
@@ -215,6 +216,13 @@ class TrainEngine:
                                        self.rows.data_ptr(), None, self.ctl.data_ptr(), self.batch_size,
                                        self.world_size, self.rank, L.DZ_BCE, self.ws.data_ptr(),
                                        self.ws.numel() * 4, None, st), "ncf_train_step")
+        self._expand(st)
+
+    def _expand(self, st):
+        """Factored layer 0: per-user/item D0 sums -> dUm, dIm, dW0 (no-op otherwise)."""
+        L.check(L.hip().ncf_expand_grads(ctypes.byref(self.lay), self.flat.data_ptr(), self.grads.data_ptr(),
+                                         self.ws.data_ptr(), st),
+                "ncf_expand_grads")
 
     def _reduce_adam(self):
         st = L.stream_ptr(self.device)

@@ -163,6 +163,8 @@ def fused_backward(flat, lay, rows, dlogit, gflat, ws, ctl):
     L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
                                    dlogit.data_ptr(), ctl.data_ptr(), int(n), 1, 0, L.DZ_DLOGIT,
                                    ws.data_ptr(), ws.numel() * 4, None, st), "ncf_train_step")
+    L.check(L.hip().ncf_expand_grads(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), ws.data_ptr(), st),
+            "ncf_expand_grads")
     L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), ws.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st),
             "ncf_reduce_slab")
 

@@ -147,6 +147,8 @@ def test_one_step_grads_vs_oracle(cfg):
     L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
                                    None, ctl.data_ptr(), B, 1, 0, L.DZ_BCE,
                                    ws.data_ptr(), ws.numel() * 4, logits.data_ptr(), st), "train")
+    L.check(L.hip().ncf_expand_grads(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), ws.data_ptr(), st),
+            "expand")
     L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), ws.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st), "reduce")
     torch.cuda.synchronize()
     np.testing.assert_allclose(logits.cpu().numpy(), logits_ref.numpy(), rtol=1e-5, atol=1e-7)
@@ -182,6 +184,8 @@ def test_rank_shards_sum_to_full_batch(world, f, Lyr):
         L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
                                        None, ctl.data_ptr(), B, world, rank, L.DZ_BCE,
                                        ws.data_ptr(), ws.numel() * 4, None, st), "train")
+        L.check(L.hip().ncf_expand_grads(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), ws.data_ptr(), st),
+            "expand")
         L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), ws.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st), "reduce")
         return gflat
     full = run(1, 0)
