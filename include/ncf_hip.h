@@ -182,9 +182,10 @@ int ncf_pack_rows(const int32_t *users, const int32_t *items, const float *label
  * of forming the layer-0 weight and data gradients per row; this call turns those
  * row sums into the true gradients (all from the same params the step used):
  *   dUm = G W0[:, :dm],  dIm = H W0[:, dm:]   (in place),
- *   dW0 = [G^T Um | H^T Im]                   (stored into grads[w0]).
- * workspace: the train workspace of the step (its tail holds per-block dW0 partials,
- * summed in a fixed order: bitwise reproducible).
+ *   dW0 = [G^T Um | H^T Im]                   (per-block partials in the tail of the
+ *                                              train workspace; ncf_reduce_slab /
+ *                                              ncf_reduce_adam_step sum them in a fixed
+ *                                              order with the other tower columns).
  * Call sequence per step: ncf_train_step[_kd] -> ncf_expand_grads ->
  * [ncf_kd_feature_step] -> ncf_reduce_slab or ncf_reduce_adam_step.
  */

@@ -15,13 +15,40 @@ namespace ncf {
 // in LDS in a fixed order.  Thread 0 of block 0 also advances the step control
 // block (batch, adam_t): the fused step before it has read `batch`, the
 // optimizer after it reads the advanced `adam_t` (kernel boundaries order it).
+// W0's columns on the factored path: the gradient is the sum of the per-block
+// partials of ncf_expand_grads (fact_expand_kernel), [nblk][dm][dm], user blocks
+// [0, nbu) for W0[:, :dm], item blocks [nbu, nblk) for W0[:, dm:].  cols = 0: none.
+struct W0Part {
+    const float* p;
+    int nbu, nblk, dm, cols;
+};
+
+// This thread's share (row group rg of 16) of the W0 gradient at tower column j.
+__device__ __forceinline__ f4 w0_part_sum(const W0Part& P, int j, int rg) {
+    f4 s = f4{0.f, 0.f, 0.f, 0.f};
+    const int row = j / (2 * P.dm), col = j - row * 2 * P.dm;
+    if (row >= P.dm) return s;  // alignment padding of the W0 segment
+    const bool item = col >= P.dm;
+    const int64_t off = (int64_t)row * P.dm + (item ? col - P.dm : col);
+    const int b1 = item ? P.nblk : P.nbu;
+    const int64_t bstride = (int64_t)P.dm * P.dm;
+#pragma unroll 4
+    for (int b = (item ? P.nbu : 0) + rg; b < b1; b += 16) {
+        const f4 v = *reinterpret_cast<const f4*>(P.p + (int64_t)b * bstride + off);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    return s;
+}
+
 __global__ __launch_bounds__(256) void reduce_slab_kernel(const float* __restrict__ slab, float* __restrict__ out,
-                                                          int lo, int stride, int rows, ncf_step_ctl* ctl) {
+                                                          int lo, int stride, int rows, ncf_step_ctl* ctl, W0Part wp) {
     __shared__ f4 part[16][16];
     const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
     const int j = lo + (blockIdx.x * 16 + c4) * 4;
     f4 s = f4{0.f, 0.f, 0.f, 0.f};
-    if (j < stride) {
+    if (j < wp.cols) {
+        s = w0_part_sum(wp, j, rg);
+    } else if (j < stride) {
         const float* p = slab + (int64_t)rg * stride + j;
         const int per = rows / 16;
 #pragma unroll 16
@@ -178,7 +205,7 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
                                                           float* __restrict__ g, float* __restrict__ m,
                                                           float* __restrict__ v, Ranges R, Ranges RE,
                                                           ncf_step_ctl* ctl, double lr, double beta1, double beta2,
-                                                          float eps, float* loss_hist, int64_t hist_len) {
+                                                          float eps, float* loss_hist, int64_t hist_len, W0Part wp) {
 #pragma clang fp contract(off)
     __shared__ float sc[2];
     __shared__ f4 part[16][16];
@@ -200,7 +227,9 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
         const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
         const int j = lo + (blockIdx.x * 16 + c4) * 4;
         f4 s = f4{0.f, 0.f, 0.f, 0.f};
-        if (j < stride) {
+        if (j < wp.cols) {
+            s = w0_part_sum(wp, j, rg);
+        } else if (j < stride) {
             const float* q = slab + (int64_t)rg * stride + j;
             const int per = rows / 16;
 #pragma unroll 16
@@ -728,9 +757,9 @@ __global__ __launch_bounds__(256) void kd_feature_kernel(KdFeatArgs a) {
 //   P_b = G^T X                       the block's partial of dW0[:, koff : koff + DM]
 //                                     (each wave owns NT of the NT x NT output tiles),
 //                                     plain stores to partials[b][DM][DM]
-// fact_w0_reduce_kernel then sums the partials of each half in block order
-// (deterministic, no atomics: every block's partial covers the same 16 KB of W0, so
-// float atomics would serialise on those lines).  v_mfma_f32_16x16x4_f32 throughout:
+// The tower reductions (reduce_slab_kernel / reduce_adam_kernel, W0Part) sum the
+// partials of each half in block order (deterministic, no atomics: every block's
+// partial covers the same 16 KB of W0, so float atomics would serialise on it).  v_mfma_f32_16x16x4_f32 throughout:
 // (U + I)/16 tile GEMMs per step in place of the per-row layer-0 dgrad / wgrad of B/16.
 constexpr int FX_WAVES = 4;
 constexpr int FX_CH = 64;  // rows per block = FX_WAVES row tiles of 16
@@ -836,41 +865,6 @@ __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout l
     }
 }
 
-// grads[w0][j][koff + k] = sum over the half's blocks of partials[b][j][k], in a fixed
-// order: one block per 64 partial columns of one half; 16 row groups x 16 float4
-// columns per block, each thread summing every 16th block's partial (16-byte
-// loads, unrolled), then the 16 group sums combined in LDS in group order.
-template <int DM>
-__global__ __launch_bounds__(256) void fact_w0_reduce_kernel(ncf_layout lay, const float* __restrict__ partials,
-                                                              float* __restrict__ grads, int nbu, int nblk) {
-    __shared__ f4 part[16][16];
-    constexpr int CB = (DM * DM + 63) / 64;  // 64-column chunks per half
-    const bool user = (int)blockIdx.x < CB;
-    const int chunk = user ? blockIdx.x : blockIdx.x - CB;
-    const int b0 = user ? 0 : nbu, b1 = user ? nbu : nblk;
-    const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
-    const int col = chunk * 64 + 4 * c4;  // element of the [DM][DM] partial
-    f4 sum = f4{0.f, 0.f, 0.f, 0.f};
-    if (col < DM * DM) {
-#pragma unroll 8
-        for (int b = b0 + rg; b < b1; b += 16) {
-            const f4 v = *reinterpret_cast<const f4*>(partials + (int64_t)b * DM * DM + col);
-            sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
-        }
-    }
-    part[rg][c4] = sum;
-    __syncthreads();
-    if (rg == 0 && col < DM * DM) {
-        f4 t = part[0][c4];
-#pragma unroll
-        for (int q = 1; q < 16; ++q) {
-            const f4 v = part[q][c4];
-            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
-        }
-        const int j = col / DM, k = col - j * DM;  // 4 | DM: the f4 stays in one row
-        *reinterpret_cast<f4*>(grads + lay.w[0] + (int64_t)j * 2 * DM + (user ? 0 : DM) + k) = t;
-    }
-}
 
 int launch_zero_f32(float* p, int64_t n, hipStream_t st) {
     if (!p || n < 0 || (n & 3) || (reinterpret_cast<uintptr_t>(p) & 15)) return NCF_E_ARG;
@@ -898,11 +892,10 @@ static bool fact_mode(const ncf_layout* lay) {
            (int64_t)lay->user_num + lay->item_num <= FACT_MAX_ROWS;
 }
 
-// First slab column (relative to tower_begin) the step writes: GMF models have no
-// tower; the factored path leaves W0's columns to ncf_expand_grads.
+// First tower column (relative to tower_begin) the reductions produce: GMF models
+// have no tower.
 static int slab_lo(const ncf_layout* lay) {
     if (lay->model_type == NCF_MODEL_GMF) return (int)(lay->wp - lay->tower_begin);
-    if (fact_mode(lay)) return (int)(lay->b[0] - lay->tower_begin);
     return 0;
 }
 
@@ -918,13 +911,23 @@ static int64_t fact_partials_floats(const ncf_layout* lay) {
     return (int64_t)fact_blocks(lay, &nbu) * DM * DM;
 }
 
+static W0Part w0_part(const ncf_layout* lay, const void* workspace) {
+    W0Part wp;
+    memset(&wp, 0, sizeof(wp));
+    if (!fact_mode(lay)) return wp;
+    wp.p = static_cast<const float*>(workspace) + (int64_t)SLAB_ROWS * (lay->tower_len + 64);
+    wp.nblk = fact_blocks(lay, &wp.nbu);
+    wp.dm = lay->factor_num << (lay->num_layers - 1);
+    wp.cols = (int)(lay->b[0] - lay->w[0]);
+    return wp;
+}
+
 static int launch_fact_expand(const ncf_layout* lay, const float* params, float* grads, float* partials,
                               hipStream_t st) {
     const int DM = lay->factor_num << (lay->num_layers - 1);
-    const void *fe, *fr;
+    const void* fe;
     switch (DM) {
-#define NCF_FX(D) case D: fe = reinterpret_cast<const void*>(&fact_expand_kernel<D>); \
-                          fr = reinterpret_cast<const void*>(&fact_w0_reduce_kernel<D>); break;
+#define NCF_FX(D) case D: fe = reinterpret_cast<const void*>(&fact_expand_kernel<D>); break;
         NCF_FX(8) NCF_FX(16) NCF_FX(32) NCF_FX(64)
 #undef NCF_FX
         default: return NCF_E_UNSUPPORTED;
@@ -937,9 +940,6 @@ static int launch_fact_expand(const ncf_layout* lay, const float* params, float*
     void* ae[] = {&l, (void*)&params, (void*)&grads, (void*)&partials, &nbu};
     if (hipLaunchKernel(fe, dim3((unsigned)nblk), dim3(FX_WAVES * 64), ae, (size_t)lds, st) != hipSuccess)
         return NCF_E_LAUNCH;
-    void* ar[] = {&l, (void*)&partials, (void*)&grads, &nbu, &nblk};
-    const unsigned br = (unsigned)(2 * ((DM * DM + 63) / 64));
-    if (hipLaunchKernel(fr, dim3(br), dim3(256), ar, 0, st) != hipSuccess) return NCF_E_LAUNCH;
     return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
 }
 
@@ -1178,7 +1178,7 @@ int ncf_reduce_slab(const ncf_layout* lay, const void* workspace, float* grads, 
     const int blocks = (stride - lo + 63) / 64;
     const int rows = fused_entry(lay) ? SLAB_ROWS : 1;  // the layered path accumulates into one row
     hipLaunchKernelGGL(reduce_slab_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab,
-                       grads + lay->tower_begin, lo, stride, rows, ctl);
+                       grads + lay->tower_begin, lo, stride, rows, ctl, w0_part(lay, workspace));
     return launch_status();
 }
 
@@ -1205,10 +1205,9 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
     int err = 0;
     Ranges R = make_ranges(ranges, nranges, &err);
     if (err) return NCF_E_ARG;
-    // plain-Adam part of the active ranges: [begin, min(end, tower_begin + lo)): the
-    // embedding tables, and W0 on the factored path (its gradient is in grads, formed
-    // by ncf_expand_grads, not in the slab)
-    const int64_t plain_end = lay->tower_begin + slab_lo(lay) * (fact_mode(lay) ? 1 : 0);
+    // plain-Adam part of the active ranges: [begin, min(end, tower_begin)), the
+    // embedding tables (their gradient is in grads)
+    const int64_t plain_end = lay->tower_begin;
     int64_t er[16];
     int ne = 0;
     for (int i = 0; i < nranges; ++i) {
@@ -1236,7 +1235,7 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
     hipLaunchKernelGGL(reduce_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
                        static_cast<const float*>(workspace), lo, stride, rows, nA, lay->tower_begin, lay->tower_len,
                        params, grads, exp_avg, exp_avg_sq, R, RE, ctl, lr, beta1, beta2, (float)eps, loss_hist,
-                       hist_len);
+                       hist_len, w0_part(lay, workspace));
     return launch_status();
 }
 
