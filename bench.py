@@ -79,15 +79,16 @@ def pmc_traffic(f, L):
     WRITE_SIZE passes of this bench: bytes = (2 * FETCH_SIZE + WRITE_SIZE) KB * 1024,
     the gfx950 correction of the MI355X guide).  (None, None) if absent."""
     import glob
-    name = f"ncf::ncf_step_kernel<{f}, {L}, 2, false>"
+    dm = f * 2 ** (L - 1)
+    names = (f"ncf::ncf_step_kernel<{f}, {L}, 2, false, true>", f"ncf::fact_expand_kernel<{dm}>")
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_prof_summary.json")), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        for k in d.get("kernels", []):
-            if k.get("kernel") == name and k.get("hbm_bytes_corrected"):
-                return float(k["hbm_bytes_corrected"]), os.path.relpath(path, ROOT)
+        got = {k.get("kernel"): k.get("hbm_bytes_corrected") for k in d.get("kernels", [])}
+        if all(got.get(n) for n in names):
+            return float(sum(got[n] for n in names)), os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -284,7 +285,9 @@ def main():
                        "dp_exchange": eng.dp_mode, "hip_graph": use_graph},
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": 157.3, "unit": "TFLOP/s",
                          "frac": achieved_tf / 157.3, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": (f"ncf_step_kernel<{f},{nl},NeuMF> (fused fwd+bwd)" if path == 1 else
+                         "kernel": (f"ncf_step_kernel<{f},{nl},NeuMF,FACT> + fact_expand_kernel<{f * 2 ** (nl - 1)}> "
+                                    "(fused fwd+bwd, factored layer 0; launch group timed back to back)"
+                                    if path == 1 else
                                     "layered path: all kernels of ncf_train_step (fwd/predict/bwd GEMMs)"),
                          "flops_per_launch": flops, "kernel_ms": ms},
             "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": 8000.0, "unit": "GB/s",

@@ -274,10 +274,11 @@ class TrainEngine:
         return {k: v / max(1, n_steps) for k, v in acc.items()}
 
     def time_train_kernel(self, reps):
-        """Mean duration (ms) of the fused step kernel alone: `reps` back-to-back
-        launches on the current batch between one HIP event pair on the launch
-        stream (per-launch event pairs add several microseconds each).  The
-        gradient buffer is zeroed afterwards (the launches accumulate into it)."""
+        """Mean duration (ms) of the gradient-forming launches of one step -- the
+        fused step kernel and, on the factored path, ncf_expand_grads: `reps`
+        back-to-back launch groups on the current batch between one HIP event pair
+        on the launch stream (per-launch event pairs add several microseconds each).
+        The gradient buffer is zeroed afterwards (the launches accumulate into it)."""
         st = torch.cuda.current_stream(self.device)
         lib = L.hip()
         lay = ctypes.byref(self.lay)
@@ -287,6 +288,7 @@ class TrainEngine:
             L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.rows.data_ptr(),
                                        None, self.ctl.data_ptr(), self.batch_size, self.world_size, self.rank,
                                        L.DZ_BCE, self.ws.data_ptr(), self.ws.numel() * 4, None, sp), "ncf_train_step")
+            self._expand(sp)
         launch()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
