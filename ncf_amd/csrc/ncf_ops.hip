@@ -32,7 +32,7 @@ __device__ __forceinline__ f4 w0_part_sum(const W0Part& P, int j, int rg) {
     const int64_t off = (int64_t)row * P.dm + (item ? col - P.dm : col);
     const int b1 = item ? P.nblk : P.nbu;
     const int64_t bstride = (int64_t)P.dm * P.dm;
-#pragma unroll 4
+#pragma unroll 8
     for (int b = (item ? P.nbu : 0) + rg; b < b1; b += 16) {
         const f4 v = *reinterpret_cast<const f4*>(P.p + (int64_t)b * bstride + off);
         s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
@@ -211,15 +211,15 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
     __shared__ f4 part[16][16];
     const int64_t t_step = ctl->snap_t;
     const int64_t b_step = ctl->snap_batch;
-    if (threadIdx.x == 0) {
-        const double t = (double)t_step;
-        const double bc1 = 1.0 - pow(beta1, t);
-        const double bc2 = 1.0 - pow(beta2, t);
-        sc[0] = (float)(-(lr / bc1));
-        sc[1] = (float)sqrt(bc2);
-    }
-    __syncthreads();
-    const float neg_step = sc[0], bc2s = sc[1];
+    // Bias corrections in double like torch's Python scalars, by thread 0 AFTER its
+    // block's loads are in flight (the double pow costs about a memory round trip).
+    auto scalars = [&]() {
+        if (threadIdx.x == 0) {
+            const double t = (double)t_step;
+            sc[0] = (float)(-(lr / (1.0 - pow(beta1, t))));
+            sc[1] = (float)sqrt(1.0 - pow(beta2, t));
+        }
+    };
     const float w1 = (float)(1.0 - beta1);
     const float b2 = (float)beta2;
     const float omb2 = (float)(1.0 - beta2);
@@ -243,7 +243,9 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
             }
         }
         part[rg][c4] = s;
+        scalars();
         __syncthreads();
+        const float neg_step = sc[0], bc2s = sc[1];
         if (rg == 0 && j < stride) {
             f4 gs = part[0][c4];
 #pragma unroll
@@ -267,18 +269,29 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
     } else {
         const int64_t total = RE.prefix[RE.n];
         const int64_t nthr = (int64_t)(gridDim.x - nA) * blockDim.x;
-        for (int64_t q = (int64_t)(blockIdx.x - nA) * blockDim.x + threadIdx.x; q < total; q += nthr) {
+        int64_t q = (int64_t)(blockIdx.x - nA) * blockDim.x + threadIdx.x;
+        int64_t i = 0;
+        f4 gg, mm, vv, pp;
+        auto load = [&]() {
             int which;
-            const int64_t i = range_locate(RE, q, &which);
-            const f4 gg = *reinterpret_cast<const f4*>(g + i);
-            f4 mm = *reinterpret_cast<const f4*>(m + i);
-            f4 vv = *reinterpret_cast<const f4*>(v + i);
-            f4 pp = *reinterpret_cast<const f4*>(p + i);
+            i = range_locate(RE, q, &which);
+            gg = *reinterpret_cast<const f4*>(g + i);
+            mm = *reinterpret_cast<const f4*>(m + i);
+            vv = *reinterpret_cast<const f4*>(v + i);
+            pp = *reinterpret_cast<const f4*>(p + i);
+        };
+        if (q < total) load();  // the first element's loads fly while thread 0 computes
+        scalars();
+        __syncthreads();
+        const float neg_step = sc[0], bc2s = sc[1];
+        while (q < total) {
             adam_f4(pp, mm, vv, gg, w1, b2, omb2, bc2s, eps, neg_step);
             *reinterpret_cast<f4*>(m + i) = mm;
             *reinterpret_cast<f4*>(v + i) = vv;
             *reinterpret_cast<f4*>(p + i) = pp;
             *reinterpret_cast<f4*>(g + i) = f4{0.f, 0.f, 0.f, 0.f};
+            q += nthr;
+            if (q < total) load();
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // no other block of this launch reads these two
