@@ -152,22 +152,29 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     // barrier -- and past that barrier waves read only their own rows.
     const int prow = 16 * w + (l0 & 15);
     const bool pub = l0 < 16;
-    auto load_idx = [&](int64_t row0, int& u, int& it, float& y) {
+    // The next tile's packed row is fetched early and decoded only where it is
+    // published into LDS: nothing touches the loaded registers before then, so no
+    // wait for it (and, the vmcnt counter being in order, for every scatter atomic
+    // issued before it) lands at the top of a tile.
+    uint64_t npr = 0;
+    float ndl = 0.f;
+    bool nok = false;
+    auto load_idx = [&](int64_t row0) {
         const int64_t r = row0 + prow;
-        const bool ok = r < nloc;
-        const int64_t rc = base + (ok ? r : 0);
-        const uint64_t pr = a.rows[rc];
-        u = (int)(uint32_t)pr;
-        it = (int)((pr >> 32) & 0x7fffffffu);
-        if constexpr (!FWD_ONLY) {  // forward launches carry no labels
-            const float dl = a.dlogit[rc];
-            y = a.dz_mode == NCF_DZ_DLOGIT ? dl : (float)(uint32_t)(pr >> 63);
-        }
-        if (!ok) u = it = -1;
+        nok = r < nloc;
+        const int64_t rc = base + (nok ? r : 0);
+        npr = a.rows[rc];
+        if constexpr (!FWD_ONLY) ndl = a.dlogit[rc];  // forward launches carry no labels
     };
-    int nu = -1, ni = -1;
-    float nlab = 0.f;
-    if ((int64_t)blockIdx.x < ntiles) load_idx((int64_t)blockIdx.x * TILE_ROWS, nu, ni, nlab);
+    auto publish = [&](int off) {
+        if (pub) {
+            su2[off + prow] = nok ? (int)(uint32_t)npr : -1;
+            si2[off + prow] = nok ? (int)((npr >> 32) & 0x7fffffffu) : -1;
+            if constexpr (!FWD_ONLY)
+                slab2[off + prow] = a.dz_mode == NCF_DZ_DLOGIT ? ndl : (float)(uint32_t)(npr >> 63);
+        }
+    };
+    if ((int64_t)blockIdx.x < ntiles) load_idx((int64_t)blockIdx.x * TILE_ROWS);
 
     // ---- tower weights, biases, predict weights -> LDS (zero-padded) ---------
     if constexpr (S_::MLP) {
@@ -232,11 +239,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     constexpr int NI = S_::GMF ? 16 / RPI : 1;
     const float bpv = prm[lay.bp];
     const float wpf = S_::GMF ? prm[lay.wp + l0 % F] : 0.f;
-    if (pub) {
-        su2[prow] = nu;
-        si2[prow] = ni;
-        slab2[prow] = nlab;
-    }
+    publish(0);
     __syncthreads();
 
     // Embedding fragments of the current tile, loaded one tile ahead:
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     //   ugv/igv: GMF rows, row-major lanes (feature l % F, rows j*RPI + l / F)
     f4 X0[KT0];
     float ugv[NI], igv[NI];
-    auto load_emb = [&](const int* su, const int* si, int c, int g, int l) {
+    auto load_mlp = [&](const int* su, const int* si, int c, int g) {
         const int wr = w * 16;
         if constexpr (S_::MLP) {
             constexpr int DM = S_::DM;
@@ -258,6 +261,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                 X0[t] = *reinterpret_cast<const f4*>(prm + off);
             }
         }
+    };
+    auto load_gmf = [&](const int* su, const int* si, int l) {
+        const int wr = w * 16;
         if constexpr (S_::GMF) {
             const int gf = l % F, gq0 = l / F;
 #pragma unroll
@@ -268,6 +274,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
             }
         }
     };
+    auto load_emb = [&](const int* su, const int* si, int c, int g, int l) {
+        load_mlp(su, si, c, g);
+        load_gmf(su, si, l);
+    };
+    // FACT (not FWD_ONLY): the next tile's ids are published and its embedding
+    // fragments requested early in the tile -- MLP rows right after this tile's
+    // forward has consumed X0, GMF rows after the GMF backward -- so they land long
+    // before the next tile needs them instead of in its first phase.
+    constexpr bool EARLY = FACT && !FWD_ONLY;
     // Item-side embedding gradients of a wave's 16 rows: rows of a tile are
     // grouped by item (ncf_prepare_epoch counting-sorts each batch by item), so
     // consecutive equal items are summed in LDS and each item segment issues one
@@ -375,8 +390,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         const int gq0 = l / F;
 
         // (a) next tile's indices
-        load_idx(row0 + (int64_t)gridDim.x * TILE_ROWS, nu, ni, nlab);
-        if (!has_next) nu = ni = -1;
+        load_idx(row0 + (int64_t)gridDim.x * TILE_ROWS);
+        nok = nok && has_next;
 
         // (b) GMF forward
         if constexpr (S_::GMF) {
@@ -427,6 +442,16 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
             });
         }
         stamp(a, sb + 1);
+        // NCF_DZ_KD: this row's teacher logit, requested ahead of the EARLY gathers
+        // so that waiting for it does not wait for them (an in-range dummy read in
+        // the other modes, where dlogit aliases the rows or carries dL/dlogit).
+        float tlog = 0.f;
+        if constexpr (!FWD_ONLY) tlog = a.dlogit[base + min(row0 + myq, nloc - 1)];
+        if constexpr (EARLY) {
+            publish((buf ^ 1) * TILE_ROWS);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // same-wave LDS hand-off
+            load_mlp(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g);
+        }
 
         // predict
         float zt = 0.f;
@@ -451,10 +476,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 
         if constexpr (FWD_ONLY) {
             if (g == 0 && valid) a.logits_out[base + row0 + myq] = z;
-            if (pub) {
-                su2[(buf ^ 1) * TILE_ROWS + prow] = nu;
-                si2[(buf ^ 1) * TILE_ROWS + prow] = ni;
-            }
+            publish((buf ^ 1) * TILE_ROWS);
             lds_barrier();
             load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
             ++titer;
@@ -492,7 +514,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                     // distillation (base.py:40-50; response term: kd_response)
                     const float y = slab_[myq];
                     float rl;
-                    const float rg = kd_response(z, a.dlogit[base + row0 + myq], a.kd_temp, &rl);
+                    const float rg = kd_response(z, tlog, a.kd_temp, &rl);
                     dz = (a.kd_wt * (sigmoidf_(z) - y) + a.kd_wr * rg) / gb_f;
                     if (g == 0) lossAcc += a.kd_wt * bce_loss(z, y) + a.kd_wr * rl;
                 } else {
@@ -517,6 +539,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                     if (!DIAG_ON(a, DIAG_NO_GMF_SCATTER)) atomicAdd(a.grads + lay.ug + (int64_t)max(su[q], 0) * F + gf, dgm * igv[j]);
                     gIg[j] = dgm * ugv[j];
                 }
+                if constexpr (EARLY) load_gmf(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, l);
             }
             stamp(a, sb + 2);
 
@@ -617,11 +640,6 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                         for (int mt = 0; mt < S_::MT(0); ++mt)
                             if (16 * mt + 4 * g < S_::S(1))
                                 *reinterpret_cast<f4*>(scr + c * S_::SCM + 16 * mt + 4 * g) = D[0][mt];
-                        if (pub) {
-                            su2[(buf ^ 1) * TILE_ROWS + prow] = nu;
-                            si2[(buf ^ 1) * TILE_ROWS + prow] = ni;
-                            slab2[(buf ^ 1) * TILE_ROWS + prow] = nlab;
-                        }
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // same-wave LDS hand-off
                         stamp(a, sb + 3 + 3 * (L - 1));
                         if (l < S_::S(1)) {
@@ -630,7 +648,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                             for (int rr = 0; rr < 16; ++rr) s += scr[rr * S_::SCM + l];
                             dbAcc[0] += s;
                         }
-                        load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
+                        // EARLY: the next tile's fragments (issued after the forward and
+                        // the GMF backward) are waited for here, before the scatter, as a
+                        // waitcnt the compiler sees: their first uses in the next tile
+                        // then need no wait that would also drain this tile's atomics.
+                        if constexpr (EARLY) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
                         stamp(a, sb + 4 + 3 * (L - 1));
                         item_segments(scr, a, su, si, wr, l, gIg, gf, gq0);
                         constexpr int RPW = DM >= 64 ? 1 : 64 / DM;  // rows per wave-instruction
@@ -664,11 +686,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
                         for (int mt = 0; mt < S_::MT(0); ++mt)
                             *reinterpret_cast<f4*>(st + c * S_::SD(0) + 16 * mt + 4 * g) = D[0][mt];
-                        if (pub) {
-                            su2[(buf ^ 1) * TILE_ROWS + prow] = nu;
-                            si2[(buf ^ 1) * TILE_ROWS + prow] = ni;
-                            slab2[(buf ^ 1) * TILE_ROWS + prow] = nlab;
-                        }
+                        publish((buf ^ 1) * TILE_ROWS);
                         lds_barrier();
                         stamp(a, sb + 3 + 3 * (L - 1));
                         // bias grad: this wave's 16 rows, lane = output feature
@@ -803,11 +821,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
             } else {
                 // GMF-only model: item-side GMF rows, then publish next indices
                 item_segments(sstage + w * S_::WAVE_STAGE, a, su, si, wr, l, gIg, gf, gq0);
-                if (pub) {
-                    su2[(buf ^ 1) * TILE_ROWS + prow] = nu;
-                    si2[(buf ^ 1) * TILE_ROWS + prow] = ni;
-                    slab2[(buf ^ 1) * TILE_ROWS + prow] = nlab;
-                }
+                publish((buf ^ 1) * TILE_ROWS);
                 lds_barrier();
                 load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
             }
