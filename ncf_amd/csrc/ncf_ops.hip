@@ -226,6 +226,15 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
     if ((int)blockIdx.x < nA) {
         const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
         const int j = lo + (blockIdx.x * 16 + c4) * 4;
+        // the updating threads' optimizer state, requested ahead of the slab reads
+        const int64_t i = tb + j;
+        const bool upd = rg == 0 && j < tower_len && in_ranges(R, i);
+        f4 pp, mm, vv;
+        if (upd) {
+            pp = *reinterpret_cast<const f4*>(p + i);
+            mm = *reinterpret_cast<const f4*>(m + i);
+            vv = *reinterpret_cast<const f4*>(v + i);
+        }
         f4 s = f4{0.f, 0.f, 0.f, 0.f};
         if (j < wp.cols) {
             s = w0_part_sum(wp, j, rg);
@@ -253,13 +262,9 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
                 const f4 x = part[q][c4];
                 gs.x += x.x; gs.y += x.y; gs.z += x.z; gs.w += x.w;
             }
-            const int64_t i = tb + j;
             if (j == tower_len) {
                 if (loss_hist != nullptr && hist_len > 0) loss_hist[((b_step % hist_len) + hist_len) % hist_len] = gs.x;
-            } else if (j < tower_len && in_ranges(R, i)) {
-                f4 pp = *reinterpret_cast<const f4*>(p + i);
-                f4 mm = *reinterpret_cast<const f4*>(m + i);
-                f4 vv = *reinterpret_cast<const f4*>(v + i);
+            } else if (upd) {
                 adam_f4(pp, mm, vv, gs, w1, b2, omb2, bc2s, eps, neg_step);
                 *reinterpret_cast<f4*>(m + i) = mm;
                 *reinterpret_cast<f4*>(v + i) = vv;
@@ -765,71 +770,68 @@ __global__ __launch_bounds__(256) void kd_feature_kernel(KdFeatArgs a) {
 // Factored layer 0 (ncf_train.hip, FACT): the step left G_u = sum of the D0 rows
 // of user u in grads[um] and H_i in grads[im] (width DM = S(1)).  fact_expand_kernel
 // turns them into the true gradients; one block per FX_CH-row chunk of one table X
-// (X = Um with koff = 0, or Im with koff = DM), its G and X rows staged in LDS once:
-//   dX = G W0[:, koff : koff + DM]   per 16-row tile (one wave each), written over G
+// (X = Um with koff = 0, or Im with koff = DM), its G and X rows and the W0 half it
+// needs staged in LDS once, 16 waves each owning output tiles:
+//   dX = G W0[:, koff : koff + DM]   (16 x 16 tiles), written over G
 //   P_b = G^T X                       the block's partial of dW0[:, koff : koff + DM]
-//                                     (each wave owns NT of the NT x NT output tiles),
-//                                     plain stores to partials[b][DM][DM]
+//                                     (NT x NT tiles), plain stores to partials[b][DM][DM]
 // The tower reductions (reduce_slab_kernel / reduce_adam_kernel, W0Part) sum the
 // partials of each half in block order (deterministic, no atomics: every block's
 // partial covers the same 16 KB of W0, so float atomics would serialise on it).  v_mfma_f32_16x16x4_f32 throughout:
 // (U + I)/16 tile GEMMs per step in place of the per-row layer-0 dgrad / wgrad of B/16.
-constexpr int FX_WAVES = 4;
-constexpr int FX_CH = 64;  // rows per block = FX_WAVES row tiles of 16
+constexpr int FX_WAVES = 16;  // one 16x16 output tile of dW0 and one of dX per wave (DM = 64)
+constexpr int FX_CH = 64;     // table rows per block
 
 template <int DM>
 __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout lay, const float* __restrict__ prm,
                                                                      float* __restrict__ grads,
                                                                      float* __restrict__ partials, int nbu) {
-    constexpr int S0 = 2 * DM, SWS = S0 + 4, ST = DM + 4, NT = (DM + 15) / 16, Q4 = DM / 4;
+    constexpr int ST = DM + 4, NT = (DM + 15) / 16, Q4 = DM / 4;
     extern __shared__ __attribute__((aligned(16))) float fsm[];
-    float* sW = fsm;                  // W0 [DM][2DM], row stride SWS
-    float* sG = sW + DM * SWS;        // G rows [FX_CH][ST]
-    float* sX = sG + FX_CH * ST;      // X rows [FX_CH][ST]
+    float* sW = fsm;              // W0[:, koff : koff + DM]  [DM][ST]
+    float* sG = sW + DM * ST;     // G rows  [FX_CH][ST]
+    float* sX = sG + FX_CH * ST;  // X rows  [FX_CH][ST]
+    float* sO = sX + FX_CH * ST;  // dX rows [FX_CH][ST]
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, c = l & 15, g = l >> 4;
     const bool user = (int)blockIdx.x < nbu;
     const int64_t nrows = user ? lay.user_num : lay.item_num;
     const int64_t xoff = user ? lay.um : lay.im;
     const int koff = user ? 0 : DM;
     const int64_t r0 = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * FX_CH;
-    {   // W0, then the chunk's G and X rows -> LDS: each thread's loads issued together
-        constexpr int NW4 = DM * S0 / 4, PW = (NW4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
+    {   // the W0 half, the chunk's G and X rows -> LDS: each thread's loads issued together
+        constexpr int NW4 = DM * Q4, PW = (NW4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
         constexpr int NR4 = FX_CH * Q4, PR = (NR4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
         f4 wv[PW], gv[PR], xv[PR];
 #pragma unroll
         for (int q = 0; q < PW; ++q) {
-            const int e4 = tid + q * FX_WAVES * 64;
-            wv[q] = e4 < NW4 ? *reinterpret_cast<const f4*>(prm + lay.w[0] + 4 * e4) : f4{0.f, 0.f, 0.f, 0.f};
+            const int e4 = tid + q * FX_WAVES * 64, j = e4 / Q4, k4 = e4 - j * Q4;
+            wv[q] = e4 < NW4 ? *reinterpret_cast<const f4*>(prm + lay.w[0] + (int64_t)j * 2 * DM + koff + 4 * k4)
+                             : f4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int q = 0; q < PR; ++q) {
-            const int e4 = tid + q * FX_WAVES * 64;
-            const int row = e4 / Q4, qq = e4 - row * Q4;
+            const int e4 = tid + q * FX_WAVES * 64, row = e4 / Q4, k4 = e4 - row * Q4;
             const bool ok = e4 < NR4 && r0 + row < nrows;
-            gv[q] = ok ? *reinterpret_cast<const f4*>(grads + xoff + (r0 + row) * DM + 4 * qq) : f4{0.f, 0.f, 0.f, 0.f};
-            xv[q] = ok ? *reinterpret_cast<const f4*>(prm + xoff + (r0 + row) * DM + 4 * qq) : f4{0.f, 0.f, 0.f, 0.f};
+            gv[q] = ok ? *reinterpret_cast<const f4*>(grads + xoff + (r0 + row) * DM + 4 * k4) : f4{0.f, 0.f, 0.f, 0.f};
+            xv[q] = ok ? *reinterpret_cast<const f4*>(prm + xoff + (r0 + row) * DM + 4 * k4) : f4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int q = 0; q < PW; ++q) {
-            const int e4 = tid + q * FX_WAVES * 64;
-            if (e4 < NW4) {
-                const int j = (4 * e4) / S0, k = 4 * e4 - j * S0;
-                *reinterpret_cast<f4*>(sW + j * SWS + k) = wv[q];
-            }
+            const int e4 = tid + q * FX_WAVES * 64, j = e4 / Q4, k4 = e4 - j * Q4;
+            if (e4 < NW4) *reinterpret_cast<f4*>(sW + j * ST + 4 * k4) = wv[q];
         }
 #pragma unroll
         for (int q = 0; q < PR; ++q) {
-            const int e4 = tid + q * FX_WAVES * 64;
-            const int row = e4 / Q4, qq = e4 - row * Q4;
+            const int e4 = tid + q * FX_WAVES * 64, row = e4 / Q4, k4 = e4 - row * Q4;
             if (e4 < NR4) {
-                *reinterpret_cast<f4*>(sG + row * ST + 4 * qq) = gv[q];
-                *reinterpret_cast<f4*>(sX + row * ST + 4 * qq) = xv[q];
+                *reinterpret_cast<f4*>(sG + row * ST + 4 * k4) = gv[q];
+                *reinterpret_cast<f4*>(sX + row * ST + 4 * k4) = xv[q];
             }
         }
     }
     __syncthreads();
-    // dW0 partial: wave w owns output tiles (mt, nt) with (mt * NT + nt) % FX_WAVES == w.
-    // A[i = j][k = row] = G[row][j],  B[k = row][n = k'] = X[row][k'].
+    // dW0 partial, tiles (mt, nt) dealt round-robin to the waves:
+    // A[i = j][k = row] = G[row][j],  B[k = row][n = k'] = X[row][k']
     for (int tt = w; tt < NT * NT; tt += FX_WAVES) {
         const int mt = tt / NT, nt = tt - mt * NT;
         const bool jok = 16 * mt + c < DM, kok = 16 * nt + c < DM;
@@ -848,33 +850,23 @@ __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout l
             if (j < DM && kok) pb[j * DM + 16 * nt + c] = lane_get(a0, q);
         }
     }
-    // dX = G W0h for row tile w: A[i = row][k = j] = G[row][j],  B[k = j][n = k'] = W0[j][koff + k']
-    const float* gt = sG + 16 * w * ST;
-    f4 d[NT];
+    // dX = G W0h, tiles (rt, nt): A[i = row][k = j] = G[row][j],  B[k = j][n = k'] = W0h[j][k']
+    for (int tt = w; tt < (FX_CH / 16) * NT; tt += FX_WAVES) {
+        const int rt = tt / NT, nt = tt - rt * NT;
+        const bool nok = 16 * nt + c < DM;
+        f4 d = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) d[nt] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < DM / 4; ++kk) {
-        const float av = gt[c * ST + 4 * kk + g];
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-            const float bv = (16 * nt + c < DM) ? sW[(4 * kk + g) * SWS + koff + 16 * nt + c] : 0.f;
-            d[nt] = MFMA4(av, bv, d[nt]);
-        }
-    }
-    __syncthreads();  // every wave is done reading sX (dW0) before tile w's dX goes there
-    float* dt = sX + 16 * w * ST;
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+        for (int kk = 0; kk < DM / 4; ++kk)
+            d = MFMA4(sG[(16 * rt + c) * ST + 4 * kk + g], nok ? sW[(4 * kk + g) * ST + 16 * nt + c] : 0.f, d);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            if (16 * nt + c < DM) dt[(4 * g + q) * ST + 16 * nt + c] = lane_get(d[nt], q);
-    wave_sync_lds();
-    for (int e = l; e < 16 * Q4; e += 64) {
+            if (nok) sO[(16 * rt + 4 * g + q) * ST + 16 * nt + c] = lane_get(d, q);
+    }
+    __syncthreads();
+    for (int e = tid; e < FX_CH * Q4; e += FX_WAVES * 64) {
         const int row = e / Q4, q = e - row * Q4;
-        const int64_t rr = r0 + 16 * w + row;
-        if (rr < nrows)
-            *reinterpret_cast<f4*>(grads + xoff + rr * DM + 4 * q) = *reinterpret_cast<const f4*>(dt + row * ST + 4 * q);
+        if (r0 + row < nrows)
+            *reinterpret_cast<f4*>(grads + xoff + (r0 + row) * DM + 4 * q) = *reinterpret_cast<const f4*>(sO + row * ST + 4 * q);
     }
 }
 
@@ -948,7 +940,7 @@ static int launch_fact_expand(const ncf_layout* lay, const float* params, float*
     ncf_layout l = *lay;
     int nbu;
     int nblk = fact_blocks(lay, &nbu);
-    const int64_t lds = ((int64_t)DM * (2 * DM + 4) + 2LL * FX_CH * (DM + 4)) * 4;
+    const int64_t lds = ((int64_t)DM * (DM + 4) + 3LL * FX_CH * (DM + 4)) * 4;
     if (ensure_lds(fe, lds) != NCF_OK) return NCF_E_LAUNCH;
     void* ae[] = {&l, (void*)&params, (void*)&grads, (void*)&partials, &nbu};
     if (hipLaunchKernel(fe, dim3((unsigned)nblk), dim3(FX_WAVES * 64), ae, (size_t)lds, st) != hipSuccess)
