@@ -100,7 +100,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     float* slab2 = reinterpret_cast<float*>(si2 + 2 * TILE_ROWS);  // [2][TILE_ROWS] labels / dlogits
     float* szg = slab2 + 2 * TILE_ROWS;  // GMF part of the logit, per tile row
     float* sdz = szg + TILE_ROWS;        // dlogit, per tile row
-    float* sB = sdz + TILE_ROWS;         // biases, layer k at boff(k), zero-padded
+    float* stl2 = sdz + TILE_ROWS;       // [2][TILE_ROWS] NCF_DZ_KD: teacher logits
+    float* sB = stl2 + 2 * TILE_ROWS;    // biases, layer k at boff(k), zero-padded
     float* sWP = sB + 128;               // predict weights, zero-padded
     float* sstage = sWP + 128;           // union: per-wave staging | epilogue images
 
@@ -156,9 +157,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     // published into LDS: nothing touches the loaded registers before then, so no
     // wait for it (and, the vmcnt counter being in order, for every scatter atomic
     // issued before it) lands at the top of a tile.
-    uint64_t npr = 0;
-    float ndl = 0.f;
-    bool nok = false;
+    // FACT: two tiles ahead (npr2 ...), shifted into npr ... behind the explicit
+    // wait before each tile's scatter, so no wait for them follows any atomic.
+    uint64_t npr = 0, npr2 = 0;
+    float ndl = 0.f, ndl2 = 0.f;
+    bool nok = false, nok2 = false;
     auto load_idx = [&](int64_t row0) {
         const int64_t r = row0 + prow;
         nok = r < nloc;
@@ -166,15 +169,25 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         npr = a.rows[rc];
         if constexpr (!FWD_ONLY) ndl = a.dlogit[rc];  // forward launches carry no labels
     };
+    auto load_idx2 = [&](int64_t row0) {
+        const int64_t r = row0 + prow;
+        nok2 = r < nloc;
+        const int64_t rc = base + (nok2 ? r : 0);
+        npr2 = a.rows[rc];
+        if constexpr (!FWD_ONLY) ndl2 = a.dlogit[rc];
+    };
     auto publish = [&](int off) {
         if (pub) {
             su2[off + prow] = nok ? (int)(uint32_t)npr : -1;
             si2[off + prow] = nok ? (int)((npr >> 32) & 0x7fffffffu) : -1;
-            if constexpr (!FWD_ONLY)
+            if constexpr (!FWD_ONLY) {
                 slab2[off + prow] = a.dz_mode == NCF_DZ_DLOGIT ? ndl : (float)(uint32_t)(npr >> 63);
+                stl2[off + prow] = ndl;  // NCF_DZ_KD: the teacher logit (else unused)
+            }
         }
     };
     if ((int64_t)blockIdx.x < ntiles) load_idx((int64_t)blockIdx.x * TILE_ROWS);
+    if constexpr (FACT && !FWD_ONLY) load_idx2(((int64_t)blockIdx.x + gridDim.x) * TILE_ROWS);
 
     // ---- tower weights, biases, predict weights -> LDS (zero-padded) ---------
     if constexpr (S_::MLP) {
@@ -240,6 +253,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     const float bpv = prm[lay.bp];
     const float wpf = S_::GMF ? prm[lay.wp + l0 % F] : 0.f;
     publish(0);
+    if constexpr (FACT && !FWD_ONLY) {
+        npr = npr2;
+        ndl = ndl2;
+        nok = nok2;
+    }
     __syncthreads();
 
     // Embedding fragments of the current tile, loaded one tile ahead:
@@ -369,6 +387,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(ugv[j]), "v"(igv[j]));
     }
+    // EARLY: nothing in flight at the loop entry (the prologue's scalars included),
+    // so the loop's only pending memory operations are its own
+    if constexpr (EARLY) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     stamp(a, 1);
     int titer = 0;
 
@@ -390,8 +411,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         const int gq0 = l / F;
 
         // (a) next tile's indices
-        load_idx(row0 + (int64_t)gridDim.x * TILE_ROWS);
-        nok = nok && has_next;
+        if constexpr (EARLY) {
+            load_idx2(row0 + 2 * (int64_t)gridDim.x * TILE_ROWS);
+        } else {
+            load_idx(row0 + (int64_t)gridDim.x * TILE_ROWS);
+            nok = nok && has_next;
+        }
 
         // (b) GMF forward
         if constexpr (S_::GMF) {
@@ -442,11 +467,6 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
             });
         }
         stamp(a, sb + 1);
-        // NCF_DZ_KD: this row's teacher logit, requested ahead of the EARLY gathers
-        // so that waiting for it does not wait for them (an in-range dummy read in
-        // the other modes, where dlogit aliases the rows or carries dL/dlogit).
-        float tlog = 0.f;
-        if constexpr (!FWD_ONLY) tlog = a.dlogit[base + min(row0 + myq, nloc - 1)];
         if constexpr (EARLY) {
             publish((buf ^ 1) * TILE_ROWS);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // same-wave LDS hand-off
@@ -514,7 +534,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                     // distillation (base.py:40-50; response term: kd_response)
                     const float y = slab_[myq];
                     float rl;
-                    const float rg = kd_response(z, tlog, a.kd_temp, &rl);
+                    const float rg = kd_response(z, stl2[buf * TILE_ROWS + myq], a.kd_temp, &rl);
                     dz = (a.kd_wt * (sigmoidf_(z) - y) + a.kd_wr * rg) / gb_f;
                     if (g == 0) lossAcc += a.kd_wt * bce_loss(z, y) + a.kd_wr * rl;
                 } else {
@@ -652,7 +672,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                         // the GMF backward) are waited for here, before the scatter, as a
                         // waitcnt the compiler sees: their first uses in the next tile
                         // then need no wait that would also drain this tile's atomics.
-                        if constexpr (EARLY) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                        if constexpr (EARLY) {
+                            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                            npr = npr2;  // the rows of tile t + 2, published in tile t + 1
+                            ndl = ndl2;
+                            nok = nok2;
+                        }
                         stamp(a, sb + 4 + 3 * (L - 1));
                         item_segments(scr, a, su, si, wr, l, gIg, gf, gq0);
                         constexpr int RPW = DM >= 64 ? 1 : 64 / DM;  // rows per wave-instruction

@@ -34,9 +34,14 @@ def _models(mt, f, L, U=50, I=80, seed=1):
     return ref, m.to(DEV)
 
 
-def _close_grad(got, exp, name):
+def _close_grad(got, exp, name, terms=None):
+    """rtol 1e-4, atol 1e-6 of the largest gradient -- or, for embedding tables whose
+    rows sum `terms` per-row contributions in float-atomic (arrival) order, an atol
+    growing like the fp32 rounding of such a sum: 2e-8 * sqrt(terms) * max|g|
+    (zipf-hot items take ~30K rows of one batch: 3.5e-6 * max|g|)."""
     scale = max(float(np.abs(exp).max()), 1e-30)
-    np.testing.assert_allclose(got, exp, rtol=1e-4, atol=1e-6 * scale, err_msg=name)
+    atol = 1e-6 * scale if terms is None else max(1e-6, 2e-8 * float(np.sqrt(terms))) * scale
+    np.testing.assert_allclose(got, exp, rtol=1e-4, atol=atol, err_msg=name)
 
 
 @pytest.mark.parametrize("mt", MODEL_TYPES)
@@ -156,7 +161,8 @@ def test_one_step_grads_vs_oracle(cfg):
     for (p, off), (name, _) in zip(ops._segments(m, lay), m.named_parameters()):
         got = gflat[off:off + p.numel()].view_as(p).cpu().numpy()
         if name in grads_ref:
-            _close_grad(got, grads_ref[name].numpy(), name)
+            hot = int(np.bincount(items).max()) if "item" in name else int(np.bincount(users).max())
+            _close_grad(got, grads_ref[name].numpy(), name, terms=hot if "embed" in name else None)
         else:  # unused in this model type (reference grad None): nothing may be written
             assert not got.any(), name
 
