@@ -114,6 +114,27 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     const ncf_layout& lay = a.lay;
     const float* __restrict__ prm = a.params;
 
+    // Tower weight / bias loads first: they depend on nothing, so they fly while
+    // the control block and the row indices make their round trips.
+    constexpr int PERMAX = S_::MLP ? (16 * S_::MT(0) * (S_::S(0) / 4) + NTHREADS - 1) / NTHREADS : 1;
+    f4 wreg[L][PERMAX];
+    float breg[L];
+    if constexpr (S_::MLP) {
+        static_for<L>([&](auto kk) {
+            constexpr int k = decltype(kk)::value;
+            constexpr int rows = 16 * S_::MT(k), cols4 = S_::S(k) / 4, outs = S_::S(k + 1);
+            constexpr int PER = (rows * cols4 + NTHREADS - 1) / NTHREADS;
+            const f4* Wg = reinterpret_cast<const f4*>(prm + lay.w[k]);
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                const int e = tid + q * NTHREADS;
+                const int o = e / cols4;
+                wreg[k][q] = (e < rows * cols4 && o < outs) ? Wg[e] : f4{0.f, 0.f, 0.f, 0.f};
+            }
+            breg[k] = tid < outs ? prm[lay.b[k] + tid] : 0.f;  // 16 * MT(k) <= 128 < NTHREADS
+        });
+    }
+
     // ---- rows of this rank -------------------------------------------------
     int64_t base, nloc;
     float gb_f = 1.0f;
@@ -191,24 +212,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 
     // ---- tower weights, biases, predict weights -> LDS (zero-padded) ---------
     if constexpr (S_::MLP) {
-        // every layer's loads first (one memory round trip for the whole prologue),
-        // then the LDS stores
-        constexpr int PERMAX = (16 * S_::MT(0) * (S_::S(0) / 4) + NTHREADS - 1) / NTHREADS;
-        f4 wreg[L][PERMAX];
-        float breg[L];
-        static_for<L>([&](auto kk) {
-            constexpr int k = decltype(kk)::value;
-            constexpr int rows = 16 * S_::MT(k), cols4 = S_::S(k) / 4, outs = S_::S(k + 1);
-            constexpr int PER = (rows * cols4 + NTHREADS - 1) / NTHREADS;
-            const f4* Wg = reinterpret_cast<const f4*>(prm + lay.w[k]);
-#pragma unroll
-            for (int q = 0; q < PER; ++q) {
-                const int e = tid + q * NTHREADS;
-                const int o = e / cols4;
-                wreg[k][q] = (e < rows * cols4 && o < outs) ? Wg[e] : f4{0.f, 0.f, 0.f, 0.f};
-            }
-            breg[k] = tid < outs ? prm[lay.b[k] + tid] : 0.f;  // 16 * MT(k) <= 128 < NTHREADS
-        });
+        // (their loads were issued at the top of the kernel, ahead of the control
+        // block read the row range depends on)
         static_for<L>([&](auto kk) {
             constexpr int k = decltype(kk)::value;
             constexpr int rows = 16 * S_::MT(k), cols4 = S_::S(k) / 4;
