@@ -950,7 +950,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                 out[pos] = ts;
             }
         };
-        lds_barrier();  // every wave is past its last tile: the staging is free
+        // every wave past its last tile: the staging is free.  FACT: a wave's staging
+        // slot was private to it during the tiles (no layer-0 wgrad across waves), so
+        // each wave writes its images into it as soon as it is done, and the first
+        // cross-wave read below waits at that round's barrier instead.
+        if constexpr (!FACT) lds_barrier();
         stamp(a, 62);
         if constexpr (S_::MLP && L >= 2) {
             // Layers k >= 1: each wave writes its register partials to its own LDS
