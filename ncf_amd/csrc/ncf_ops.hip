@@ -884,7 +884,10 @@ int launch_zero_f32(float* p, int64_t n, hipStream_t st) {
 // have fewer rows than FACT_MAX_ROWS (the expand pass works on U + I rows per step,
 // the per-row layer-0 gradients on B rows: at ml-1m 9.7K vs 65K; at ml-20m the
 // tables have 165K rows and the per-row form stays).
-constexpr int64_t FACT_MAX_ROWS = 32768;
+#ifndef NCF_FACT_MAX_ROWS
+#define NCF_FACT_MAX_ROWS 32768
+#endif
+constexpr int64_t FACT_MAX_ROWS = NCF_FACT_MAX_ROWS;
 // Fused kernel for this layout, or nullptr (then the layered path runs).
 static const KernelEntry* fused_entry(const ncf_layout* lay) {
     const KernelEntry* e = find_entry(lay->model_type, lay->factor_num, lay->num_layers);
