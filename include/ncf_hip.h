@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 7
+#define NCF_ABI_VERSION 8
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -175,19 +175,20 @@ int ncf_pack_rows(const int32_t *users, const int32_t *items, const float *label
                   uint64_t *rows_out, void *stream);
 
 /*
- * Second half of the backward on the factored path (MLP shapes with a fused kernel
- * and user_num + item_num <= 32768; a no-op returning NCF_OK for every other
- * layout).  There ncf_train_step scatter-adds, per row, the layer-0 pre-activation
- * gradient D0 (width dm) into the user and item rows of grads[um] / grads[im] instead
- * of forming the layer-0 weight and data gradients per row; this call turns those
- * row sums into the true gradients (all from the same params the step used):
+ * Factored layer 0 (MLP shapes with a fused kernel and user_num + item_num <= 32768):
+ * there the fused kernel scatter-adds, per row, the layer-0 pre-activation gradient
+ * D0 (width dm) into the user and item rows of grads[um] / grads[im] instead of
+ * forming the layer-0 weight and data gradients per row, and a second launch turns
+ * those row sums into the true gradients (from the same params the step used):
  *   dUm = G W0[:, :dm],  dIm = H W0[:, dm:]   (in place),
  *   dW0 = [G^T Um | H^T Im]                   (per-block partials in the tail of the
  *                                              train workspace; ncf_reduce_slab /
  *                                              ncf_reduce_adam_step sum them in a fixed
  *                                              order with the other tower columns).
- * Call sequence per step: ncf_train_step[_kd] -> ncf_expand_grads ->
- * [ncf_kd_feature_step] -> ncf_reduce_slab or ncf_reduce_adam_step.
+ * Since ABI 8 ncf_train_step / ncf_train_step_kd issue that second launch
+ * themselves, so a step is always: ncf_train_step[_kd] -> [ncf_kd_feature_step] ->
+ * ncf_reduce_slab or ncf_reduce_adam_step.  ncf_expand_grads is kept as a no-op
+ * (NCF_OK) so an ABI-7 sequence that still calls it trains correctly.
  */
 int ncf_expand_grads(const ncf_layout *lay, const float *params, float *grads, void *workspace, void *stream);
 
@@ -255,6 +256,29 @@ int64_t ncf_prepare_epoch_workspace(int64_t n, int64_t batch_global, int item_nu
 int ncf_prepare_epoch(const uint64_t *rows, const int64_t *perm, int64_t n, int64_t batch_global,
                       int item_num, uint64_t *rows_out, void *workspace, int64_t workspace_bytes,
                       void *stream);
+
+/*
+ * Device epoch pipeline: the DataLoader(shuffle=True) permutation and the epoch's
+ * rows built on the device (the negatives come from the host sampler,
+ * ncf_sampler.h; the generator words from ncf_mt_words).
+ *
+ * ncf_randperm: torch.randperm(n, generator=g) after g.manual_seed(seed) (the
+ * RandomSampler of DataLoader(shuffle=True), train_neumf.py:55): Fisher-Yates
+ * swapping r[i] with r[i + words[i] % (n - i)], words = the first n - 1 words of
+ * ncf_mt_seed(seed & 0xffffffff), run as `rounds` parallel reservation rounds
+ * (~2.3 log2(n) needed; 2.5 log2(n) + 16 is ample), then any swap still pending
+ * (up to 4096) applied in order by one thread.  *remaining (device int32) = 0 when
+ * the permutation is complete, else the number left (call again, more rounds).
+ *
+ * ncf_build_rows: rows_out = NCF_ROW_PACK of features_fill / labels_fill
+ * (datasets.py:65-69): positives in file order, then positive p's num_ng
+ * negatives neg[p*num_ng .. (p+1)*num_ng).
+ */
+int64_t ncf_randperm_workspace(int64_t n);
+int ncf_randperm(const uint32_t *words, int64_t n, int64_t *perm, int rounds, void *workspace, int64_t workspace_bytes,
+                 int32_t *remaining, void *stream);
+int ncf_build_rows(const int32_t *pos_users, const int32_t *pos_items, int64_t n_pos, const int32_t *neg, int num_ng,
+                   uint64_t *rows_out, void *stream);
 
 /*
  * HR@K / NDCG@K per DataLoader batch (metrics.py:4-25): batches of `batch`

@@ -29,6 +29,15 @@ int ncf_sampler_contains(const void *s, int32_t u, int32_t i);
 void ncf_mt_seed(uint32_t seed, uint32_t *key, int32_t *pos);
 
 /*
+ * Continue the MT19937 stream (key, pos) by n tempered 32-bit words into out
+ * (NULL: advance only) -- the words numpy's legacy RandomState and torch's CPU
+ * generator (torch.Generator.manual_seed(s): key = ncf_mt_seed(s & 0xffffffff))
+ * draw next.  The device epoch pipeline (ncf_sample_negatives, ncf_randperm in
+ * ncf_hip.h) consumes them.
+ */
+void ncf_mt_words(uint32_t *key, int32_t *pos, int64_t n, uint32_t *out);
+
+/*
  * One ng_sample() pass: for every positive p (file order) and t < num_ng, draw
  * j = randint(num_item) until (user[p], j) is not a positive; out_items[p*num_ng+t] = j.
  * key/pos: the MT19937 state, advanced in place.  Returns the number of 32-bit

@@ -1081,7 +1081,11 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
     if (hipLaunchKernel(fn, dim3(SLAB_ROWS), dim3(NTHREADS), args, (size_t)lds, (hipStream_t)stream) !=
         hipSuccess)
         return NCF_E_LAUNCH;
-    return launch_status();
+    const int rc = launch_status();
+    if (rc != NCF_OK || !fact_mode(lay)) return rc;
+    // factored layer 0: the per-user / per-item D0 sums -> dUm, dIm, dW0 partials
+    float* partials = slab + (int64_t)SLAB_ROWS * ncf_slab_stride(lay);
+    return launch_fact_expand(lay, params, grads, partials, (hipStream_t)stream);
 }
 
 int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
@@ -1265,11 +1269,12 @@ int ncf_sgd_step(float* params, float* grads, const int64_t* ranges, int nranges
 int ncf_zero_f32(float* p, int64_t n, void* stream) { return launch_zero_f32(p, n, (hipStream_t)stream); }
 
 int ncf_expand_grads(const ncf_layout* lay, const float* params, float* grads, void* workspace, void* stream) {
+    (void)workspace;
+    (void)stream;
+    // ABI 8: ncf_train_step[_kd] launches the expansion itself; kept as a no-op so
+    // an ABI-7 call sequence (step -> expand -> reduce) still trains correctly.
     if (!lay || !params || !grads) return NCF_E_ARG;
-    if (!fact_mode(lay)) return NCF_OK;
-    if (!workspace) return NCF_E_ARG;
-    float* partials = static_cast<float*>(workspace) + (int64_t)SLAB_ROWS * ncf_slab_stride(lay);
-    return launch_fact_expand(lay, params, grads, partials, (hipStream_t)stream);
+    return NCF_OK;
 }
 
 int ncf_pack_rows(const int32_t* users, const int32_t* items, const float* labels, int64_t n, uint64_t* rows_out,
@@ -1295,6 +1300,7 @@ int ncf_gather_epoch(const uint64_t* rows, const int64_t* perm, int64_t n, uint6
 
 int64_t ncf_prepare_epoch_workspace(int64_t n, int64_t batch_global, int item_num) {
     if (n < 0 || batch_global <= 0 || item_num <= 0) return -1;
+    if (batch_global < PREP_GROUP_MIN) return al256(8);  // plain shuffle: no histogram, no parts
     const int64_t nb = (n + batch_global - 1) / batch_global;
     const int P = prep_parts(batch_global);
     return al256(n * 8) + al256(nb * item_num * 4) + al256(nb * (P + 1) * 2 * 4);
@@ -1306,12 +1312,6 @@ int ncf_prepare_epoch(const uint64_t* rows, const int64_t* perm, int64_t n, int6
     if (batch_global > 0x7fffffff) return NCF_E_ARG;
     if (workspace_bytes < ncf_prepare_epoch_workspace(n, batch_global, item_num)) return NCF_E_ARG;
     if (n == 0) return NCF_OK;
-    const int64_t nb = (n + batch_global - 1) / batch_global;
-    const int P = prep_parts(batch_global);
-    char* ws = static_cast<char*>(workspace);
-    uint64_t* shuf = reinterpret_cast<uint64_t*>(ws);
-    int* hist = reinterpret_cast<int*>(ws + al256(n * 8));
-    int* parts = reinterpret_cast<int*>(ws + al256(n * 8) + al256(nb * item_num * 4));
     hipStream_t st = (hipStream_t)stream;
     if (batch_global < PREP_GROUP_MIN) {  // small batches: item runs ~1 row, grouping buys nothing
         int64_t grid = (n + 255) / 256;
@@ -1319,6 +1319,12 @@ int ncf_prepare_epoch(const uint64_t* rows, const int64_t* perm, int64_t n, int6
         hipLaunchKernelGGL(gather_epoch_kernel, dim3((int)grid), dim3(256), 0, st, rows, perm, n, rows_out);
         return launch_status();
     }
+    const int64_t nb = (n + batch_global - 1) / batch_global;
+    const int P = prep_parts(batch_global);
+    char* ws = static_cast<char*>(workspace);
+    uint64_t* shuf = reinterpret_cast<uint64_t*>(ws);
+    int* hist = reinterpret_cast<int*>(ws + al256(n * 8));
+    int* parts = reinterpret_cast<int*>(ws + al256(n * 8) + al256(nb * item_num * 4));
     if (hipMemsetAsync(hist, 0, (size_t)(nb * item_num * 4), st) != hipSuccess) return NCF_E_LAUNCH;
     if (item_num <= SH2_MAX_ITEMS && !(g_diag & DIAG_PREP_DIRECT)) {
         const int chunks = (int)((batch_global + SH_CHUNK - 1) / SH_CHUNK);

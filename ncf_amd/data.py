@@ -54,13 +54,19 @@ class HostSampler:
     def contains(self, u, i):
         return bool(L.sampler_lib().ncf_sampler_contains(self._h, int(u), int(i)))
 
-    def sample(self, num_item, num_ng, key=None, pos=None):
+    def sample(self, num_item, num_ng, key=None, pos=None, out=None):
         """Negatives for every positive (file order) x num_ng.  With key/pos None
-        NumPy's global stream is used and advanced (the np.random.seed protocol)."""
+        NumPy's global stream is used and advanced (the np.random.seed protocol);
+        else the given state arrays (uint32[624], int32[1]) are advanced in place.
+        out: optional int32 destination (e.g. pinned staging)."""
         use_global = key is None
         if use_global:
             st, key, pos = _state_arrays()
-        out = np.empty(len(self.pos_users) * int(num_ng), dtype=np.int32)
+        n = len(self.pos_users) * int(num_ng)
+        if out is None:
+            out = np.empty(n, dtype=np.int32)
+        elif out.dtype != np.int32 or not out.flags.c_contiguous or len(out) < n:
+            raise ValueError("out: contiguous int32 of at least n_pos * num_ng")
         words = L.sampler_lib().ncf_sampler_sample(self._h, int(num_item), int(num_ng), key.ctypes.data,
                                                    pos.ctypes.data, out.ctypes.data)
         if words < 0:
@@ -92,6 +98,7 @@ class NCFData(data.Dataset):
         self.labels = np.zeros(len(f), dtype=np.int64)
         self._fill_u = self._fill_i = self._fill_y = None
         self._ng_u = self._ng_i = None
+        self._neg_dev = None  # negatives drawn on the device (ncf_amd.pipeline), fetched on use
         self._sampler = None
 
     # -- compatibility views (lists, like the reference) ---------------------
@@ -101,19 +108,44 @@ class NCFData(data.Dataset):
 
     @property
     def features_ng(self):
+        self._materialize()
         return np.stack([self._ng_u, self._ng_i], 1).astype(np.int64).tolist()
 
     @property
     def features_fill(self):
+        self._materialize()
         return np.stack([self._fill_u, self._fill_i], 1).astype(np.int64).tolist()
 
     @property
     def labels_fill(self):
+        self._materialize()
         return self._fill_y.astype(np.int64).tolist()
 
     # -- arrays for the device engine ----------------------------------------
+    def _set_negatives(self, neg):
+        self._ng_u = np.repeat(self._ps_u, self.num_ng)
+        self._ng_i = neg
+        self._fill_u = np.concatenate([self._ps_u, self._ng_u])
+        self._fill_i = np.concatenate([self._ps_i, self._ng_i])
+        self._fill_y = np.concatenate([np.ones(len(self._ps_u), dtype=np.int64),
+                                       np.zeros(len(self._ng_u), dtype=np.int64)])
+
+    def _set_device_negatives(self, neg_dev):
+        """This epoch's negatives live on the device (ng_sample done there); the host
+        arrays are rebuilt from them only if something asks for them."""
+        self._neg_dev = neg_dev if neg_dev is not None else None
+        if neg_dev is None:
+            self._set_negatives(np.zeros(0, dtype=np.int32))
+
+    def _materialize(self):
+        if self._neg_dev is not None:
+            neg = self._neg_dev.cpu().numpy().astype(np.int32)
+            self._neg_dev = None
+            self._set_negatives(neg)
+
     def arrays(self):
         """(users int32, items int32, labels float32) in reference fill order."""
+        self._materialize()
         if self.is_training:
             return self._fill_u, self._fill_i, self._fill_y.astype(np.float32)
         return self._ps_u, self._ps_i, self.labels.astype(np.float32)
@@ -138,23 +170,21 @@ class NCFData(data.Dataset):
 
     def ng_sample(self):
         assert self.is_training, "no need to sampling when testing"
-        neg = self._get_sampler().sample(self.num_item, self.num_ng)
-        self._ng_u = np.repeat(self._ps_u, self.num_ng)
-        self._ng_i = neg
-        self._fill_u = np.concatenate([self._ps_u, self._ng_u])
-        self._fill_i = np.concatenate([self._ps_i, self._ng_i])
-        self._fill_y = np.concatenate([np.ones(len(self._ps_u), dtype=np.int64),
-                                       np.zeros(len(self._ng_u), dtype=np.int64)])
+        self._neg_dev = None
+        self._set_negatives(self._get_sampler().sample(self.num_item, self.num_ng))
 
     def __len__(self):
         return (self.num_ng + 1) * len(self.labels)
 
     def __getitem__(self, idx):
+        if self._neg_dev is not None:
+            self._materialize()
         if self.is_training:
             return int(self._fill_u[idx]), int(self._fill_i[idx]), int(self._fill_y[idx])
         return int(self._ps_u[idx]), int(self._ps_i[idx]), int(self.labels[idx])
 
     def __getitems__(self, indices):
+        self._materialize()
         idx = np.asarray(indices, dtype=np.int64)
         if self.is_training:
             u, i, y = self._fill_u[idx], self._fill_i[idx], self._fill_y[idx]
@@ -211,13 +241,29 @@ def load_all(test_num=100):
     return train_data, test_data, user_num, item_num, train_mat
 
 
+def epoch_permutation_seed(generator=None, peek=False):
+    """The two draws a DataLoader(shuffle=True) epoch makes on the torch global (or
+    given) generator -- one int64 base_seed by the loader iterator, one int64
+    seeding RandomSampler's private generator -- returning the latter
+    (scripts/train_neumf.py:55,106; torch/utils/data).  peek: restore the
+    generator afterwards (nothing consumed)."""
+    if peek:
+        state = generator.get_state() if generator is not None else torch.get_rng_state()
+    try:
+        torch.empty((), dtype=torch.int64).random_(generator=generator)
+        return int(torch.empty((), dtype=torch.int64).random_(generator=generator).item())
+    finally:
+        if peek:
+            if generator is not None:
+                generator.set_state(state)
+            else:
+                torch.set_rng_state(state)
+
+
 def epoch_permutation(n, generator=None):
-    """DataLoader(shuffle=True) epoch order on the torch global (or given)
-    generator: one int64 base_seed draw by the loader iterator, one int64 draw
-    seeding RandomSampler's private generator, then randperm(n) -- the exact
-    consumption of scripts/train_neumf.py:55,106 (torch/utils/data)."""
-    torch.empty((), dtype=torch.int64).random_(generator=generator)
-    seed = int(torch.empty((), dtype=torch.int64).random_(generator=generator).item())
+    """DataLoader(shuffle=True) epoch order: epoch_permutation_seed, then
+    randperm(n) on a generator seeded with it."""
+    seed = epoch_permutation_seed(generator)
     g = torch.Generator()
     g.manual_seed(seed)
     return torch.randperm(n, generator=g)

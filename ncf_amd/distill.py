@@ -363,8 +363,7 @@ class DeviceDistillPlan:
                                       eng.rows.data_ptr(), self.tlog.data_ptr(), eng.ctl.data_ptr(),
                                       eng.batch_size, eng.world_size, eng.rank, self.w_task, self.w_resp,
                                       self.temperature, eng.ws.data_ptr(), eng.ws.numel() * 4, None, st),
-                "ncf_train_step_kd")
-        eng._expand(st)  # before the feature terms add plain embedding gradients
+                "ncf_train_step_kd")  # (factored layer 0 expanded inside, before the feature terms)
         if self.keys:
             g = self.keys.get("gmf_features", (None, None, 0.0))
             m = self.keys.get("mlp_input", (None, None, 0.0))

@@ -7,8 +7,8 @@ with the all-reduce issued between them, see ``_capture_collective``):
 
   1. ``ncf_train_step``  fused gather / GMF / MFMA tower fwd / BCE / MFMA tower
                          bwd / embedding scatter-add   (models.py:97-118,
-                         train_neumf.py:111-114), then ``ncf_expand_grads``
-                         (factored layer 0: per-user/item sums -> dUm, dIm, dW0)
+                         train_neumf.py:111-114); on the factored path it also
+                         launches the expansion (per-user/item sums -> dUm, dIm, dW0)
   2. ``ncf_reduce_slab`` per-workgroup tower grads -> flat grad buffer
   3. world > 1, dp_mode "zero1" (default): RCCL reduce-scatter of the flat grad
      buffer; dp_mode "allreduce": RCCL all-reduce of it
@@ -124,11 +124,15 @@ class TrainEngine:
         self._graph_key = None
 
     # ------------------------------------------------------------------ data
-    def set_epoch_stream(self, rows, batch_size):
+    def set_epoch_stream(self, rows, batch_size, checked=False):
         """Packed int64 rows (ops.pack_rows / ncf_prepare_epoch output) already in
-        training order: batch b is rows[b*batch_size, ...)."""
+        training order: batch b is rows[b*batch_size, ...).  Ids are range-checked
+        once here (IndexError like nn.Embedding) unless the caller already did
+        (`checked`, e.g. Trainer on the host arrays)."""
         if rows.dtype != torch.int64 or not rows.is_contiguous() or rows.device != self.device:
             raise ValueError("epoch stream: contiguous int64 packed rows on the engine's device")
+        if not checked:
+            ops.check_rows(rows, self.model.user_num, self.model.item_num)
         n = rows.numel()
         self.rows = rows
         self.n_total = n
@@ -137,6 +141,11 @@ class TrainEngine:
             per = (int(batch_size) + self.world_size - 1) // self.world_size
             self.ws = ops.new_workspace(self.lay, per, self.device)
         self.batch_size = int(batch_size)
+        if self.num_batches > self.loss_hist.numel():
+            # the optimizer launches write loss_hist[b % num_batches]: one slot per
+            # batch of the epoch (a captured graph holds the old pointer: re-capture)
+            self.loss_hist = torch.zeros(self.num_batches, dtype=torch.float32, device=self.device)
+            self._graph = None
         self.ctl[0] = 0
         self.ctl[2] = n
         self.ctl[3] = 0
@@ -216,13 +225,6 @@ class TrainEngine:
                                        self.rows.data_ptr(), None, self.ctl.data_ptr(), self.batch_size,
                                        self.world_size, self.rank, L.DZ_BCE, self.ws.data_ptr(),
                                        self.ws.numel() * 4, None, st), "ncf_train_step")
-        self._expand(st)
-
-    def _expand(self, st):
-        """Factored layer 0: per-user/item D0 sums -> dUm, dIm, dW0 (no-op otherwise)."""
-        L.check(L.hip().ncf_expand_grads(ctypes.byref(self.lay), self.flat.data_ptr(), self.grads.data_ptr(),
-                                         self.ws.data_ptr(), st),
-                "ncf_expand_grads")
 
     def _reduce_adam(self):
         st = L.stream_ptr(self.device)
@@ -288,7 +290,6 @@ class TrainEngine:
             L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.rows.data_ptr(),
                                        None, self.ctl.data_ptr(), self.batch_size, self.world_size, self.rank,
                                        L.DZ_BCE, self.ws.data_ptr(), self.ws.numel() * 4, None, sp), "ncf_train_step")
-            self._expand(sp)
         launch()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)

@@ -35,6 +35,7 @@ def evaluate_arrays(model, users, items, batch, top_k):
     from . import ops
     flat, lay = ops.ensure_flat(model)
     dev = flat.device
+    ops.check_ids(users, items, model.user_num, model.item_num)  # nn.Embedding raises (models.py:108-112)
     u = torch.as_tensor(np.asarray(users), dtype=torch.int32).to(dev)
     i = torch.as_tensor(np.asarray(items), dtype=torch.int32).to(dev)
     with torch.no_grad():

@@ -90,6 +90,34 @@ def pack_rows(users_i32, items_i32, labels_f32=None, out=None):
     return out
 
 
+def check_ids(users, items, user_num, item_num):
+    """nn.Embedding's range check (reference models.py:98-112 raise IndexError on an
+    id outside the table) for host arrays; the kernels do not bound-check gathers."""
+    u = np.asarray(users)
+    i = np.asarray(items)
+    if u.size and (int(u.min()) < 0 or int(u.max()) >= user_num):
+        raise IndexError("index out of range in self (user id)")
+    if i.size and (int(i.min()) < 0 or int(i.max()) >= item_num):
+        raise IndexError("index out of range in self (item id)")
+
+
+def check_rows(rows, user_num, item_num):
+    """Range check of a packed device stream (padding rows, user -1, allowed): a
+    few reductions on the device and one host read."""
+    if rows.numel() == 0:
+        return
+    u = (rows & 0xFFFFFFFF).to(torch.int64)
+    it = (rows >> 32) & 0x7FFFFFFF
+    pad = u == 0xFFFFFFFF
+    bad_u = ((u >= user_num) & ~pad).any()
+    bad_i = ((it >= item_num) & ~pad).any()
+    bu, bi = torch.stack([bad_u, bad_i]).tolist()
+    if bu:
+        raise IndexError("index out of range in self (user id)")
+    if bi:
+        raise IndexError("index out of range in self (item id)")
+
+
 def pack_rows_host(users, items, labels=None):
     """Host-side NCF_ROW_PACK of numpy arrays -> int64 numpy array."""
     r = np.asarray(users).astype(np.int64) & 0xFFFFFFFF
@@ -163,8 +191,6 @@ def fused_backward(flat, lay, rows, dlogit, gflat, ws, ctl):
     L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
                                    dlogit.data_ptr(), ctl.data_ptr(), int(n), 1, 0, L.DZ_DLOGIT,
                                    ws.data_ptr(), ws.numel() * 4, None, st), "ncf_train_step")
-    L.check(L.hip().ncf_expand_grads(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), ws.data_ptr(), st),
-            "ncf_expand_grads")
     L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), ws.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st),
             "ncf_reduce_slab")
 

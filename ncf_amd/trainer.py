@@ -21,6 +21,7 @@ all-reduces gradients over RCCL; evaluation and checkpoints are rank 0's.
 """
 from __future__ import annotations
 
+import os
 import time
 
 import numpy as np
@@ -60,13 +61,27 @@ class Trainer:
         self._test = None
         self.test_batch = test_batch
         self.history = []
+        self._pipe = None
 
     # ------------------------------------------------------------------ data
     def _epoch_stream(self):
-        """ng_sample + DataLoader order for one epoch -> device stream in batch order."""
+        """ng_sample + DataLoader order for one epoch -> device stream in batch order.
+        Default: the epoch pipeline (ncf_amd.pipeline: the next epoch's negatives and
+        permutation words drawn on host threads while this one trains, the
+        permutation and rows built on the device); NCF_HOST_EPOCH=1: sampler, torch
+        randperm, packing and upload in line (the round-1 path, for comparison)."""
+        if os.environ.get("NCF_HOST_EPOCH", "0") != "1":
+            if self._pipe is None:
+                from .pipeline import EpochPipeline
+                self._pipe = EpochPipeline(self.ds, self.device, self.batch_size, int(self.model.item_num),
+                                                 user_num=int(self.model.user_num))
+            # fit() evaluates after every epoch (one torch draw): the next epoch's
+            # sampler seed is peeked past it
+            return self._pipe.next_epoch(peek_eval_draw=True)
         self.ds.ng_sample()
         u, i, y = self.ds.arrays()
         n = len(u)
+        ops.check_ids(u, i, int(self.model.user_num), int(self.model.item_num))
         perm = epoch_permutation(n).to(self.device)
         if getattr(self, "_rows", None) is None or self._rows.numel() != n:
             self._rows = torch.empty(n, dtype=torch.int64, device=self.device)
@@ -104,7 +119,7 @@ class Trainer:
 
     def train_epoch(self):
         rows = self._epoch_stream()
-        self.engine.set_epoch_stream(rows, self.batch_size)
+        self.engine.set_epoch_stream(rows, self.batch_size, checked=True)  # ids checked on the host
         self.engine.run(self.engine.num_batches, use_graph=self.use_graph)
         return float(np.mean(self.engine.epoch_losses()))
 

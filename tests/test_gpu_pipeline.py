@@ -1,0 +1,133 @@
+"""Epoch pipeline (ncf_amd.pipeline; include/ncf_hip.h ncf_randperm,
+ncf_build_rows) -- bit-exact against the host path that the reference's own
+outputs pin (test_host.py / test_oracle.py, G1 and G2):
+
+  * the permutation == torch.randperm(n, generator) (DataLoader(shuffle=True),
+    train_neumf.py:55), including n = 1, 2 and the ml-1m / ml-20m sizes;
+  * whole epochs (with the prefetch threads) == ng_sample + epoch_permutation +
+    rows[perm] of the host path, batch by batch, and both generators end in the
+    same state; a prefetch invalidated by an unexpected draw is discarded.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _dataset(pu, pi, num_item, ng):
+    from ncf_amd.data import NCFData
+    return NCFData(np.stack([pu, pi], 1), num_item, None, ng, True)
+
+
+@pytest.mark.parametrize("n,seed", [(1, 0), (2, 3), (1000, 7), (65537, 2**40 + 5), (4970845, 123),
+                                    (99308850, 9)])
+def test_randperm_matches_torch(n, seed):
+    import ncf_amd._lib as L
+    from ncf_amd.pipeline import torch_words
+    g = torch.Generator()
+    g.manual_seed(seed)
+    exp = torch.randperm(n, generator=g)
+    w = np.empty(max(1, n - 1), dtype=np.uint32)
+    torch_words(seed, n - 1, w)
+    words = torch.from_numpy(w.view(np.int32)).to(DEV)
+    perm = torch.empty(n, dtype=torch.int64, device=DEV)
+    ws = torch.empty(int(L.hip().ncf_randperm_workspace(n)), dtype=torch.uint8, device=DEV)
+    rem = torch.zeros(1, dtype=torch.int32, device=DEV)
+    # rounds = 2 leaves most swaps to the in-order tail (or reports them); the
+    # default schedule (2.5 log2 n + 16) finishes in the parallel rounds
+    for rounds in ([2] if n <= 4096 else []) + [int(2.5 * np.log2(max(2, n))) + 16]:
+        L.check(L.hip().ncf_randperm(words.data_ptr(), n, perm.data_ptr(), rounds, ws.data_ptr(), ws.numel(),
+                                     rem.data_ptr(), L.stream_ptr()), "ncf_randperm")
+        assert int(rem.item()) == 0
+        assert torch.equal(perm.cpu(), exp)
+
+
+def test_randperm_reports_unfinished_tail():
+    import ncf_amd._lib as L
+    from ncf_amd.pipeline import torch_words
+    n = 200000
+    w = np.empty(n - 1, dtype=np.uint32)
+    torch_words(1, n - 1, w)
+    words = torch.from_numpy(w.view(np.int32)).to(DEV)
+    perm = torch.empty(n, dtype=torch.int64, device=DEV)
+    ws = torch.empty(int(L.hip().ncf_randperm_workspace(n)), dtype=torch.uint8, device=DEV)
+    rem = torch.zeros(1, dtype=torch.int32, device=DEV)
+    L.check(L.hip().ncf_randperm(words.data_ptr(), n, perm.data_ptr(), 1, ws.data_ptr(), ws.numel(),
+                                 rem.data_ptr(), L.stream_ptr()), "ncf_randperm")
+    assert int(rem.item()) > 4096  # one round leaves ~2/3 of the swaps: reported, not silently dropped
+
+
+def test_pipeline_epochs_equal_host_path():
+    """Three epochs with prefetch and an eval draw between them, vs the host path."""
+    from ncf_amd import ops
+    from ncf_amd.data import consume_test_pass, epoch_permutation
+    from ncf_amd.pipeline import EpochPipeline
+    from ncf_amd import synthetic
+    d = synthetic.make_dataset("ml-100k", seed=1)
+    pu, pi, I, U, B = d["train_users"], d["train_items"], d["item_num"], d["user_num"], 4096
+    np.random.seed(3)
+    torch.manual_seed(3)
+    ds = _dataset(pu, pi, I, 4)
+    exp = []
+    for _ in range(3):
+        ds.ng_sample()
+        u, i, y = ds.arrays()
+        perm = epoch_permutation(len(u)).numpy()
+        exp.append(ops.pack_rows_host(u, i, y)[perm])
+        consume_test_pass()
+    np_exp, t_exp = np.random.get_state(), torch.get_rng_state()
+    np.random.seed(3)
+    torch.manual_seed(3)
+    ds2 = _dataset(pu, pi, I, 4)
+    pipe = EpochPipeline(ds2, DEV, B, I, user_num=U)
+    for e in range(3):
+        got = pipe.next_epoch(peek_eval_draw=True).cpu().numpy()
+        for b0 in range(0, len(got), B):
+            assert np.array_equal(np.sort(got[b0:b0 + B]), np.sort(exp[e][b0:b0 + B])), (e, b0)
+        consume_test_pass()
+    pipe.close()
+    assert pipe.stats["prefetch_hits"] == 2
+    u2, i2, _ = ds2.arrays()  # host views of the device negatives
+    assert np.array_equal(ops.pack_rows_host(u2, i2, ds2.arrays()[2]), ops.pack_rows_host(*ds.arrays()))
+    st = np.random.get_state()
+    assert np.array_equal(st[1], np_exp[1]) and st[2] == np_exp[2]
+    assert torch.equal(torch.get_rng_state(), t_exp)
+
+
+def test_pipeline_discards_prefetch_after_foreign_draws():
+    """Another consumer of either generator between epochs: the prefetched epoch
+    is rebuilt from the real state, and the result still equals the host path."""
+    from ncf_amd import ops
+    from ncf_amd.data import epoch_permutation
+    from ncf_amd.pipeline import EpochPipeline
+    rng = np.random.default_rng(2)
+    pu = np.repeat(np.arange(300, dtype=np.int32), 30)
+    pi = rng.integers(0, 500, len(pu)).astype(np.int32)
+    B = 1000
+    np.random.seed(4)
+    torch.manual_seed(4)
+    ds = _dataset(pu, pi, 500, 4)
+    exp = []
+    for e in range(3):
+        ds.ng_sample()
+        u, i, y = ds.arrays()
+        exp.append(ops.pack_rows_host(u, i, y)[epoch_permutation(len(u)).numpy()])
+        if e == 0:
+            np.random.randint(7)      # a foreign NumPy draw
+        if e == 1:
+            torch.rand(3)             # a foreign torch draw
+    np.random.seed(4)
+    torch.manual_seed(4)
+    ds2 = _dataset(pu, pi, 500, 4)
+    pipe = EpochPipeline(ds2, DEV, B, 500, user_num=300)
+    for e in range(3):
+        got = pipe.next_epoch(peek_eval_draw=False).cpu().numpy()
+        assert np.array_equal(got, exp[e]), e  # B < 4096: shuffled, not grouped
+        if e == 0:
+            np.random.randint(7)
+        if e == 1:
+            torch.rand(3)
+    pipe.close()
+    assert pipe.stats["prefetch_hits"] == 0

@@ -175,3 +175,30 @@ def test_cpu_module_semantics_match_golden(golden):
     m = NCF(50, 80, 16, 3, 0.0, "NeuMF-end")
     p = m(torch.from_numpy(g["users"]), torch.from_numpy(g["items"]))
     np.testing.assert_allclose(p.detach().numpy(), g["NeuMF-end_f16_L3_logits"], rtol=1e-6, atol=1e-7)
+
+
+def test_pipelined_sampler_many_blocks_matches_oracle():
+    """ml-1m-sized pass (~4.3M words: the generator thread's block ring wraps many
+    times) vs the oracle's C restatement, twice in a row on the global stream."""
+    from ncf_amd.data import NCFData
+    from oracle import ncf_oracle as O
+    rng = np.random.default_rng(8)
+    U, I = 6041, 3707
+    counts = rng.integers(1, 330, U)
+    pu = np.repeat(np.arange(U), counts)
+    pi = rng.integers(0, I, len(pu))
+    np.random.seed(21)
+    d = NCFData(np.stack([pu, pi], 1), I, None, 4, True)
+    d.ng_sample()
+    first = d._ng_i.copy()
+    d.ng_sample()
+    after = np.random.randint(1 << 30, size=4)
+    exp = O.ng_sample(pu, pi, I, 4, 21)
+    assert np.array_equal(first, exp)
+    # the second pass continues the stream: replay both on numpy's own generator state
+    np.random.seed(21)
+    from ncf_amd.data import HostSampler
+    s = HostSampler(pu, pi, U, I)
+    s.sample(I, 4)
+    assert np.array_equal(s.sample(I, 4), d._ng_i)
+    assert np.array_equal(np.random.randint(1 << 30, size=4), after)
