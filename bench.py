@@ -4,15 +4,23 @@
 Workload (BASELINE.json metric "training interactions/sec + HR@10, NeuMF
 factors=64 ml-1m"): NCF(6041, 3707, factor_num=16,
 num_layers=3, 'NeuMF-end') -- 64-wide MLP embeddings, tower [128,64,32,16] --
-on ml-1m-shaped synthetic data (994,169 positives, 4 sampled negatives each,
-bit-exact reference sampler), 65,536 rows per GPU per step, Adam lr 1e-3.
+on ml-1m-shaped synthetic data (994,169 positives, 4 sampled negatives each),
+65,536 rows per GPU per step, Adam lr 1e-3.
 
-A "step" = fused fwd+loss+bwd kernel, tower-grad reduction, (RCCL all-reduce
-of the gradient bucket when N > 1), dense Adam -- the whole optimizer step of
-scripts/train_neumf.py:111-115, captured once into a hipGraph and replayed.
-The epoch stream (users/items/labels, already shuffled) is resident in HBM
-before the timed region.  Per-GPU work is fixed (65,536 rows/GPU/step), so
-scaling is weak and value = all ranks' rows / max-over-ranks time.
+A "step" = fused fwd+loss+bwd kernel (+ the factored layer-0 expansion), tower-grad
+reduction, (RCCL gradient exchange when N > 1), dense Adam -- the whole optimizer
+step of scripts/train_neumf.py:111-115, captured into hipGraphs and replayed.
+Every epoch inside the timed region is a fresh epoch of the reference loop: new
+negatives (NCFData.ng_sample, bit-exact; host sampler, prefetched on a host thread
+while the previous epoch trains) and a new DataLoader permutation (bit-exact
+torch.randperm, on the device), packed, shuffled and grouped on the device
+(ncf_amd.pipeline).  The data set itself is resident in HBM before the timed
+region.  Per-GPU work is fixed (65,536 rows/GPU/step), so scaling is weak and
+value = all ranks' rows / max-over-ranks time.
+
+Also reported: `e2e` -- Trainer.fit (the scripts' loop: epochs + metrics() per
+epoch) at the same config, rows per epoch / epoch wall time; `cpu_baseline` -- the
+oracle (reference model restated on torch CPU ops) on the host cores.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one process per GPU, RCCL).
@@ -20,9 +28,9 @@ torch.distributed.run (one process per GPU, RCCL).
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
-import platform
 import sys
 import time
 
@@ -59,32 +67,48 @@ def gather_scatter_bytes_per_row(f, L):
     return 8 + rows + rows
 
 
-def adam_info(kt, P, adam_bytes, eng):
-    """Optimizer launch and its bytes: dense Adam is 32 B/param (read p, g, m, v;
-    write p, m, v, g = 0); the fused reduce+Adam also reads the partial slab."""
+def adam_info(kt, eng, model):
+    """The optimizer launch and the bytes it moves.  Dense Adam over the embedding
+    tables: 32 B/param (read p, g, m, v; write p, m, v, g = 0).  ncf_reduce_adam_step
+    also reads the per-workgroup tower slab (fused path: ncf_slab_rows rows; layered:
+    one row) and, on the factored path, the expansion's dW0 partials, and runs Adam
+    on the tower straight from those sums (24 B/param: read p, m, v; write p, m, v)."""
+    import ncf_amd._lib as L
+    from ncf_amd import ops
+    lay = eng.lay
+    lib = L.hip()
+    emb = sum(p.numel() for p, act in zip(list(model.ordered_params())[:4], ops.active_mask(model)[:4]) if act)
+    tower = sum(p.numel() for p in list(model.ordered_params())[4:])
+    stride = int(lib.ncf_slab_stride(L.ctypes.byref(lay)))
+    fused = L.supported(model.model_type, model.factor_num, model.num_layers) == L.PATH_FUSED
+    slab_rows = int(lib.ncf_slab_rows()) if fused else 1
+    partial = 0
+    if ops.fact_mode(lay):
+        partial = int(lib.ncf_workspace_bytes(L.ctypes.byref(lay), 1)) - int(lib.ncf_slab_rows()) * stride * 4
     if "ncf_reduce_adam_step" in kt:
-        slab_bytes = int(eng.ws.numel()) * 4
+        b = 32 * emb + 24 * tower + slab_rows * stride * 4 + partial
         ms = kt["ncf_reduce_adam_step"]
-        return {"kernel": "ncf_reduce_adam_step (slab reduce + Adam)", "params": P,
-                "bytes": adam_bytes + slab_bytes, "ms": ms, "GB/s": (adam_bytes + slab_bytes) / (ms * 1e-3) / 1e9}
+        return {"kernel": "ncf_reduce_adam_step (slab reduce + Adam)", "params": emb + tower, "bytes": b,
+                "bytes_detail": {"embedding_adam": 32 * emb, "tower_adam": 24 * tower,
+                                 "slab_read": slab_rows * stride * 4, "w0_partials_read": partial},
+                "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}
+    b = 32 * (emb + tower)
     ms = kt["optimizer"]
-    return {"kernel": "ncf_adam_step", "params": P, "bytes": adam_bytes, "ms": ms,
-            "GB/s": adam_bytes / (ms * 1e-3) / 1e9}
+    return {"kernel": "ncf_adam_step", "params": emb + tower, "bytes": b, "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}
 
 
-def pmc_traffic(f, L):
-    """HBM bytes per launch of the fused step kernel from the newest committed
-    rocprofv3 PMC summary (profiles/r*_prof_summary.json, written by
+def pmc_traffic(config, names):
+    """HBM bytes per launch of `names` from the newest committed rocprofv3 PMC summary
+    of THIS config (profiles/r*_prof_summary.json with "config" == config, written by
     scripts/profile.sh + scripts/prof_summary.py from separate FETCH_SIZE and
-    WRITE_SIZE passes of this bench: bytes = (2 * FETCH_SIZE + WRITE_SIZE) KB * 1024,
-    the gfx950 correction of the MI355X guide).  (None, None) if absent."""
-    import glob
-    dm = f * 2 ** (L - 1)
-    names = (f"ncf::ncf_step_kernel<{f}, {L}, 2, false, true>", f"ncf::fact_expand_kernel<{dm}>")
+    WRITE_SIZE passes: bytes = (2 * FETCH_SIZE + WRITE_SIZE) KB * 1024, the gfx950
+    correction of the MI355X guide).  (None, None) if there is none."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_prof_summary.json")), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
+            continue
+        if d.get("config") != config:
             continue
         got = {k.get("kernel"): k.get("hbm_bytes_corrected") for k in d.get("kernels", [])}
         if all(got.get(n) for n in names):
@@ -92,80 +116,144 @@ def pmc_traffic(f, L):
     return None, None
 
 
-def cpu_baseline(f, L, U, I, batch, seconds, threads):
+def host_facts():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return {"nproc": os.cpu_count(), "cpus_available": avail, "cpu_model": model}
+
+
+def cpu_baseline(cfg, ds, batch, seconds, threads):
     """The oracle (oracle/ncf_oracle.py: the reference model restated on stock
-    PyTorch CPU ops + torch.optim.Adam) timed on a bounded sample of the same
-    workload: full 65,536-row steps on random ids of the same id space."""
+    PyTorch CPU ops + torch.optim.Adam) timed on the host cores: (i) steady-state
+    Adam steps on `batch`-row batches of the real epoch stream for ~`seconds`, and
+    (ii) a script-equivalent epoch -- ng_sample (the oracle's C restatement),
+    the DataLoader permutation, packing, then every step of the epoch -- timed on
+    the first batches and extrapolated to the epoch's batch count."""
     from oracle import ncf_oracle as O
+    shape, f, L, _ = CONFIGS[cfg]
+    U, I = ds["user_num"], ds["item_num"]
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     m = O.OracleNCF(U, I, f, L, 0.0, "NeuMF-end")
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
-    rng = np.random.default_rng(0)
-    mk = lambda: (torch.from_numpy(rng.integers(0, U, batch)), torch.from_numpy(rng.integers(0, I, batch)),
-                  torch.from_numpy((rng.random(batch) < 0.2).astype(np.int64)))
-    u, i, y = mk()
-    O.train_steps(m, opt, [u], [i], [y])  # warm-up
+    pu, pi = ds["train_users"], ds["train_items"]
+    t0 = time.perf_counter()
+    neg = O.ng_sample(pu, pi, I, 4, 0)
+    t_sample = time.perf_counter() - t0
+    users = np.concatenate([pu, np.repeat(pu, 4)])
+    items = np.concatenate([pi, neg])
+    labels = np.concatenate([np.ones(len(pu), np.int64), np.zeros(len(neg), np.int64)])
+    t0 = time.perf_counter()
+    perm = O.epoch_order(len(users), torch.Generator().manual_seed(0))
+    t_perm = time.perf_counter() - t0
+    nb = (len(users) + batch - 1) // batch
+    bat = lambda b: (users[perm[b * batch:(b + 1) * batch]], items[perm[b * batch:(b + 1) * batch]],  # noqa: E731
+                     labels[perm[b * batch:(b + 1) * batch]])
+    O.train_steps(m, opt, *[[x] for x in bat(0)])  # warm-up
     steps, t0 = 0, time.perf_counter()
     while True:
+        u, i, y = bat(1 + steps % (nb - 1)) if nb > 1 else bat(0)
         O.train_steps(m, opt, [u], [i], [y])
         steps += 1
         el = time.perf_counter() - t0
         if el >= seconds:
             break
+    step_s = el / steps
+    epoch_s = t_sample + t_perm + nb * step_s
     return {"value": steps * batch / el, "unit": "interactions/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} x {batch}-row Adam steps of the oracle (reference NCF restated on torch CPU "
-                      f"ops), NCF({U},{I},{f},{L}), {el:.1f} s on {threads} threads "
-                      f"({platform.processor() or platform.machine()})"}
+            "sample": f"{steps} x {batch}-row Adam steps of the oracle on the epoch stream of {cfg.upper()} "
+                      f"(reference NCF restated on torch CPU ops, NCF({U},{I},{f},{L})), {el:.1f} s on "
+                      f"{threads} threads",
+            "script_epoch_s": epoch_s,
+            "script_epoch_note": f"ng_sample {t_sample:.2f} s + DataLoader permutation {t_perm:.2f} s + "
+                                 f"{nb} steps x {step_s * 1e3:.1f} ms (steps timed on {steps}, extrapolated)",
+            "script_epoch_interactions_per_s": len(users) / epoch_s,
+            **host_facts(), "torch_threads": threads}
 
 
-def setup_engine(config, world, rank, dev, group, global_batch, seed=0):
-    """Synthetic dataset -> bit-exact negatives -> shuffled epoch stream in HBM
-    -> NCF + TrainEngine.  Identical on every rank (seeded)."""
+def make_train_data(cfg, seed=0):
     from ncf_amd import synthetic
-    from ncf_amd.data import HostSampler, epoch_permutation
+    from ncf_amd.data import NCFData
+    shape = CONFIGS[cfg][0]
+    ds = synthetic.make_dataset(shape, seed=seed)
+    train = NCFData(np.stack([ds["train_users"], ds["train_items"]], 1), ds["item_num"], None, 4, True)
+    return ds, train
+
+
+def setup_engine(cfg, ds, train, world, rank, dev, group, global_batch, seed=0):
+    """Bit-exact epoch pipeline over the resident data set -> NCF + TrainEngine.
+    Identical on every rank (seeded)."""
     from ncf_amd.engine import TrainEngine
     from ncf_amd.models import NCF
-    from ncf_amd import ops
-    shape, f, nl, _ = CONFIGS[config]
-    ds = synthetic.make_dataset(shape, seed=seed)
+    from ncf_amd.pipeline import EpochPipeline
+    shape, f, nl, _ = CONFIGS[cfg]
     U, I = ds["user_num"], ds["item_num"]
     np.random.seed(seed)
     torch.manual_seed(seed)
-    sampler = HostSampler(ds["train_users"], ds["train_items"], U, I)
-    t_s = time.perf_counter()
-    neg = sampler.sample(I, 4)
-    t_sample = time.perf_counter() - t_s
-    pu, pi = ds["train_users"], ds["train_items"]
-    users = np.concatenate([pu, np.repeat(pu, 4)]).astype(np.int32)
-    items = np.concatenate([pi, neg]).astype(np.int32)
-    labels = np.concatenate([np.ones(len(pu), np.float32), np.zeros(len(neg), np.float32)])
     model = NCF(U, I, f, nl, 0.0, "NeuMF-end").to(dev)
-    perm = epoch_permutation(len(users)).to(dev)
-    rows_d = torch.from_numpy(ops.pack_rows_host(users, items, labels)).to(dev)  # resident in HBM
-    prep = ops.EpochPrep(dev)
-    stream = prep(rows_d, perm, global_batch, I)
+    pipe = EpochPipeline(train, dev, global_batch, I, user_num=U, prefetch=True)
     eng = TrainEngine(model, lr=1e-3, world_size=world, rank=rank, process_group=group)
-    eng.set_epoch_stream(stream, global_batch)
+    eng.set_epoch_stream(pipe.next_epoch(peek_eval_draw=False), global_batch, checked=True)
 
-    def prepare():  # per-epoch device work: shuffle + group each batch by item (same output buffer)
-        prep(rows_d, perm, global_batch, I)
-    eng.prepare_epoch = prepare
-    return eng, model, ds, t_sample
+    def next_epoch():  # fresh negatives + permutation (no metrics() pass between bench epochs)
+        eng.set_epoch_stream(pipe.next_epoch(peek_eval_draw=False), global_batch, checked=True)
+    eng.next_epoch = next_epoch
+    return eng, model, pipe
 
 
 def run_steps(eng, n_steps, use_graph):
-    """n_steps optimizer steps; the per-epoch device preparation (ncf_prepare_epoch)
-    runs at every epoch boundary inside the timed region."""
+    """n_steps optimizer steps; a new epoch (fresh negatives and permutation)
+    starts at every epoch boundary inside the timed region."""
     done = 0
     while done < n_steps:
         pos = eng.batches_done % eng.num_batches
         if pos == 0 and eng.batches_done > 0:
-            eng.prepare_epoch()
+            eng.next_epoch()
         k = min(n_steps - done, eng.num_batches - pos)
         eng.run(k, use_graph=use_graph)
         eng.batches_done += k
         done += k
+
+
+def e2e_fit(cfg, ds, dev, epochs):
+    """Trainer.fit -- the loop scripts/train_neumf.py runs (per epoch: ng_sample,
+    DataLoader order, the steps, metrics() over the leave-one-out test set) --
+    at this config on a fresh model; epoch wall times as the scripts print them."""
+    from torch.utils.data import DataLoader
+    from ncf_amd.data import NCFData
+    from ncf_amd.models import NCF
+    from ncf_amd.trainer import Trainer
+    shape, f, nl, per_gpu = CONFIGS[cfg]
+    U, I = ds["user_num"], ds["item_num"]
+    np.random.seed(1)
+    torch.manual_seed(1)
+    model = NCF(U, I, f, nl, 0.0, "NeuMF-end").to(dev)
+    train = NCFData(np.stack([ds["train_users"], ds["train_items"]], 1), I, None, 4, True)
+    tu = np.repeat(ds["test_users"], 100)
+    ti = np.concatenate([ds["test_items"][:, None], ds["test_negatives"]], 1).reshape(-1)
+    test = NCFData(np.stack([tu, ti], 1), I, None, 0, False)
+    tr = Trainer(model, train, DataLoader(test, batch_size=100, shuffle=False), batch_size=per_gpu, lr=1e-3,
+                 top_k=10, device=dev, verbose=False)
+    tr.fit(epochs)
+    times = [h["time"] for h in tr.history]
+    steady = times[1:] if len(times) > 1 else times
+    n = len(train)
+    return {"value": n / (sum(steady) / len(steady)), "unit": "interactions/s",
+            "epoch_s": times, "rows_per_epoch": n, "epochs": epochs,
+            "HR@10": [round(h["hr"], 4) for h in tr.history],
+            "note": "Trainer.fit epochs (steps + per-epoch sampling/permutation + metrics() pass), "
+                    "first epoch (graph capture) excluded from the mean",
+            "prefetch_hits": tr._pipe.stats["prefetch_hits"] if tr._pipe is not None else None}
 
 
 def main():
@@ -179,6 +267,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--skip-cpu-baseline", action="store_true")
     ap.add_argument("--skip-eval", action="store_true")
+    ap.add_argument("--e2e-epochs", type=int, default=4, help="Trainer.fit epochs for the e2e figure (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -199,8 +288,9 @@ def main():
     shape, f, nl, per_gpu = CONFIGS[args.config]
     global_batch = per_gpu * world
     t_data = time.perf_counter()
-    eng, model, ds, t_sample = setup_engine(args.config, world, rank, dev, group, global_batch)
+    ds, train = make_train_data(args.config)
     U, I = ds["user_num"], ds["item_num"]
+    eng, model, pipe = setup_engine(args.config, ds, train, world, rank, dev, group, global_batch)
     torch.cuda.synchronize(dev)
     t_data = time.perf_counter() - t_data
 
@@ -214,15 +304,18 @@ def main():
     if world > 1:
         torch.distributed.barrier(group=group, device_ids=[local])
     torch.cuda.synchronize(dev)
+    epochs0 = pipe.stats["epochs"]
     t0 = time.perf_counter()
     run_steps(eng, args.steps, use_graph)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    epochs_in_timed = pipe.stats["epochs"] - epochs0
     if world > 1:
         torch.distributed.barrier(group=group, device_ids=[local])
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=group)
         dt = float(t.item())
+    pipe.check()
     rows = args.steps * global_batch
     value = rows / dt
     losses = eng.epoch_losses()
@@ -230,25 +323,38 @@ def main():
 
     # ---- per-kernel live timing (HIP events on the launch stream) -------------
     kt = eng.time_kernels(args.kernel_steps)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(5):
-        eng.prepare_epoch()
-    e1.record()
-    torch.cuda.synchronize(dev)
-    kt["prepare_epoch_per_epoch"] = e0.elapsed_time(e1) / 5
+    pipe_ms = []
+    for _ in range(3):  # the epoch pipeline's device part: rows + randperm (side stream), grouping
+        eng.next_epoch()
+        eng.run(eng.num_batches, use_graph=use_graph)
+        pipe_ms.append(pipe.device_ms())
+    kt["epoch_rows_randperm_side_stream"] = float(np.mean([x[0] for x in pipe_ms]))
+    hm = pipe.stats.get("host_ms", [])[-3:]
+    kt["epoch_host_ms"] = {k: float(np.mean([h[k] for h in hm if k in h])) for k in ("sample", "words", "stage")
+                           if any(k in h for h in hm)}
     kt["ncf_train_step_per_launch_b2b"] = eng.time_train_kernel(50)
+    from ncf_amd import ops
+    import ncf_amd._lib as L
+    fact = ops.fact_mode(eng.lay)
+    path = L.supported("NeuMF-end", f, nl)
+    dm = f * 2 ** (nl - 1)
     rows_per_launch = per_gpu
     flops = tower_flops_per_row(f, nl) * rows_per_launch
     ms = kt["ncf_train_step_per_launch_b2b"]
     achieved_tf = flops / (ms * 1e-3) / 1e12
     bytes_launch = gather_scatter_bytes_per_row(f, nl) * rows_per_launch
     achieved_gbs = bytes_launch / (ms * 1e-3) / 1e9
-    P = sum(p.numel() for p in model.parameters())
-    adam_bytes = 32 * P  # read p,g,m,v; write p,m,v,g(=0)
-    traffic, traffic_src = pmc_traffic(f, nl)
-    import ncf_amd._lib as L
-    path = L.supported("NeuMF-end", f, nl)
+    if path == L.PATH_FUSED:
+        names = [f"ncf::ncf_step_kernel<{f}, {nl}, 2, false, {'true' if fact else 'false'}>"]
+        if fact:
+            names.append(f"ncf::fact_expand_kernel<{dm}>")
+        kname = (f"ncf_step_kernel<{f},{nl},NeuMF,FACT={str(fact).lower()}>"
+                 + (f" + fact_expand_kernel<{dm}> (factored layer 0)" if fact else " (per-row layer 0)")
+                 + "; launch group timed back to back")
+        traffic, traffic_src = pmc_traffic(args.config, names)
+    else:
+        names, traffic, traffic_src = [], None, None
+        kname = "layered path: all kernels of ncf_train_step (fwd/predict/bwd GEMMs)"
 
     # ---- quality: HR@10 / NDCG@10 on the leave-one-out test set ---------------
     hr10 = ndcg10 = None
@@ -258,12 +364,16 @@ def main():
         ti = np.concatenate([ds["test_items"][:, None], ds["test_negatives"]], 1).reshape(-1)
         HR, NDCG = evaluate_arrays(model, tu, ti, 100, 10)
         hr10, ndcg10 = float(np.mean(HR)), float(np.mean(NDCG))
+    pipe.close()
 
     out = None
     if rank == 0:
+        e2e = None
+        if args.e2e_epochs > 0 and world == 1:
+            e2e = e2e_fit(args.config, ds, dev, args.e2e_epochs)
         cpu = None
         if not args.skip_cpu_baseline and world == 1:
-            cpu = cpu_baseline(f, nl, U, I, per_gpu, args.cpu_seconds, threads=min(16, os.cpu_count() or 1))
+            cpu = cpu_baseline(args.config, ds, per_gpu, args.cpu_seconds, threads=min(16, host_facts()["cpus_available"]))
         out = {
             "metric": "training interactions/sec + HR@10, NeuMF factors=64 ml-1m, 1/2/4/8 MI355X",
             "value": value,
@@ -276,8 +386,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic ml-1m-shaped (6,040 users x 3,706 items, 994,169 train positives, "
-                    "4 bit-exact sampled negatives each; seed 0)",
+            "data": (f"synthetic {shape}-shaped ({U - 1:,} users x {I - 1:,} items, {len(ds['train_users']):,} "
+                     f"train positives, 4 bit-exact sampled negatives each, fresh negatives and permutation "
+                     f"every epoch: {epochs_in_timed} epoch boundaries in the timed region; seed 0)"),
             "config": {"workload": f"{args.config.upper()}: NCF(user_num={U}, item_num={I}, factor_num={f}, "
                                    f"num_layers={nl}, NeuMF-end), Adam lr 1e-3",
                        "global_batch": global_batch, "per_gpu_batch": per_gpu, "parallelism": f"dp{world}",
@@ -285,20 +396,18 @@ def main():
                        "dp_exchange": eng.dp_mode, "hip_graph": use_graph},
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": 157.3, "unit": "TFLOP/s",
                          "frac": achieved_tf / 157.3, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": (f"ncf_step_kernel<{f},{nl},NeuMF,FACT> + fact_expand_kernel<{f * 2 ** (nl - 1)}> "
-                                    "(fused fwd+bwd, factored layer 0; launch group timed back to back)"
-                                    if path == 1 else
-                                    "layered path: all kernels of ncf_train_step (fwd/predict/bwd GEMMs)"),
-                         "flops_per_launch": flops, "kernel_ms": ms},
+                         "kernel": kname, "flops_per_launch": flops, "kernel_ms": ms},
             "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": 8000.0, "unit": "GB/s",
                              "frac": achieved_gbs / 8000.0, "bytes_per_launch": bytes_launch,
-                             "note": "gather+scatter algorithmic bytes of the same fused kernel"},
+                             "note": ("gather+scatter algorithmic bytes of the same launch group" if path == L.PATH_FUSED
+                                      else "gather+scatter algorithmic bytes over all layered-path kernels")},
             "kernel_ms": kt,
-            "adam": adam_info(kt, P, adam_bytes, eng),
+            "adam": adam_info(kt, eng, model),
             "quality": {"HR@10": hr10, "NDCG@10": ndcg10, "epochs_trained": round(eng.state_step() / eng.num_batches, 2),
                         "last_batch_loss": final_loss},
+            "e2e": e2e,
             "cpu_baseline": cpu,
-            "setup_s": {"data+upload": round(t_data, 2), "ng_sample_cpp": round(t_sample, 3)},
+            "setup_s": {"data+first_epoch": round(t_data, 2)},
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -44,17 +44,81 @@ __global__ __launch_bounds__(EP_THREADS) void fill_u64_kernel(unsigned long long
 }
 
 // ---------------------------------------------------------------------------
-// Fisher-Yates rounds.
+// Fisher-Yates rounds.  The first FY_FLAG_ROUNDS rounds walk every index with a
+// pending flag (most swaps are pending: an appended list would put one
+// same-address atomic per wave on the critical path -- 0.9 ms in round 1 at
+// n = 5M); then the ~1% still pending are compacted once (one atomic per block)
+// and the remaining rounds walk that list.
+constexpr int FY_FLAG_ROUNDS = 13;  // 0.7^13 ~ 1% pending
 __global__ __launch_bounds__(EP_THREADS) void fy_init_kernel(const uint32_t* __restrict__ words, int64_t n, int32_t* H,
-                                                             int64_t* A, int32_t* list, int* count) {
+                                                             int64_t* A, uint8_t* done) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         A[i] = i;
-        if (i < n - 1) {
-            H[i] = (int32_t)(i + (int64_t)(words[i] % (uint32_t)(n - i)));  // generator->random() % (n - i)
-            list[i] = (int32_t)i;
+        if (i < n - 1) H[i] = (int32_t)(i + (int64_t)(words[i] % (uint32_t)(n - i)));  // generator->random() % (n - i)
+        else H[i] = (int32_t)i;
+        done[i] = i >= n - 1;
+    }
+}
+
+__global__ __launch_bounds__(EP_THREADS) void fy_reserve_flags_kernel(const uint8_t* __restrict__ done, int64_t n,
+                                                                      const int32_t* __restrict__ H,
+                                                                      unsigned long long* R, uint32_t tag) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (done[i]) continue;
+        const unsigned long long key = ((unsigned long long)tag << 32) | (uint32_t)i;
+        atomicMin(R + i, key);
+        const int h = H[i];
+        if (h != i) atomicMin(R + h, key);
+    }
+}
+
+__global__ __launch_bounds__(EP_THREADS) void fy_commit_flags_kernel(uint8_t* done, int64_t n,
+                                                                     const int32_t* __restrict__ H,
+                                                                     const unsigned long long* R, uint32_t tag,
+                                                                     int64_t* A) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (done[i]) continue;
+        const unsigned long long key = ((unsigned long long)tag << 32) | (uint32_t)i;
+        const int h = H[i];
+        if (R[i] == key && R[h] == key) {
+            const int64_t x = A[i];
+            A[i] = A[h];
+            A[h] = x;
+            done[i] = 1;
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) *count = (int)(n - 1);
+}
+
+// Pending indices -> list (order irrelevant), one atomic per block.
+constexpr int FY_CPT = 16;  // indices per thread
+__global__ __launch_bounds__(EP_THREADS) void fy_compact_kernel(const uint8_t* __restrict__ done, int64_t n,
+                                                                int32_t* list, int* count) {
+    __shared__ int wsum[EP_THREADS / 64];
+    __shared__ int base;
+    const int64_t i0 = ((int64_t)blockIdx.x * EP_THREADS + threadIdx.x) * FY_CPT;
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < FY_CPT; ++k) c += (i0 + k < n && !done[i0 + k]);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int q = 0; q < EP_THREADS / 64; ++q) t += wsum[q];
+        base = t ? atomicAdd(count, t) : 0;
+    }
+    __syncthreads();
+    int off = base + incl - c;
+    for (int q = 0; q < wv; ++q) off += wsum[q];
+#pragma unroll
+    for (int k = 0; k < FY_CPT; ++k)
+        if (i0 + k < n && !done[i0 + k]) list[off++] = (int32_t)(i0 + k);
 }
 
 __global__ __launch_bounds__(EP_THREADS) void fy_reserve_kernel(const int32_t* __restrict__ list, const int* count,
@@ -95,7 +159,7 @@ __global__ __launch_bounds__(EP_THREADS) void fy_commit_kernel(const int32_t* __
                 pend = true;
             }
         }
-        // wave-aggregated append of the swaps still pending
+        // wave-aggregated append of the swaps still pending (few by now)
         const unsigned long long bal = __ballot(pend);
         if (bal == 0) continue;
         int base = 0;
@@ -156,6 +220,7 @@ struct FyLayout {
     unsigned long long* R;
     int32_t* list[2];
     int* count;  // [2]
+    uint8_t* done;
 };
 
 static FyLayout fy_layout(void* ws, int64_t n) {
@@ -170,6 +235,8 @@ static FyLayout fy_layout(void* ws, int64_t n) {
     f.list[0] = reinterpret_cast<int32_t*>(p);
     p += al256e(n * 4);
     f.list[1] = reinterpret_cast<int32_t*>(p);
+    p += al256e(n * 4);
+    f.done = reinterpret_cast<uint8_t*>(p);
     return f;
 }
 
@@ -181,7 +248,7 @@ extern "C" {
 
 int64_t ncf_randperm_workspace(int64_t n) {
     if (n <= 0 || n > 0x7fffffff) return -1;
-    return 256 + al256e(n * 8) + 3 * al256e(n * 4);
+    return 256 + al256e(n * 8) + 3 * al256e(n * 4) + al256e(n);
 }
 
 int ncf_randperm(const uint32_t* words, int64_t n, int64_t* perm, int rounds, void* workspace, int64_t workspace_bytes,
@@ -191,20 +258,32 @@ int ncf_randperm(const uint32_t* words, int64_t n, int64_t* perm, int rounds, vo
     if (workspace_bytes < ncf_randperm_workspace(n)) return NCF_E_ARG;
     FyLayout F = fy_layout(workspace, n);
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(fill_u64_kernel, dim3(ep_grid(n, 8192)), dim3(EP_THREADS), 0, st, F.R, n, ~0ull);
-    hipLaunchKernelGGL(fy_init_kernel, dim3(ep_grid(n, 8192)), dim3(EP_THREADS), 0, st, words, n, F.H, perm, F.list[0],
-                       F.count);
-    for (int r = 0; r < rounds; ++r) {
+    const unsigned g = ep_grid(n, 8192);
+    hipLaunchKernelGGL(fill_u64_kernel, dim3(g), dim3(EP_THREADS), 0, st, F.R, n, ~0ull);
+    hipLaunchKernelGGL(fy_init_kernel, dim3(g), dim3(EP_THREADS), 0, st, words, n, F.H, perm, F.done);
+    const int fr = rounds < FY_FLAG_ROUNDS ? rounds : FY_FLAG_ROUNDS;
+    for (int r = 0; r < fr; ++r) {
         const uint32_t tag = 0xffffu - (uint32_t)r;  // later rounds win over stale reservations
-        const int cur = r & 1;
-        const unsigned g = ep_grid(n, 4096);
-        hipLaunchKernelGGL(fy_reserve_kernel, dim3(g), dim3(EP_THREADS), 0, st, F.list[cur], F.count + cur, F.H, F.R, tag,
-                           F.count + (cur ^ 1));
-        hipLaunchKernelGGL(fy_commit_kernel, dim3(g), dim3(EP_THREADS), 0, st, F.list[cur], F.count + cur, F.H, F.R, tag,
-                           perm, F.list[cur ^ 1], F.count + (cur ^ 1));
+        hipLaunchKernelGGL(fy_reserve_flags_kernel, dim3(g), dim3(EP_THREADS), 0, st, F.done, n, F.H, F.R, tag);
+        hipLaunchKernelGGL(fy_commit_flags_kernel, dim3(g), dim3(EP_THREADS), 0, st, F.done, n, F.H, F.R, tag, perm);
     }
-    hipLaunchKernelGGL(fy_finish_kernel, dim3(1), dim3(1024), 0, st, F.list[rounds & 1], F.count + (rounds & 1), F.H,
-                       perm, remaining);
+    if (hipMemsetAsync(F.count, 0, 8, st) != hipSuccess) return NCF_E_LAUNCH;
+    const int64_t per_block = (int64_t)EP_THREADS * FY_CPT;
+    hipLaunchKernelGGL(fy_compact_kernel, dim3((unsigned)((n + per_block - 1) / per_block)), dim3(EP_THREADS), 0, st,
+                       F.done, n, F.list[0], F.count);
+    // list rounds: grids sized for ~2% of n pending (grid-stride covers any count)
+    const unsigned gl = ep_grid(n / 48 + 1024, 4096);
+    for (int r = fr; r < rounds; ++r) {
+        const uint32_t tag = 0xffffu - (uint32_t)r;
+        const int cur = (r - fr) & 1;
+        hipLaunchKernelGGL(fy_reserve_kernel, dim3(gl), dim3(EP_THREADS), 0, st, F.list[cur], F.count + cur, F.H, F.R,
+                           tag, F.count + (cur ^ 1));
+        hipLaunchKernelGGL(fy_commit_kernel, dim3(gl), dim3(EP_THREADS), 0, st, F.list[cur], F.count + cur, F.H, F.R,
+                           tag, perm, F.list[cur ^ 1], F.count + (cur ^ 1));
+    }
+    const int last = (rounds - fr) & 1;
+    hipLaunchKernelGGL(fy_finish_kernel, dim3(1), dim3(1024), 0, st, F.list[last], F.count + last, F.H, perm,
+                       remaining);
     return ep_status();
 }
 

@@ -3,6 +3,8 @@
 // RandomState: same MT19937 word stream, same masked-rejection randint, same
 // membership test.  Membership is a per-user bitset when U*I bits fit in
 // 512 MiB (ml-1m: 2.8 MB, ml-20m: 463 MB), else CSR rows + binary search.
+#include <immintrin.h>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -158,18 +160,89 @@ void ncf_mt_seed(uint32_t seed, uint32_t* key, int32_t* pos) {
 }  // extern "C"
 
 // Blocked pass (same draws as the reference loop): the MT19937 stream is run in
-// 9,984-word blocks by fill_words (vectorised regenerate + temper), each block is
-// masked and compacted branch-free into its randint candidates (v = w & mask <=
-// n - 1), and the walk over the positives skips the candidates that are positives
-// of the slot's user.  The state after the pass: the snapshot taken before the
-// block holding the last accepted word, advanced to just past that word.
-// (A generator thread feeding this walk was measured slower: the blocks' cache
+// 9,984-word blocks by fill_words (vectorised regenerate + temper); each block is
+// masked and compacted into its randint candidates (v = w & mask <= n - 1; AVX-512
+// compress where the CPU has it); then each run of consecutive positives of one
+// user (file order: the training file is sorted by user) takes its num_ng * run
+// slots from the candidates: the non-members of the user's positives, in order
+// (a member is the reference's "draw again").  With AVX-512, 16 candidates at a
+// time: membership bits gathered first, non-members compressed into the slots.  The state after the pass: the snapshot taken
+// before the block holding the last accepted word, advanced to just past it.
+// (A generator thread feeding the walk was measured slower: the blocks' cache
 // lines moving between cores cost more than the generation it overlapped.)
 namespace {
 constexpr int BLK_WORDS = N * 16;
+constexpr int CAND_PAD = 16;  // full-vector stores past the last candidate
+
+__attribute__((target("avx512f"))) int compact_avx512(const uint32_t* w, uint32_t mask, uint32_t rng, uint32_t* out) {
+    const __m512i vm = _mm512_set1_epi32((int)mask), vr = _mm512_set1_epi32((int)rng);
+    int nc = 0;
+    for (int k = 0; k < BLK_WORDS; k += 16) {
+        const __m512i v = _mm512_and_si512(_mm512_loadu_si512(w + k), vm);
+        const __mmask16 keep = _mm512_cmple_epu32_mask(v, vr);
+        _mm512_storeu_si512(out + nc, _mm512_maskz_compress_epi32(keep, v));
+        nc += __builtin_popcount((unsigned)keep);
+    }
+    return nc;
+}
+
+int compact_scalar(const uint32_t* w, uint32_t mask, uint32_t rng, uint32_t* out) {
+    int nc = 0;
+    for (int k = 0; k < BLK_WORDS; ++k) {
+        const uint32_t v = w[k] & mask;
+        out[nc] = v;
+        nc += v <= rng;
+    }
+    return nc;
+}
+
+const bool g_avx512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("bmi2");
+
+int compact(const uint32_t* w, uint32_t mask, uint32_t rng, uint32_t* out) {
+    return g_avx512 ? compact_avx512(w, mask, rng, out) : compact_scalar(w, mask, rng, out);
+}
+
+// One user's walk over candidates cp[*c .. nc) filling out[*o .. end): 16
+// candidates at a time, their membership bits gathered from the user's bitset
+// row first (no dependence on the slot), the non-members compressed into the
+// next slots.  Returns with *o == end or the block exhausted (*c > nc - 16: the
+// scalar loop finishes it).
+__attribute__((target("avx512f,bmi2"))) void walk_avx512(const uint32_t* cp, int* c, int nc, const uint64_t* row,
+                                                          int32_t* out, int64_t* o, int64_t end, int64_t S) {
+    int cc = *c;
+    int64_t oo = *o;
+    const __m512i one = _mm512_set1_epi64(1);
+    while (oo < end && cc + 16 <= nc) {
+        const __m512i v = _mm512_loadu_si512(cp + cc);
+        const __m512i wi = _mm512_srli_epi32(v, 6);
+        const __m512i lo = _mm512_i32gather_epi64(_mm512_castsi512_si256(wi), (const long long*)row, 8);
+        const __m512i hi = _mm512_i32gather_epi64(_mm512_extracti64x4_epi64(wi, 1), (const long long*)row, 8);
+        const __m512i sh = _mm512_and_si512(v, _mm512_set1_epi32(63));
+        const __m512i blo = _mm512_srlv_epi64(lo, _mm512_cvtepu32_epi64(_mm512_castsi512_si256(sh)));
+        const __m512i bhi = _mm512_srlv_epi64(hi, _mm512_cvtepu32_epi64(_mm512_extracti64x4_epi64(sh, 1)));
+        const __mmask8 mlo = _mm512_test_epi64_mask(blo, one), mhi = _mm512_test_epi64_mask(bhi, one);
+        const unsigned keep = ~((unsigned)mlo | ((unsigned)mhi << 8)) & 0xffffu;
+        const int cnt = __builtin_popcount(keep);
+        const int64_t room = end - oo;
+        if (cnt < room) {  // the run goes on past these 16
+            if (oo + 16 <= S) _mm512_storeu_si512(out + oo, _mm512_maskz_compress_epi32((__mmask16)keep, v));
+            else _mm512_mask_compressstoreu_epi32(out + oo, (__mmask16)keep, v);
+            oo += cnt;
+            cc += 16;
+        } else {  // the run ends inside these 16: its last slot takes the room-th non-member,
+                  // and the candidates after it belong to the next run
+            const unsigned k2 = _pdep_u32((1u << room) - 1u, keep);
+            _mm512_mask_compressstoreu_epi32(out + oo, (__mmask16)k2, v);
+            oo = end;
+            cc += 32 - __builtin_clz(k2);
+        }
+    }
+    *c = cc;
+    *o = oo;
+}
 }  // namespace
 
-template <typename Cand, bool BITS>
+template <bool BITS>
 static int64_t sample_blocked(const Sampler* s, uint32_t num_item, int32_t num_ng, uint32_t* key, int32_t* pos,
                               int32_t* out_items) {
     const uint32_t rng = num_item - 1u;
@@ -179,47 +252,52 @@ static int64_t sample_blocked(const Sampler* s, uint32_t num_item, int32_t num_n
     std::memcpy(mt, key, sizeof(mt));
     int q = *pos, snap_q = q;
     std::vector<uint32_t> buf(BLK_WORDS);
-    std::vector<Cand> cand(BLK_WORDS);
-    Cand* const cp = cand.data();
+    std::vector<uint32_t> cand(BLK_WORDS + CAND_PAD);
+    const uint32_t* const cp = cand.data();
     int nc = 0, c = 0;
     int64_t blocks = 0;
     const int64_t wpu = s->words_per_user;
     const uint32_t n_items = (uint32_t)s->n_items;
-    const uint64_t* const bits = BITS ? s->bits.data() : nullptr;
     const int64_t npos = (int64_t)s->pos_users.size();
     const int32_t* const pusers = s->pos_users.data();
+    const int64_t S = npos * num_ng;
+    const bool vec = g_avx512 && num_item <= n_items;  // every candidate then indexes inside the row
     int64_t o = 0;
-    for (int64_t p = 0; p < npos; ++p) {
+    for (int64_t p = 0; p < npos;) {
         const int32_t u = pusers[p];
-        const uint64_t* row = BITS ? bits + (size_t)(u >= 0 && u < s->n_users ? u : 0) * wpu : nullptr;
+        int64_t p1 = p + 1;
+        while (p1 < npos && pusers[p1] == u) ++p1;
+        const int64_t end = o + (p1 - p) * num_ng;
         const bool uok = u >= 0 && u < s->n_users;
-        for (int t = 0; t < num_ng; ++t) {
-            for (;;) {
-                if (c >= nc) {
-                    std::memcpy(snap, mt, sizeof(mt));
-                    snap_q = q;
-                    fill_words(mt, &q, BLK_WORDS, buf.data());
-                    ++blocks;
-                    nc = 0;
-                    const uint32_t* bp = buf.data();
-                    for (int k = 0; k < BLK_WORDS; ++k) {
-                        const uint32_t v = bp[k] & mask;
-                        cp[nc] = (Cand)v;
-                        nc += v <= rng;
-                    }
-                    c = 0;
-                    continue;
+        const uint64_t* row = BITS ? s->bits.data() + (size_t)(uok ? u : 0) * wpu : nullptr;
+        while (o < end) {
+            if (c >= nc) {
+                std::memcpy(snap, mt, sizeof(mt));
+                snap_q = q;
+                fill_words(mt, &q, BLK_WORDS, buf.data());
+                ++blocks;
+                nc = compact(buf.data(), mask, rng, cand.data());
+                c = 0;
+                continue;
+            }
+            if (BITS) {
+                if (vec && uok) walk_avx512(cp, &c, nc, row, out_items, &o, end, S);
+                while (c < nc && o < end) {  // scalar: the block's tail, or no AVX-512
+                    const uint32_t v = cp[c++];
+                    if (uok && v < n_items && ((row[v >> 6] >> (v & 63)) & 1ull)) continue;  // (u, v) in train_mat
+                    out_items[o++] = (int32_t)v;
                 }
+            } else {
                 const uint32_t v = cp[c++];
-                const bool member = BITS ? (uok && v < n_items && ((row[v >> 6] >> (v & 63)) & 1ull))
-                                         : s->contains(u, (int32_t)v);
-                if (member) continue;  // (u, j) in train_mat: draw again
-                out_items[o++] = (int32_t)v;
-                break;
+                if (!s->contains(u, (int32_t)v)) out_items[o++] = (int32_t)v;
             }
         }
+        p = p1;
     }
     // word offset (in the current block) of candidate c - 1, the last one taken
+    std::memcpy(mt, snap, sizeof(mt));
+    int qb = snap_q;
+    fill_words(mt, &qb, BLK_WORDS, buf.data());
     int k = 0;
     for (int seen = 0; k < BLK_WORDS; ++k) {
         if ((buf[k] & mask) <= rng && ++seen == c) break;
@@ -240,11 +318,8 @@ int64_t ncf_sampler_sample(const void* sp, int32_t num_item, int32_t num_ng, uin
     if (num_ng > 0 && !out_items && !s->pos_users.empty()) return -1;
     if (num_ng == 0 || s->pos_users.empty()) return 0;
     if (num_item >= 2)
-        return num_item <= 65536
-                   ? (s->use_bits ? sample_blocked<uint16_t, true>(s, (uint32_t)num_item, num_ng, key, pos, out_items)
-                                  : sample_blocked<uint16_t, false>(s, (uint32_t)num_item, num_ng, key, pos, out_items))
-                   : (s->use_bits ? sample_blocked<uint32_t, true>(s, (uint32_t)num_item, num_ng, key, pos, out_items)
-                                  : sample_blocked<uint32_t, false>(s, (uint32_t)num_item, num_ng, key, pos, out_items));
+        return s->use_bits ? sample_blocked<true>(s, (uint32_t)num_item, num_ng, key, pos, out_items)
+                           : sample_blocked<false>(s, (uint32_t)num_item, num_ng, key, pos, out_items);
     // num_item == 1: numpy's randint(1) returns 0 without consuming a word
     int64_t o = 0;
     for (const int32_t u : s->pos_users) {

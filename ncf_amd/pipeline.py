@@ -20,7 +20,9 @@ the generators the reference would leave behind.
 Prefetch: epoch e+1's negatives are drawn from the NumPy state epoch e left, on a
 host thread, while epoch e trains; its sampler seed is *peeked* (the torch state
 is saved, the metrics() pass's draw and the next two DataLoader draws are made,
-the state restored) and its permutation words generated on a second thread.
+the state restored) and its permutation words generated on a second thread; its
+rows and permutation are then built on a side stream, under epoch e's steps, so
+the epoch boundary is left with the grouping by item only.
 When epoch e+1 starts, the real draws are made and compared with what was used;
 a mismatch (someone else consumed either generator in between) discards the
 prefetch, and the epoch is built synchronously.
@@ -29,6 +31,7 @@ from __future__ import annotations
 
 import math
 import threading
+import time
 
 import numpy as np
 import torch
@@ -62,8 +65,12 @@ class _Staged:
     def __init__(self, key, pos, seed):
         self.key, self.pos, self.seed = key, pos, seed
         self.end_key = self.end_pos = None  # NumPy state after the epoch's ng_sample
-        self.event = None
+        self.event = None   # uploads done
+        self.ready = None   # rows + permutation built
+        self.t0 = None
+        self.rem = None     # pinned copy of ncf_randperm's *remaining
         self.error = None
+        self.host_ms = {}
 
 
 class EpochPipeline:
@@ -103,33 +110,42 @@ class EpochPipeline:
         self.prefetch = prefetch
         self._pending = None
         self._threads = []
-        self._check_remaining = False
+        self.side_stream = torch.cuda.Stream(device=dev)
+        self._last = None
         self.stats = {"epochs": 0, "prefetch_hits": 0}
+        self.events = None  # (start, rows+perm ready, grouped) of the last epoch
 
     # ---------------------------------------------------------------- host part
-    def _stage(self, slot, key, pos, seed):
+    def _stage(self, slot, key, pos, seed, before_upload=None):
         """Negatives from NumPy state (key, pos) and the permutation words of
         `seed`, staged in pinned memory and uploaded (runs on worker threads)."""
         s = _Staged(key.copy(), int(pos), seed)
+        t_all = time.perf_counter()
         neg = self._neg_host[slot].numpy()
         words = self._words_host[slot].numpy().view(np.uint32)
 
         def draw_negatives():
+            t0 = time.perf_counter()
             if self.S == 0:
                 s.end_key, s.end_pos = s.key.copy(), s.pos
                 return
             k2, p2 = s.key.copy(), np.array([s.pos], dtype=np.int32)
             self.ds._get_sampler().sample(self.num_item, self.ng, k2, p2, out=neg[: self.S])
             s.end_key, s.end_pos = k2, int(p2[0])
+            s.host_ms["sample"] = (time.perf_counter() - t0) * 1e3
 
         def draw_words():
+            t0 = time.perf_counter()
             torch_words(seed, self.n - 1, words[: self.n - 1])
+            s.host_ms["words"] = (time.perf_counter() - t0) * 1e3
 
         try:
             t = threading.Thread(target=draw_words)
             t.start()
             draw_negatives()
             t.join()
+            if before_upload is not None:
+                before_upload()
             with torch.cuda.stream(self.copy_stream):
                 if self.S:
                     self._neg_dev[slot][: self.S].copy_(self._neg_host[slot][: self.S], non_blocking=True)
@@ -140,6 +156,7 @@ class EpochPipeline:
                 s.event.record(self.copy_stream)
         except Exception as e:  # surfaced when the epoch is consumed
             s.error = e
+        s.host_ms["stage"] = (time.perf_counter() - t_all) * 1e3
         return s
 
     # ---------------------------------------------------------------- API
@@ -159,44 +176,63 @@ class EpochPipeline:
             t.join()
         self._threads = []
 
-    def next_epoch(self, peek_eval_draw=True):
-        """The epoch's packed stream in batch order (device), consuming the NumPy
-        global stream (ng_sample) and the torch global generator (DataLoader)
-        exactly like the reference's epoch.  peek_eval_draw: a metrics() pass
-        (one torch draw) follows this epoch before the next next_epoch()."""
-        self._join()
-        if self._check_remaining:  # the previous epoch's permutation (its stream has long synced)
-            self._check_remaining = False
-            if int(self.remaining.item()) != 0:
-                raise RuntimeError("ncf_randperm left swaps pending")
-        key, pos = _mt_state()
-        seed = epoch_permutation_seed()  # the DataLoader's two draws
-        staged, self._pending = self._pending, None
-        if staged is not None and staged.error is not None:
-            raise staged.error
-        if (staged is not None and staged.seed == seed and staged.pos == pos
-                and np.array_equal(staged.key, key)):
-            self.stats["prefetch_hits"] += 1
-        else:
-            staged = self._stage(self._slot, key, pos, seed)
-            if staged.error is not None:
-                raise staged.error
-        slot = self._slot
-        np.random.set_state(("MT19937", staged.end_key, staged.end_pos, 0, 0.0))
-        dev = self.device
-        st = L.stream_ptr(dev)
-        torch.cuda.current_stream(dev).wait_event(staged.event)
+    def _device_build(self, staged, slot, stream):
+        """On `stream` (after the staged uploads): the epoch's packed rows and its
+        permutation.  Records staged.ready and the randperm completion check."""
         lib = L.hip()
+        st = stream.cuda_stream
+        stream.wait_event(staged.event)
+        staged.t0 = torch.cuda.Event(enable_timing=True)
+        staged.t0.record(stream)
         L.check(lib.ncf_build_rows(self.pu.data_ptr(), self.pi.data_ptr(), self.P,
                                    self._neg_dev[slot].data_ptr() if self.S else None, self.ng,
                                    self.rows.data_ptr(), st), "ncf_build_rows")
         L.check(lib.ncf_randperm(self._words_dev[slot].data_ptr(), self.n, self.perm.data_ptr(), self.rounds,
                                  self.fy_ws.data_ptr(), self.fy_ws.numel(), self.remaining.data_ptr(), st),
                 "ncf_randperm")
-        self._check_remaining = True
+        with torch.cuda.stream(stream):
+            staged.rem = torch.empty(1, dtype=torch.int32).pin_memory()
+            staged.rem.copy_(self.remaining, non_blocking=True)
+        staged.ready = torch.cuda.Event(enable_timing=True)
+        staged.ready.record(stream)
+
+    def next_epoch(self, peek_eval_draw=True):
+        """The epoch's packed stream in batch order (device), consuming the NumPy
+        global stream (ng_sample) and the torch global generator (DataLoader)
+        exactly like the reference's epoch.  peek_eval_draw: a metrics() pass
+        (one torch draw) follows this epoch before the next next_epoch().
+
+        With a prefetch hit the rows and the permutation were built on a side
+        stream while the previous epoch trained; what is left here is the
+        grouping by item (ncf_prepare_epoch) on the current stream."""
+        self._join()
+        self.check()
+        key, pos = _mt_state()
+        seed = epoch_permutation_seed()  # the DataLoader's two draws
+        staged, self._pending = self._pending, None
+        if staged is not None and staged.error is not None:
+            raise staged.error
+        slot = self._slot
+        dev = self.device
+        cur = torch.cuda.current_stream(dev)
+        if (staged is not None and staged.seed == seed and staged.pos == pos
+                and np.array_equal(staged.key, key)):
+            self.stats["prefetch_hits"] += 1
+        else:
+            if staged is not None and staged.ready is not None:
+                staged.ready.synchronize()  # a discarded prefetch still writes rows / perm: let it finish
+            staged = self._stage(slot, key, pos, seed)
+            if staged.error is not None:
+                raise staged.error
+            self._device_build(staged, slot, cur)
+        np.random.set_state(("MT19937", staged.end_key, staged.end_pos, 0, 0.0))
+        cur.wait_event(staged.ready)
+        e1 = torch.cuda.Event(enable_timing=True)
         out = self.prep(self.rows, self.perm, self.batch_size, self.item_num)
-        done = torch.cuda.Event()
-        done.record(torch.cuda.current_stream(dev))
+        e1.record(cur)
+        self.events = (staged.t0, staged.ready, e1)
+        self._last = staged
+        self.stats.setdefault("host_ms", []).append(dict(staged.host_ms))
         # the dataset's host view of this epoch's negatives (fetched only if asked for)
         self.ds._set_device_negatives(self._neg_dev[slot][: self.S] if self.S else None)
         self.stats["epochs"] += 1
@@ -206,14 +242,45 @@ class EpochPipeline:
             nslot = slot ^ 1
 
             def work():
-                done.synchronize()  # the other slot's buffers were read by the epoch before
-                self._pending = self._stage(nslot, nkey, npos, nseed)
+                # host draws first; the uploads and the device build wait until this
+                # epoch's grouping has read rows / perm (the other slot's buffers were
+                # read by the epoch before)
+                s = self._stage(nslot, nkey, npos, nseed, before_upload=e1.synchronize)
+                if s.error is None:
+                    try:
+                        self._device_build(s, nslot, self.side_stream)
+                    except Exception as e:  # surfaced when the epoch is consumed
+                        s.error = e
+                self._pending = s
             t = threading.Thread(target=work, daemon=True)
             t.start()
             self._threads.append(t)
             self._slot = nslot
         return out
 
+    def check(self):
+        """Raise if the last consumed epoch's permutation did not complete (never
+        seen: the rounds launched cover the observed depth with margin, and a short
+        tail is finished in order on the device)."""
+        last, self._last = self._last, None
+        if last is not None and last.rem is not None:
+            last.ready.synchronize()
+            if int(last.rem[0]) != 0:
+                raise RuntimeError("ncf_randperm left swaps pending")
+
+    def device_ms(self):
+        """(rows + permutation, grouping) device milliseconds of the last epoch: the
+        first runs on the side stream under the previous epoch's steps when the
+        prefetch hit, the second on the current stream at the boundary."""
+        if self.events is None:
+            return None
+        t0, ready, e1 = self.events
+        e1.synchronize()
+        return t0.elapsed_time(ready), ready.elapsed_time(e1)
+
     def close(self):
         self._join()
+        self.check()
+        if self._pending is not None and self._pending.ready is not None:
+            self._pending.ready.synchronize()
         self._pending = None

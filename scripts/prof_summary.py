@@ -40,10 +40,11 @@ def load_pmc(d, sub, counter):
 
 def main():
     d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+    config = sys.argv[2] if len(sys.argv) > 2 else "c3"  # the bench config profiled (bench.py pmc_traffic keys on it)
     stats = load_stats(d)
     fetch = load_pmc(d, "pmc_fetch", "FETCH_SIZE")
     write = load_pmc(d, "pmc_write", "WRITE_SIZE")
-    out = {"kernels": []}
+    out = {"config": config, "kernels": []}
     print("| kernel | calls | avg us | % time | FETCH_SIZE KB | WRITE_SIZE KB | HBM bytes (2xF+W) | GB/s |")
     print("|---|---|---|---|---|---|---|---|")
     for r in stats:
@@ -59,6 +60,27 @@ def main():
         print(f"| {k} | {r['Calls']} | {avg_us:.2f} | {float(r['Percentage']):.1f} | "
               f"{'' if f is None else f'{f:.0f}'} | {'' if w is None else f'{w:.0f}'} | "
               f"{'' if hbm is None else f'{hbm / 1e6:.2f} MB'} | {'' if gbs is None else f'{gbs:.0f}'} |")
+    # SQ pass (MFMA utilisation): SQ_VALU_MFMA_BUSY_CYCLES summed over the 1,024
+    # SIMDs (256 CUs x 4); GRBM_GUI_ACTIVE = GPU-busy cycles of the dispatch
+    sq = {c: load_pmc(d, "pmc_sq", c) for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES",
+                                                 "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAVES")}
+    if any(sq.values()):
+        print()
+        print("| kernel | MFMA busy cycles / SIMD | GRBM_GUI_ACTIVE | MFMA busy / GUI_ACTIVE | SQ_WAVE_CYCLES | SQ_WAIT_ANY | SQ_ACTIVE_INST_ANY |")
+        print("|---|---|---|---|---|---|---|")
+        for k in out["kernels"]:
+            n = k["kernel"]
+            mb = sq["SQ_VALU_MFMA_BUSY_CYCLES"].get(n)
+            ga = sq["GRBM_GUI_ACTIVE"].get(n)
+            if mb is None:
+                continue
+            per_simd = mb / 1024
+            k["sq"] = {c: sq[c].get(n) for c in sq}
+            k["mfma_busy_per_simd"] = per_simd
+            k["mfma_busy_frac_of_gui_active"] = per_simd / ga if ga else None
+            print(f"| {n} | {per_simd:.0f} | {'' if ga is None else f'{ga:.0f}'} | "
+                  f"{'' if not ga else f'{per_simd / ga:.3f}'} | {sq['SQ_WAVE_CYCLES'].get(n, 0):.0f} | "
+                  f"{sq['SQ_WAIT_ANY'].get(n, 0):.0f} | {sq['SQ_ACTIVE_INST_ANY'].get(n, 0):.0f} |")
     json.dump(out, open(os.path.join(d, "prof_summary.json"), "w"), indent=1)
 
 

@@ -8,10 +8,11 @@ Tolerances (north star: "within 1e-5 relative for fp32 loss/logits"):
     atomics and MFMA K-order vs ATen's CPU kernels)
   * Adam trajectories: per-step loss rtol 1e-5 over 100 steps; parameters
     rtol 1e-4, atol 1e-6 after 100 steps on the golden (50 x 80) id space;
-    at full id spaces (ml-1m multitile, C4 ml-20m) per _assert_trajectory_close:
-    rtol 1e-4 + atol 1e-6*max|p| for >= 98% of every tensor, every element
-    within 4*T*lr, and no table row mostly off by > lr/4 (what a wrong-row
-    update looks like).
+    at full id spaces (ml-1m multitile, C4 ml-20m): free-running, rtol 1e-4 +
+    atol 1e-6*max|p| for >= 90% of every tensor and every element within 4*T*lr
+    -- 90% for a free-running 20-step C4 run: two fp32 trajectories drift apart --
+    and every step teacher-forced from the
+    oracle's state to rtol 1e-5 + atol 5e-3*lr.
   * HR / NDCG: exact.
 """
 import numpy as np
@@ -130,11 +131,8 @@ ONE_STEP = {  # name: (model_type, f, L, B, expected path)
 
 
 def _fact_mode(lay):
-    """Whether the factored layer-0 path runs for this layout: its workspace holds
-    the expansion's dW0 partials after the slab (include/ncf_hip.h)."""
-    import ncf_amd._lib as L
-    slab = L.hip().ncf_slab_rows() * L.hip().ncf_slab_stride(L.ctypes.byref(lay)) * 4
-    return L.hip().ncf_workspace_bytes(L.ctypes.byref(lay), 1) > slab
+    from ncf_amd import ops
+    return ops.fact_mode(lay)
 
 
 def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3):
@@ -203,33 +201,97 @@ def test_one_step_fact_boundary(U, I, fact):
 
 
 def _assert_trajectory_close(got, exp, T, lr, name):
-    """Parameters after T Adam steps.  Elements are held to rtol 1e-4 + atol
-    1e-6 * max|p|.  Adam turns fp32 summation-order noise into parameter movement
-    where a gradient is near zero (its sign: up to ~lr a step) or near eps (its
-    size: a row touched once whose gradient is ~1e-8 moves lr * g / (|g| + eps)),
-    so some elements -- even whole rows of the second kind -- may exceed that, by
-    at most 4 * T * lr; at most 2% of a tensor may.  What a wrong-row update (stale
-    staging, a row added twice or to the wrong id) produces instead -- most of a
-    row moved by a sizeable fraction of lr -- is rejected: no table row may have
-    more than half of its elements off by more than lr / 4."""
+    """Parameters after T free-running Adam steps.  Two correct fp32 trajectories
+    drift apart: Adam turns the summation-order noise of a near-zero gradient into
+    up to ~lr of movement, and the drifted parameters later flip ReLU mask bits of
+    pre-activations near the kink, which moves a whole embedding row differently.
+    So: every element within 4 * T * lr, at most 10% of a tensor outside rtol 1e-4 +
+    atol 1e-6 * max|p| (C4, 20 steps: up to ~4% of the first tower weight drifts
+    past that); the step-by-step check that catches a wrong update is
+    _teacher_forced_steps."""
     got = np.asarray(got, dtype=np.float64)
     exp = np.asarray(exp, dtype=np.float64)
     dev = np.abs(got - exp)
     tol = 1e-4 * np.abs(exp) + 1e-6 * max(float(np.abs(exp).max()), 1e-30)
     off = dev > tol
-    bound = 4 * T * lr
     info = f"{name}: max dev {dev.max(initial=0.0):.3g}, {off.mean():.5f} of elements off"
-    assert float(dev.max(initial=0.0)) <= bound, info
-    assert off.mean() <= 0.02, info
-    if got.ndim == 2 and got.shape[1] >= 8:
-        gross = (dev > lr / 4).mean(axis=1)
-        r = int(gross.argmax())
-        assert gross[r] <= 0.5, f"{info}; row {r}: {gross[r]:.2f} of it off by > lr/4 (max {dev[r].max():.3g})"
+    assert float(dev.max(initial=0.0)) <= 4 * T * lr, info
+    assert off.mean() <= 0.10, info
+
+
+def _relu_ties(ref, users, items, tau=1e-7):
+    """Samples of a batch with a tower pre-activation within `tau` of the ReLU kink
+    at the oracle's current parameters: there the two summation orders (MFMA
+    K-order vs ATen's CPU GEMM, ~1e-8 apart at these scales) may pick different
+    mask bits -- both correct to fp32 -- and that sample's gradient changes
+    discontinuously.  Returns (users, items) of those samples."""
+    pres = []
+    hs = [mm.register_forward_hook(lambda mod, i, o: pres.append(o.detach())) for mm in ref.MLP_layers
+          if isinstance(mm, torch.nn.Linear)]
+    with torch.no_grad():
+        ref(torch.as_tensor(users), torch.as_tensor(items))
+    for h in hs:
+        h.remove()
+    if not pres:
+        return set(), set()
+    near = (torch.stack([p.abs().min(dim=1).values for p in pres]).min(dim=0).values < tau).numpy()
+    return set(np.asarray(users)[near].tolist()), set(np.asarray(items)[near].tolist())
+
+
+def _teacher_forced_steps(ref, m, eng, users, items, labels, lr=1e-3):
+    """Every step of an Adam trajectory, checked from the oracle's own state: before
+    step t the engine gets the oracle's parameters and Adam moments (and step count),
+    runs one fused step (graph off) on batch t, and the loss must match to rtol
+    1e-5 and the parameters the oracle's after step t to rtol 1e-5 + atol 5e-3 * lr
+    (one Adam step from the same state: only the summation order differs).  The
+    exceptions are the discontinuities of ReLU ties (_relu_ties): embedding rows of
+    the tied samples' users / items, and at most 1% of a tower tensor (their
+    rank-one share of the tower gradients) when the step has a tie -- each element
+    within 2 * lr, one Adam step's largest change.  A wrong-row update, stale
+    staging or a bad moment fails at the step it happens."""
+    from ncf_amd import ops
+    opt = torch.optim.Adam(ref.parameters(), lr=lr)
+    segs = ops._segments(m, eng.lay)
+    params = dict(ref.named_parameters())
+    ties = 0
+    for t in range(len(users)):
+        with torch.no_grad():
+            for (p, off), (k, rp) in zip(segs, params.items()):
+                n = rp.numel()
+                eng.flat[off:off + n].copy_(rp.detach().reshape(-1))
+                st = opt.state.get(rp, {})
+                eng.exp_avg[off:off + n].copy_(st["exp_avg"].reshape(-1) if st else torch.zeros(n))
+                eng.exp_avg_sq[off:off + n].copy_(st["exp_avg_sq"].reshape(-1) if st else torch.zeros(n))
+        tie_u, tie_i = _relu_ties(ref, users[t], items[t])
+        ties += len(tie_u)
+        eng.ctl[0] = t
+        eng.ctl[1] = t
+        eng.run(1, use_graph=False)
+        losses = O.train_steps(ref, opt, [users[t]], [items[t]], [labels[t]])
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(eng.epoch_losses()[t], losses[0], rtol=1e-5, err_msg=f"loss step {t}")
+        for (p, off), (k, rp) in zip(segs, params.items()):
+            got = eng.flat[off:off + p.numel()].view_as(p).cpu().numpy().astype(np.float64)
+            exp = rp.detach().numpy().astype(np.float64)
+            dev = np.abs(got - exp)
+            off_ = dev > 1e-5 * np.abs(exp) + 5e-3 * lr
+            if not off_.any():
+                continue
+            where = f"{k} after step {t}: {int(off_.sum())} elements off, max {dev.max():.3g}"
+            assert dev.max() <= 2 * lr, where
+            if k.startswith("embed"):
+                rows = set(np.flatnonzero(off_.any(axis=1)).tolist())
+                unexplained = sorted(rows - (tie_u if "user" in k else tie_i))
+                assert not unexplained, f"{where}; rows with no ReLU tie: {unexplained[:10]}"
+            else:
+                assert (tie_u or tie_i) and off_.mean() <= 0.01, where
+    return ties
 
 
 def test_engine_trajectory_c4_id_space():
     """20 engine Adam steps (hipGraph) at the C4 id space vs torch.optim.Adam on the
-    oracle: per-step loss rtol 1e-5, parameters per _assert_trajectory_close."""
+    oracle: free-running per-step loss rtol 1e-5 and parameters per
+    _assert_trajectory_close, then every step teacher-forced (_teacher_forced_steps)."""
     T, B = 20, 16384
     ref, m, eng = _engine_for("NeuMF-end", 16, 3, C4_U, C4_I, 15)
     rng = np.random.default_rng(41)
@@ -240,11 +302,16 @@ def test_engine_trajectory_c4_id_space():
     assert not _fact_mode(eng.lay)
     eng.run(T, use_graph=True)
     torch.cuda.synchronize()
+    got_losses = eng.epoch_losses()[:T].copy()
+    got = {k: v.cpu().numpy().copy() for k, v in m.state_dict().items()}
+    ref0 = {k: v.clone() for k, v in ref.state_dict().items()}
     opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
     losses = O.train_steps(ref, opt, users, items, labels)
-    np.testing.assert_allclose(eng.epoch_losses()[:T], losses, rtol=1e-5)
-    for (k, v), (_, r) in zip(m.state_dict().items(), ref.state_dict().items()):
-        _assert_trajectory_close(v.cpu().numpy(), r.numpy(), T, 1e-3, k)
+    np.testing.assert_allclose(got_losses, losses, rtol=1e-5)
+    for k, r in ref.state_dict().items():
+        _assert_trajectory_close(got[k], r.numpy(), T, 1e-3, k)
+    ref.load_state_dict(ref0)
+    _teacher_forced_steps(ref, m, eng, users, items, labels)
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -456,8 +523,9 @@ def test_fused_reduce_adam_bitwise_equals_separate_kernels(monkeypatch, mt, f, L
 @pytest.mark.parametrize("mt,f,Lyr", [("NeuMF-end", 16, 3), ("NeuMF-end", 8, 2)])
 def test_engine_multitile_trajectory_vs_oracle(mt, f, Lyr):
     """Batches of 40,000 rows (every workgroup runs 2 tiles per step): 6 engine
-    Adam steps vs torch.optim.Adam on the oracle (parameters per
-    _assert_trajectory_close: a wrong tile, e.g. stale staging, moves whole rows)."""
+    Adam steps vs torch.optim.Adam on the oracle, free-running
+    (_assert_trajectory_close) and teacher-forced step by step (_teacher_forced_steps:
+    a wrong tile, e.g. stale staging, fails at the step it happens)."""
     T, B = 6, 40000
     ref, m, eng = _engine_for(mt, f, Lyr, 3000, 2000, 9)
     rng = np.random.default_rng(31)
@@ -467,8 +535,13 @@ def test_engine_multitile_trajectory_vs_oracle(mt, f, Lyr):
     _stream(eng, users, items, labels, B)
     eng.run(T, use_graph=True)
     torch.cuda.synchronize()
+    got_losses = eng.epoch_losses()[:T].copy()
+    got = {k: v.cpu().numpy().copy() for k, v in m.state_dict().items()}
+    ref0 = {k: v.clone() for k, v in ref.state_dict().items()}
     opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
     losses = O.train_steps(ref, opt, users, items, labels)
-    np.testing.assert_allclose(eng.epoch_losses()[:T], losses, rtol=1e-5)
-    for (k, v), (_, r) in zip(m.state_dict().items(), ref.state_dict().items()):
-        _assert_trajectory_close(v.cpu().numpy(), r.numpy(), T, 1e-3, k)
+    np.testing.assert_allclose(got_losses, losses, rtol=1e-5)
+    for k, r in ref.state_dict().items():
+        _assert_trajectory_close(got[k], r.numpy(), T, 1e-3, k)
+    ref.load_state_dict(ref0)
+    _teacher_forced_steps(ref, m, eng, users, items, labels)
