@@ -123,3 +123,36 @@ def test_teacher_script_runs(ml100k_dir):
     assert re.search(r"Epoch 001: Loss=[\d.]+, HR=[\d.]+, NDCG=[\d.]+, Time=\d\d:\d\d:\d\d", out.stdout), out.stdout
     assert re.search(r"Best Epoch 000: Loss=", out.stdout), out.stdout
     assert os.path.exists(os.path.join(str(ml100k_dir), "results", "models", "teacher_NeuMF-end_best.pth"))
+
+
+def test_pretrain_chain_matches_reference(golden, ml100k_dir):
+    """The NeuMF-pre chain (tests/golden/G11_pretrain_chain.npz, the reference's own
+    run): scripts/pretrain.py GMF -> MLP -> scripts/train_neumf.py --model NeuMF-pre
+    --pretraining, which loads both checkpoints (models.py:48-95) and trains with
+    SGD(lr * 10) (train_neumf.py:62-90).  Each run seeded 0 like the golden; epoch
+    lines within G7's tolerances (loss 1e-3 relative, HR/NDCG 0.01), the same
+    checkpoint files, the same parameter counts and loading messages."""
+    g = golden("G11_pretrain_chain")
+    runs = [("gmf", "pretrain.py", ["--model", "GMF", "--epochs", "2", "--factor_num", "8"]),
+            ("mlp", "pretrain.py", ["--model", "MLP", "--epochs", "2", "--factor_num", "8", "--num_layers", "3"]),
+            ("neumf_pre", "train_neumf.py", ["--model", "NeuMF-pre", "--pretraining", "--epochs", "2",
+                                             "--factor_num", "8", "--num_layers", "3"])]
+    models = os.path.join(str(ml100k_dir), "results", "models")
+    for tag, script, args in runs:
+        before = set(os.listdir(models)) if os.path.isdir(models) else set()
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", script)] + args + ["--seed", "0"],
+                             capture_output=True, text=True, timeout=600, cwd=str(ml100k_dir))
+        assert out.returncode == 0, out.stderr[-2000:]
+        ref_lines = [str(x) for x in g[f"{tag}_stdout"]]
+        got, ref = _parse(out.stdout.splitlines()), _parse(ref_lines)
+        assert len(got) == len(ref) == 2, (tag, out.stdout[-2000:])
+        for (e1, l1, h1, n1), (e2, l2, h2, n2) in zip(got, ref):
+            assert e1 == e2
+            assert abs(l1 - l2) <= 1e-3 * l2 + 1e-4, (tag, got, ref)
+            assert abs(h1 - h2) <= 0.01 and abs(n1 - n2) <= 0.01, (tag, got, ref)
+        for ln in ref_lines:
+            if ln.startswith(("Parameters:", "Model parameters:", "Loading pretrained", "Pretrained weights loaded",
+                              "Pretraining:")):
+                assert ln in out.stdout, (tag, ln)
+        new = sorted(set(os.listdir(models)) - before)
+        assert new == [str(x) for x in g[f"{tag}_checkpoints"]], (tag, new)
