@@ -11,11 +11,13 @@ with the all-reduce issued between them, see ``_capture_collective``):
                          launches the expansion (per-user/item sums -> dUm, dIm, dW0)
   2. ``ncf_reduce_slab`` per-workgroup tower grads -> flat grad buffer
   3. world > 1, dp_mode "zero1" (default): RCCL reduce-scatter of the flat grad
-     buffer; dp_mode "allreduce": RCCL all-reduce of it
+     buffer; dp_mode "sparse": the touched embedding rows as (id, row) buckets to
+     their owners + all-reduce of the dense tower tail; dp_mode "allreduce":
+     RCCL all-reduce of the flat grad buffer
   4. ``ncf_adam_step``   dense Adam over the active parameters (zero1: of this
                          rank's shard only) + grad zeroing + loss bookkeeping
                          (train_neumf.py:90,115)
-  5. zero1 only: RCCL all-gather of the updated parameter shards (in place)
+  5. zero1 / sparse: RCCL all-gather of the updated parameter shards (in place)
 
 Data parallelism: every rank holds the same epoch stream (same seeds, same
 sampler, same permutation); rank r processes rows [r*ceil(gb/W), ...) of each
@@ -72,11 +74,11 @@ class TrainEngine:
             dp_mode = os.environ.get("NCF_DP_MODE", "zero1") if self.world_size > 1 else "single"
         if self.world_size == 1:
             dp_mode = "single"
-        if dp_mode not in ("single", "zero1", "allreduce"):
+        if dp_mode not in ("single", "zero1", "allreduce", "sparse"):
             raise ValueError(f"dp_mode {dp_mode!r}")
         self.dp_mode = dp_mode
         lay = L.layout(model.user_num, model.item_num, model.factor_num, model.num_layers, model.model_type)
-        if dp_mode == "zero1":
+        if dp_mode in ("zero1", "sparse"):
             # flat buffers padded to world x shard floats; rank r owns [r*S, (r+1)*S)
             self.shard = D.shard_floats(int(lay.total), self.world_size)
             n = self.shard * self.world_size
@@ -89,7 +91,7 @@ class TrainEngine:
         n = self.flat.numel()
         self.grads = torch.zeros(n, dtype=torch.float32, device=dev)
         self.optimizer = optimizer
-        n_opt = self.shard if dp_mode == "zero1" else n
+        n_opt = self.shard if dp_mode in ("zero1", "sparse") else n
         if optimizer == "adam":
             self.exp_avg = torch.zeros(n_opt, dtype=torch.float32, device=dev)
             self.exp_avg_sq = torch.zeros(n_opt, dtype=torch.float32, device=dev)
@@ -103,9 +105,9 @@ class TrainEngine:
         self._nranges = len(rng)
         self._loss_slot = int(self.lay.loss_slot)
         self._opt_ptrs = (self.flat.data_ptr(), self.grads.data_ptr())
-        if dp_mode == "zero1":
+        if dp_mode in ("zero1", "sparse"):
             S, r = self.shard, self.rank
-            self.gshard = torch.zeros(S, dtype=torch.float32, device=dev)
+            self.gshard = torch.zeros(S if dp_mode == "zero1" else 0, dtype=torch.float32, device=dev)
             # an empty [0, 0) range when no active parameter falls in the shard: the
             # launch still records the loss if this rank owns the loss slot
             srng = D.shard_ranges(rng, self.world_size, r, S) or [[0, 0]]
@@ -114,6 +116,18 @@ class TrainEngine:
             self.loss_owner = self._loss_slot // S
             self._loss_slot = self._loss_slot - r * S
             self._opt_ptrs = (self.flat.data_ptr() + 4 * r * S, self.gshard.data_ptr())
+            if dp_mode == "sparse":  # the owner's summed shard gradient sits in the local buffer
+                self._opt_ptrs = (self.flat.data_ptr() + 4 * r * S, self.grads.data_ptr() + 4 * r * S)
+                lay = self.lay
+                f, dm = model.factor_num, model.factor_num << (model.num_layers - 1)
+                act = ops.active_mask(model)[:4]
+                if distill is not None and distill.active_extra is not None:
+                    act = [a or b for a, b in zip(act, distill.active_extra[:4])]
+                self._sparse_tables = [(int(off), w, nrows, side) for (off, w, nrows, side), a in zip(
+                    [(lay.ug, f, model.user_num, 0), (lay.ig, f, model.item_num, 1),
+                     (lay.um, dm, model.user_num, 0), (lay.im, dm, model.item_num, 1)], act) if a]
+                self._sparse_tail = (int(lay.tower_begin), int(lay.total))
+                self.sparse_bytes_sent = 0
             self._ag_scratch = None
         self.loss_hist = torch.zeros(max_batches, dtype=torch.float32, device=dev)
         self.rows = None
@@ -149,6 +163,7 @@ class TrainEngine:
         self.ctl[0] = 0
         self.ctl[2] = n
         self.ctl[3] = 0
+        self._hb = 0  # host copy of the batch index (the sparse exchange needs the batch's rows)
         if self.distill is not None:
             # the frozen teacher's logit for every row of the epoch stream (one
             # forward launch per epoch instead of one no_grad forward per step)
@@ -174,12 +189,33 @@ class TrainEngine:
             return
         if self.dp_mode == "zero1":
             D.reduce_scatter_flat(self.gshard, self.grads, self.rank, self.group)
+        elif self.dp_mode == "sparse":
+            self._sparse_exchange()
         else:
             D.allreduce_flat_grads(self.grads, self.group)
 
+    def _touched(self):
+        """Sorted unique user and item ids of this rank's shard of the current batch."""
+        b = self._hb % self.num_batches
+        b0 = b * self.batch_size
+        lo, hi = D.shard_range(min(self.batch_size, self.n_total - b0), self.world_size, self.rank)
+        seg = self.rows[b0 + lo:b0 + hi]
+        u = seg & 0xFFFFFFFF
+        u = u[u != 0xFFFFFFFF]  # padding rows
+        return torch.unique(u), torch.unique((seg >> 32) & 0x7FFFFFFF)
+
+    def _sparse_exchange(self):
+        """dp_mode "sparse": the touched rows' gradients to their owners, the dense
+        tower / predict / loss tail all-reduced (ncf_amd.distributed.sparse_exchange)."""
+        ids = self._touched()
+        tables = [(off, w, nrows, ids[side]) for off, w, nrows, side in self._sparse_tables]
+        self.sparse_bytes_sent += D.sparse_exchange(self.grads, tables, self._sparse_tail, self.shard, self.rank,
+                                                    self.world_size, self.group)
+        self._hb += 1
+
     def _allgather(self):
-        """Launch 5 (zero1): every rank's updated parameter shard to every rank."""
-        if self.dp_mode == "zero1":
+        """Launch 5 (zero1, sparse): every rank's updated parameter shard to every rank."""
+        if self.dp_mode in ("zero1", "sparse"):
             if self._ag_scratch is None and not D._native_ok(self.flat, self.group):
                 self._ag_scratch = torch.empty_like(self.flat)
             D.all_gather_flat(self.flat, self.rank, self.shard, self.group, self._ag_scratch)
@@ -191,8 +227,9 @@ class TrainEngine:
         st = L.stream_ptr(self.device)
         lib = L.hip()
         hist_len = self.num_batches
-        if self.dp_mode == "zero1":
-            L.check(lib.ncf_zero_f32(self.grads.data_ptr(), self.grads.numel(), st), "ncf_zero_f32")
+        if self.dp_mode in ("zero1", "sparse"):
+            if self.dp_mode == "zero1":  # the shard gradient is in gshard: clear the local bucket now
+                L.check(lib.ncf_zero_f32(self.grads.data_ptr(), self.grads.numel(), st), "ncf_zero_f32")
             ranges, nr = self._sranges, self._nsranges
             hist = self.loss_hist.data_ptr() if self.rank == self.loss_owner else None
         else:
@@ -209,6 +246,8 @@ class TrainEngine:
             L.check(lib.ncf_sgd_step(p, g, ranges, nr,
                                      self.ctl.data_ptr(), self.lr, self._loss_slot,
                                      hist, hist_len, st), "ncf_sgd_step")
+        if self.dp_mode == "sparse":  # the local bucket (own rows of other shards, received rows) for the next step
+            L.check(lib.ncf_zero_f32(self.grads.data_ptr(), self.grads.numel(), st), "ncf_zero_f32")
 
     @property
     def _fused_optimizer(self):
@@ -256,9 +295,10 @@ class TrainEngine:
                      ("ncf_reduce_slab", lambda: L.check(L.hip().ncf_reduce_slab(
                          ctypes.byref(self.lay), self.ws.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(),
                          L.stream_ptr(self.device)), "ncf_reduce_slab")),
-                     ("allreduce" if self.dp_mode != "zero1" else "reduce_scatter", self._allreduce),
+                     ({"zero1": "reduce_scatter", "sparse": "sparse_exchange"}.get(self.dp_mode, "allreduce"),
+                      self._allreduce),
                      ("optimizer", self._optimize)]
-            if self.dp_mode == "zero1":
+            if self.dp_mode in ("zero1", "sparse"):
                 parts.append(("all_gather", self._allgather))
         acc = {k: 0.0 for k, _ in parts}
         evs = []
@@ -310,6 +350,8 @@ class TrainEngine:
         default for world > 1: the step is then two graphs (compute, optimizer)
         with the collective issued eagerly between them, which needs nothing of
         the process group beyond a plain all_reduce (any backend)."""
+        if self.dp_mode == "sparse":  # bucket sizes go through the host every step
+            return self.world_size == 1
         return self.world_size == 1 or os.environ.get("NCF_CAPTURE_ALLREDUCE", "0") == "1"
 
     def _graph_of(self, fn):
@@ -380,7 +422,7 @@ class TrainEngine:
         """Per-batch mean BCE of the last epoch (host copy).  zero1: the rank owning
         the loss slot recorded it; it is broadcast to the others (a collective: every
         rank calls this)."""
-        if self.dp_mode == "zero1":
+        if self.dp_mode in ("zero1", "sparse"):
             import torch.distributed as dist
             h = self.loss_hist[: self.num_batches].clone()
             if D._native_ok(h, self.group):
