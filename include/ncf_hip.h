@@ -63,8 +63,15 @@ typedef struct ncf_layout {
     int64_t wp, bp;
     int64_t tower_begin, tower_len;
     int64_t total; /* floats in the flat buffer, loss slot included */
-    int32_t user_num, item_num, factor_num, num_layers, model_type, pad_;
+    int32_t user_num, item_num, factor_num, num_layers, model_type;
+    int32_t flags; /* 0 from ncf_layout_init; ncf_layout_tune sets the launch shape */
 } ncf_layout;
+
+/* ncf_layout.flags (set by ncf_layout_tune; every entry point reads them from the
+ * layout it is given, so one tuned layout must be used for a whole step) */
+#define NCF_LAYOUT_PER_ROW_L0 0x1   /* per-row layer-0 gradients even where the factored path applies */
+#define NCF_LAYOUT_WG_SHIFT 8       /* bits 8..19: workgroups of the fused step (0 = ncf_slab_rows()) */
+#define NCF_LAYOUT_WG_MASK 0xfff
 
 /* Device-resident step control block (16-byte aligned, 6 x int64).  Lets a
  * captured hipGraph replay consecutive batches with no host involvement. */
@@ -98,8 +105,19 @@ int64_t ncf_forward_workspace_bytes(const ncf_layout *lay, int64_t n);
 int ncf_layout_init(int user_num, int item_num, int factor_num, int num_layers, int model_type,
                     ncf_layout *out);
 
-/* Workgroups the fused step launches (rows of its partial slab). */
+/* Workgroups the fused step launches at most (rows of its partial slab). */
 int ncf_slab_rows(void);
+
+/*
+ * Host-only: shape the fused step for launches of up to `rows_per_launch` rows
+ * (ceil(batch_global / world)) by setting lay->flags:
+ *   - workgroups = min(ncf_slab_rows(), ceil(rows / 128)) -- a 1,024-row batch
+ *     (config C2) runs 8 workgroups and the reductions read 8 slab rows, not 256;
+ *   - per-row layer-0 gradients when rows < (user_num + item_num) / 2: the factored
+ *     path's expansion costs per table row, the per-row form per batch row.
+ * Call before sizing the workspace (ncf_workspace_bytes depends on the flags).
+ */
+int ncf_layout_tune(ncf_layout *lay, int64_t rows_per_launch);
 
 /* Floats per slab row: tower_len + 64 (16-byte aligned rows; loss at index tower_len). */
 int64_t ncf_slab_stride(const ncf_layout *lay);

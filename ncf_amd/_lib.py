@@ -43,7 +43,7 @@ class NcfLayout(ctypes.Structure):
                 ("w", c_i64 * 4), ("b", c_i64 * 4), ("wp", c_i64), ("bp", c_i64),
                 ("tower_begin", c_i64), ("tower_len", c_i64), ("total", c_i64),
                 ("user_num", c_i32), ("item_num", c_i32), ("factor_num", c_i32),
-                ("num_layers", c_i32), ("model_type", c_i32), ("pad_", c_i32)]
+                ("num_layers", c_i32), ("model_type", c_i32), ("flags", c_i32)]
 
     @property
     def loss_slot(self) -> int:
@@ -60,6 +60,7 @@ _HIP_PROTOS = {
     "ncf_supported": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "ncf_layout_init": (ctypes.c_int, [ctypes.c_int] * 5 + [ctypes.POINTER(NcfLayout)]),
     "ncf_slab_rows": (ctypes.c_int, []),
+    "ncf_layout_tune": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_i64]),
     "ncf_train_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_i64, c_vp, c_vp]),
     "ncf_train_step_kd": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp,

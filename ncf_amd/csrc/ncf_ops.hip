@@ -897,7 +897,13 @@ static const KernelEntry* fused_entry(const ncf_layout* lay) {
 static bool fact_mode(const ncf_layout* lay) {
     const KernelEntry* e = fused_entry(lay);
     return e != nullptr && e->train_fact != nullptr && lay->model_type != NCF_MODEL_GMF &&
-           (int64_t)lay->user_num + lay->item_num <= FACT_MAX_ROWS;
+           (int64_t)lay->user_num + lay->item_num <= FACT_MAX_ROWS && !(lay->flags & NCF_LAYOUT_PER_ROW_L0);
+}
+
+// Workgroups of the fused step = rows of the slab the reductions read.
+static int slab_rows_of(const ncf_layout* lay) {
+    const int w = (lay->flags >> NCF_LAYOUT_WG_SHIFT) & NCF_LAYOUT_WG_MASK;
+    return (w > 0 && w < SLAB_ROWS) ? w : SLAB_ROWS;
 }
 
 // First tower column (relative to tower_begin) the reductions produce: GMF models
@@ -970,6 +976,16 @@ int ncf_debug_set_stamps(unsigned long long* dev_buf) {
 }
 
 int ncf_slab_rows(void) { return SLAB_ROWS; }
+
+int ncf_layout_tune(ncf_layout* lay, int64_t rows) {
+    if (!lay || rows <= 0) return NCF_E_ARG;
+    int32_t f = lay->flags & ~(NCF_LAYOUT_PER_ROW_L0 | (NCF_LAYOUT_WG_MASK << NCF_LAYOUT_WG_SHIFT));
+    const int64_t tiles = (rows + TILE_ROWS - 1) / TILE_ROWS;
+    if (tiles < SLAB_ROWS) f |= (int32_t)tiles << NCF_LAYOUT_WG_SHIFT;
+    if (2 * rows < (int64_t)lay->user_num + lay->item_num) f |= NCF_LAYOUT_PER_ROW_L0;
+    lay->flags = f;
+    return NCF_OK;
+}
 
 int ncf_layout_init(int U, int I, int F, int L, int mode, ncf_layout* o) {
     if (!o || U <= 0 || I <= 0 || F <= 0 || L < 1 || L > 4 || mode < 0 || mode > 2) return NCF_E_ARG;
@@ -1078,7 +1094,7 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
     a.slab = slab;
     a.logits_out = logits_out;
     void* args[] = {&a};
-    if (hipLaunchKernel(fn, dim3(SLAB_ROWS), dim3(NTHREADS), args, (size_t)lds, (hipStream_t)stream) !=
+    if (hipLaunchKernel(fn, dim3(slab_rows_of(lay)), dim3(NTHREADS), args, (size_t)lds, (hipStream_t)stream) !=
         hipSuccess)
         return NCF_E_LAUNCH;
     const int rc = launch_status();
@@ -1188,7 +1204,7 @@ int ncf_reduce_slab(const ncf_layout* lay, const void* workspace, float* grads, 
     const int stride = (int)ncf_slab_stride(lay);
     const int lo = slab_lo(lay);
     const int blocks = (stride - lo + 63) / 64;
-    const int rows = fused_entry(lay) ? SLAB_ROWS : 1;  // the layered path accumulates into one row
+    const int rows = fused_entry(lay) ? slab_rows_of(lay) : 1;  // the layered path accumulates into one row
     hipLaunchKernelGGL(reduce_slab_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab,
                        grads + lay->tower_begin, lo, stride, rows, ctl, w0_part(lay, workspace));
     return launch_status();
@@ -1240,7 +1256,7 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
     const int stride = (int)ncf_slab_stride(lay);
     const int lo = slab_lo(lay);
     const int nA = (stride - lo + 63) / 64;
-    const int rows = fused_entry(lay) ? SLAB_ROWS : 1;
+    const int rows = fused_entry(lay) ? slab_rows_of(lay) : 1;
     const int64_t etotal = RE.prefix[RE.n];
     int64_t nB = (etotal + 255) / 256;
     if (nB > 2048) nB = 2048;

@@ -85,7 +85,9 @@ class TrainEngine:
         else:
             self.shard = None
             n = int(lay.total)
-        self.flat, self.lay = ops.ensure_flat(model, n)
+        self.flat, lay0 = ops.ensure_flat(model, n)
+        # the engine's own copy: ncf_layout_tune shapes it for the batch size
+        self.lay = type(lay0).from_buffer_copy(lay0)
         dev = self.flat.device
         self.device = dev
         n = self.flat.numel()
@@ -153,6 +155,9 @@ class TrainEngine:
         if self.batch_size != batch_size or self.ws is None:
             self._graph = None
             per = (int(batch_size) + self.world_size - 1) // self.world_size
+            # launch shape for this batch size: workgroups = its 128-row tiles (up to
+            # one per CU), per-row layer 0 for batches small against the tables
+            L.check(L.hip().ncf_layout_tune(ctypes.byref(self.lay), per), "ncf_layout_tune")
             self.ws = ops.new_workspace(self.lay, per, self.device)
         self.batch_size = int(batch_size)
         if self.num_batches > self.loss_hist.numel():

@@ -545,3 +545,28 @@ def test_engine_multitile_trajectory_vs_oracle(mt, f, Lyr):
         _assert_trajectory_close(got[k], r.numpy(), T, 1e-3, k)
     ref.load_state_dict(ref0)
     _teacher_forced_steps(ref, m, eng, users, items, labels)
+
+
+@pytest.mark.parametrize("B,per_row", [(1024, True), (4096, True), (8192, False), (300, True)])
+def test_engine_tuned_launch_shape_vs_oracle(B, per_row):
+    """ncf_layout_tune: the engine launches ceil(B/128) workgroups (the reductions read
+    that many slab rows) and takes per-row layer 0 when 2B < U + I (config C2:
+    NCF(8,3), bs 1024, ml-1m ids).  Every step teacher-forced from the oracle."""
+    import ncf_amd._lib as L
+    T = 6
+    ref, m, eng = _engine_for("NeuMF-end", 8, 3, 6041, 3707, 17)
+    rng = np.random.default_rng(43)
+    users = rng.integers(0, 6041, (T, B))
+    items = np.minimum(rng.zipf(1.3, (T, B)) - 1, 3706)
+    labels = (rng.random((T, B)) < 0.2).astype(np.int64)
+    _stream(eng, users, items, labels, B)
+    assert _fact_mode(eng.lay) == (not per_row)
+    assert (eng.lay.flags >> 8) & 0xFFF == (B + 127) // 128
+    ref0 = {k: v.clone() for k, v in ref.state_dict().items()}
+    eng.run(T, use_graph=True)
+    torch.cuda.synchronize()
+    got_losses = eng.epoch_losses()[:T].copy()
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    np.testing.assert_allclose(got_losses, O.train_steps(ref, opt, users, items, labels), rtol=1e-5)
+    ref.load_state_dict(ref0)
+    _teacher_forced_steps(ref, m, eng, users, items, labels)
