@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 8
+#define NCF_ABI_VERSION 9
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -283,18 +283,17 @@ int ncf_prepare_epoch(const uint64_t *rows, const int64_t *perm, int64_t n, int6
  * ncf_randperm: torch.randperm(n, generator=g) after g.manual_seed(seed) (the
  * RandomSampler of DataLoader(shuffle=True), train_neumf.py:55): Fisher-Yates
  * swapping r[i] with r[i + words[i] % (n - i)], words = the first n - 1 words of
- * ncf_mt_seed(seed & 0xffffffff), run as `rounds` parallel reservation rounds
- * (~2.3 log2(n) needed; 2.5 log2(n) + 16 is ample), then any swap still pending
- * (up to 4096) applied in order by one thread.  *remaining (device int32) = 0 when
- * the permutation is complete, else the number left (call again, more rounds).
+ * ncf_mt_seed(seed & 0xffffffff).  Computed in closed form (three passes, no
+ * rounds; see ncf_epoch.hip), always complete.  Since ABI 9 (was: a `rounds`
+ * count and a device `remaining` report of the round-based version).
  *
  * ncf_build_rows: rows_out = NCF_ROW_PACK of features_fill / labels_fill
  * (datasets.py:65-69): positives in file order, then positive p's num_ng
  * negatives neg[p*num_ng .. (p+1)*num_ng).
  */
 int64_t ncf_randperm_workspace(int64_t n);
-int ncf_randperm(const uint32_t *words, int64_t n, int64_t *perm, int rounds, void *workspace, int64_t workspace_bytes,
-                 int32_t *remaining, void *stream);
+int ncf_randperm(const uint32_t *words, int64_t n, int64_t *perm, void *workspace, int64_t workspace_bytes,
+                 void *stream);
 int ncf_build_rows(const int32_t *pos_users, const int32_t *pos_items, int64_t n_pos, const int32_t *neg, int num_ng,
                    uint64_t *rows_out, void *stream);
 

@@ -11,8 +11,8 @@ and this module produces the same batches as one packed device stream:
   host    the negatives (libncf_sampler.so, blocked C++ sampler: the draws are a
           sequential scan), the torch generator's words for the permutation
           (ncf_mt_words); pinned staging, upload on a copy stream
-  device  ncf_build_rows (features_fill / labels_fill), ncf_randperm (parallel
-          Fisher-Yates rounds), ncf_prepare_epoch (batch membership, grouped by item)
+  device  ncf_build_rows (features_fill / labels_fill), ncf_randperm (Fisher-Yates
+          in closed form, three passes), ncf_prepare_epoch (batch membership, grouped by item)
 The NumPy global state ends where ng_sample leaves it and the torch generator
 has made exactly the DataLoader's two draws, so everything after an epoch sees
 the generators the reference would leave behind.
@@ -29,7 +29,6 @@ prefetch, and the epoch is built synchronously.
 """
 from __future__ import annotations
 
-import math
 import threading
 import time
 
@@ -68,7 +67,6 @@ class _Staged:
         self.event = None   # uploads done
         self.ready = None   # rows + permutation built
         self.t0 = None
-        self.rem = None     # pinned copy of ncf_randperm's *remaining
         self.error = None
         self.host_ms = {}
 
@@ -96,9 +94,7 @@ class EpochPipeline:
         self.n = self.P + self.S
         self.rows = torch.empty(self.n, dtype=torch.int64, device=dev)
         self.perm = torch.empty(self.n, dtype=torch.int64, device=dev)
-        self.remaining = torch.zeros(1, dtype=torch.int32, device=dev)
         self.fy_ws = torch.empty(int(L.hip().ncf_randperm_workspace(self.n)), dtype=torch.uint8, device=dev)
-        self.rounds = int(2.5 * math.log2(max(2, self.n))) + 16
         self.prep = ops.EpochPrep(dev)
         self.copy_stream = torch.cuda.Stream(device=dev)
         # two slots: one being consumed by the device, one being filled by the host
@@ -111,7 +107,6 @@ class EpochPipeline:
         self._pending = None
         self._threads = []
         self.side_stream = torch.cuda.Stream(device=dev)
-        self._last = None
         self.stats = {"epochs": 0, "prefetch_hits": 0}
         self.events = None  # (start, rows+perm ready, grouped) of the last epoch
 
@@ -178,7 +173,7 @@ class EpochPipeline:
 
     def _device_build(self, staged, slot, stream):
         """On `stream` (after the staged uploads): the epoch's packed rows and its
-        permutation.  Records staged.ready and the randperm completion check."""
+        permutation.  Records staged.ready."""
         lib = L.hip()
         st = stream.cuda_stream
         stream.wait_event(staged.event)
@@ -187,12 +182,8 @@ class EpochPipeline:
         L.check(lib.ncf_build_rows(self.pu.data_ptr(), self.pi.data_ptr(), self.P,
                                    self._neg_dev[slot].data_ptr() if self.S else None, self.ng,
                                    self.rows.data_ptr(), st), "ncf_build_rows")
-        L.check(lib.ncf_randperm(self._words_dev[slot].data_ptr(), self.n, self.perm.data_ptr(), self.rounds,
-                                 self.fy_ws.data_ptr(), self.fy_ws.numel(), self.remaining.data_ptr(), st),
-                "ncf_randperm")
-        with torch.cuda.stream(stream):
-            staged.rem = torch.empty(1, dtype=torch.int32).pin_memory()
-            staged.rem.copy_(self.remaining, non_blocking=True)
+        L.check(lib.ncf_randperm(self._words_dev[slot].data_ptr(), self.n, self.perm.data_ptr(),
+                                 self.fy_ws.data_ptr(), self.fy_ws.numel(), st), "ncf_randperm")
         staged.ready = torch.cuda.Event(enable_timing=True)
         staged.ready.record(stream)
 
@@ -206,7 +197,6 @@ class EpochPipeline:
         stream while the previous epoch trained; what is left here is the
         grouping by item (ncf_prepare_epoch) on the current stream."""
         self._join()
-        self.check()
         key, pos = _mt_state()
         seed = epoch_permutation_seed()  # the DataLoader's two draws
         staged, self._pending = self._pending, None
@@ -231,7 +221,6 @@ class EpochPipeline:
         out = self.prep(self.rows, self.perm, self.batch_size, self.item_num)
         e1.record(cur)
         self.events = (staged.t0, staged.ready, e1)
-        self._last = staged
         self.stats.setdefault("host_ms", []).append(dict(staged.host_ms))
         # the dataset's host view of this epoch's negatives (fetched only if asked for)
         self.ds._set_device_negatives(self._neg_dev[slot][: self.S] if self.S else None)
@@ -258,16 +247,6 @@ class EpochPipeline:
             self._slot = nslot
         return out
 
-    def check(self):
-        """Raise if the last consumed epoch's permutation did not complete (never
-        seen: the rounds launched cover the observed depth with margin, and a short
-        tail is finished in order on the device)."""
-        last, self._last = self._last, None
-        if last is not None and last.rem is not None:
-            last.ready.synchronize()
-            if int(last.rem[0]) != 0:
-                raise RuntimeError("ncf_randperm left swaps pending")
-
     def device_ms(self):
         """(rows + permutation, grouping) device milliseconds of the last epoch: the
         first runs on the side stream under the previous epoch's steps when the
@@ -280,7 +259,6 @@ class EpochPipeline:
 
     def close(self):
         self._join()
-        self.check()
         if self._pending is not None and self._pending.ready is not None:
             self._pending.ready.synchronize()
         self._pending = None

@@ -61,12 +61,13 @@ def main():
               f"{'' if f is None else f'{f:.0f}'} | {'' if w is None else f'{w:.0f}'} | "
               f"{'' if hbm is None else f'{hbm / 1e6:.2f} MB'} | {'' if gbs is None else f'{gbs:.0f}'} |")
     # SQ pass (MFMA utilisation): SQ_VALU_MFMA_BUSY_CYCLES summed over the 1,024
-    # SIMDs (256 CUs x 4); GRBM_GUI_ACTIVE = GPU-busy cycles of the dispatch
+    # SIMDs (256 CUs x 4); GRBM_GUI_ACTIVE summed over the 8 XCDs (per XCD it is the
+    # dispatch's busy cycles: /8 over the trace's duration gives ~2.5 GHz)
     sq = {c: load_pmc(d, "pmc_sq", c) for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES",
                                                  "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAVES")}
     if any(sq.values()):
         print()
-        print("| kernel | MFMA busy cycles / SIMD | GRBM_GUI_ACTIVE | MFMA busy / GUI_ACTIVE | SQ_WAVE_CYCLES | SQ_WAIT_ANY | SQ_ACTIVE_INST_ANY |")
+        print("| kernel | MFMA busy cycles / SIMD | GRBM_GUI_ACTIVE / XCD | MFMA busy fraction | SQ_WAVE_CYCLES | SQ_WAIT_ANY | SQ_ACTIVE_INST_ANY |")
         print("|---|---|---|---|---|---|---|")
         for k in out["kernels"]:
             n = k["kernel"]
@@ -75,9 +76,10 @@ def main():
             if mb is None:
                 continue
             per_simd = mb / 1024
+            ga = ga / 8 if ga else ga
             k["sq"] = {c: sq[c].get(n) for c in sq}
             k["mfma_busy_per_simd"] = per_simd
-            k["mfma_busy_frac_of_gui_active"] = per_simd / ga if ga else None
+            k["mfma_busy_frac"] = per_simd / ga if ga else None
             print(f"| {n} | {per_simd:.0f} | {'' if ga is None else f'{ga:.0f}'} | "
                   f"{'' if not ga else f'{per_simd / ga:.3f}'} | {sq['SQ_WAVE_CYCLES'].get(n, 0):.0f} | "
                   f"{sq['SQ_WAIT_ANY'].get(n, 0):.0f} | {sq['SQ_ACTIVE_INST_ANY'].get(n, 0):.0f} |")

@@ -21,42 +21,48 @@ def _dataset(pu, pi, num_item, ng):
     return NCFData(np.stack([pu, pi], 1), num_item, None, ng, True)
 
 
+def _randperm(words_u32, n):
+    import ncf_amd._lib as L
+    words = torch.from_numpy(np.ascontiguousarray(words_u32).view(np.int32)).to(DEV)
+    perm = torch.empty(n, dtype=torch.int64, device=DEV)
+    ws = torch.empty(int(L.hip().ncf_randperm_workspace(n)), dtype=torch.uint8, device=DEV)
+    L.check(L.hip().ncf_randperm(words.data_ptr(), n, perm.data_ptr(), ws.data_ptr(), ws.numel(), L.stream_ptr()),
+            "ncf_randperm")
+    return perm.cpu()
+
+
 @pytest.mark.parametrize("n,seed", [(1, 0), (2, 3), (1000, 7), (65537, 2**40 + 5), (4970845, 123),
                                     (99308850, 9)])
 def test_randperm_matches_torch(n, seed):
-    import ncf_amd._lib as L
     from ncf_amd.pipeline import torch_words
     g = torch.Generator()
     g.manual_seed(seed)
     exp = torch.randperm(n, generator=g)
     w = np.empty(max(1, n - 1), dtype=np.uint32)
     torch_words(seed, n - 1, w)
-    words = torch.from_numpy(w.view(np.int32)).to(DEV)
-    perm = torch.empty(n, dtype=torch.int64, device=DEV)
-    ws = torch.empty(int(L.hip().ncf_randperm_workspace(n)), dtype=torch.uint8, device=DEV)
-    rem = torch.zeros(1, dtype=torch.int32, device=DEV)
-    # rounds = 2 leaves most swaps to the in-order tail (or reports them); the
-    # default schedule (2.5 log2 n + 16) finishes in the parallel rounds
-    for rounds in ([2] if n <= 4096 else []) + [int(2.5 * np.log2(max(2, n))) + 16]:
-        L.check(L.hip().ncf_randperm(words.data_ptr(), n, perm.data_ptr(), rounds, ws.data_ptr(), ws.numel(),
-                                     rem.data_ptr(), L.stream_ptr()), "ncf_randperm")
-        assert int(rem.item()) == 0
-        assert torch.equal(perm.cpu(), exp)
+    assert torch.equal(_randperm(w, n), exp)
 
 
-def test_randperm_reports_unfinished_tail():
-    import ncf_amd._lib as L
-    from ncf_amd.pipeline import torch_words
-    n = 200000
-    w = np.empty(n - 1, dtype=np.uint32)
-    torch_words(1, n - 1, w)
-    words = torch.from_numpy(w.view(np.int32)).to(DEV)
-    perm = torch.empty(n, dtype=torch.int64, device=DEV)
-    ws = torch.empty(int(L.hip().ncf_randperm_workspace(n)), dtype=torch.uint8, device=DEV)
-    rem = torch.zeros(1, dtype=torch.int32, device=DEV)
-    L.check(L.hip().ncf_randperm(words.data_ptr(), n, perm.data_ptr(), 1, ws.data_ptr(), ws.numel(),
-                                 rem.data_ptr(), L.stream_ptr()), "ncf_randperm")
-    assert int(rem.item()) > 4096  # one round leaves ~2/3 of the swaps: reported, not silently dropped
+def _fisher_yates(w, n):
+    a = np.arange(n, dtype=np.int64)
+    for i in range(n - 1):
+        h = i + int(w[i]) % (n - i)
+        a[i], a[h] = a[h], a[i]
+    return a
+
+
+@pytest.mark.parametrize("kind", ["zeros", "all_to_last", "chain", "few_targets"])
+def test_randperm_structured_words(kind):
+    """Words far from uniform (identity swaps, every step into the last position,
+    one long chain, a handful of hot targets) -- the closed form's list and chain
+    walks at their longest -- vs the sequential loop."""
+    n = 3000
+    i = np.arange(n - 1, dtype=np.int64)
+    w = {"zeros": np.zeros(n - 1),
+         "all_to_last": n - 1 - i,                       # H[i] = n - 1
+         "chain": np.ones(n - 1),                        # H[i] = i + 1
+         "few_targets": (np.array([2000, 2500, 2999])[i % 3] - i) % (n - i)}[kind].astype(np.uint32)
+    assert np.array_equal(_randperm(w, n).numpy(), _fisher_yates(w, n))
 
 
 def test_pipeline_epochs_equal_host_path():
