@@ -81,16 +81,19 @@ def adam_info(kt, eng, model):
     tower = sum(p.numel() for p in list(model.ordered_params())[4:])
     stride = int(lib.ncf_slab_stride(L.ctypes.byref(lay)))
     fused = L.supported(model.model_type, model.factor_num, model.num_layers) == L.PATH_FUSED
-    slab_rows = int(lib.ncf_slab_rows()) if fused else 1
+    wg = (int(lay.flags) >> L.LAYOUT_WG_SHIFT) & L.LAYOUT_WG_MASK  # ncf_layout_tune's workgroup count
+    slab_rows = (wg if 0 < wg < int(lib.ncf_slab_rows()) else int(lib.ncf_slab_rows())) if fused else 1
     partial = 0
+    slab_cols = stride
     if ops.fact_mode(lay):
         partial = int(lib.ncf_workspace_bytes(L.ctypes.byref(lay), 1)) - int(lib.ncf_slab_rows()) * stride * 4
+        slab_cols = stride - (int(lay.b[0]) - int(lay.w[0]))  # W0's columns come from the partials
     if "ncf_reduce_adam_step" in kt:
-        b = 32 * emb + 24 * tower + slab_rows * stride * 4 + partial
+        b = 32 * emb + 24 * tower + slab_rows * slab_cols * 4 + partial
         ms = kt["ncf_reduce_adam_step"]
         return {"kernel": "ncf_reduce_adam_step (slab reduce + Adam)", "params": emb + tower, "bytes": b,
                 "bytes_detail": {"embedding_adam": 32 * emb, "tower_adam": 24 * tower,
-                                 "slab_read": slab_rows * stride * 4, "w0_partials_read": partial},
+                                 "slab_read": slab_rows * slab_cols * 4, "w0_partials_read": partial},
                 "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}
     b = 32 * (emb + tower)
     ms = kt["optimizer"]
@@ -203,6 +206,7 @@ def setup_engine(cfg, ds, train, world, rank, dev, group, global_batch, seed=0):
     model = NCF(U, I, f, nl, 0.0, "NeuMF-end").to(dev)
     pipe = EpochPipeline(train, dev, global_batch, I, user_num=U, prefetch=True)
     eng = TrainEngine(model, lr=1e-3, world_size=world, rank=rank, process_group=group)
+    eng.stream_buffers = pipe.buffers  # the pipeline alternates two: graphs captured for both up front
     eng.set_epoch_stream(pipe.next_epoch(peek_eval_draw=False), global_batch, checked=True)
 
     def next_epoch():  # fresh negatives + permutation (no metrics() pass between bench epochs)
@@ -328,9 +332,14 @@ def main():
         eng.run(min(eng.num_batches, 100), use_graph=use_graph)
         pipe_ms.append(pipe.device_ms())
     kt["epoch_rows_randperm_side_stream"] = float(np.mean([x[0] for x in pipe_ms]))
+    kt["epoch_grouping_side_stream"] = float(np.mean([x[1] for x in pipe_ms]))
     hm = pipe.stats.get("host_ms", [])[-3:]
     kt["epoch_host_ms"] = {k: float(np.mean([h[k] for h in hm if k in h])) for k in ("sample", "words", "stage")
                            if any(k in h for h in hm)}
+    bm = pipe.stats.get("boundary_ms", [])[1:]
+    if bm:
+        kt["epoch_host_ms"]["boundary_join"] = float(np.mean([x[0] for x in bm]))
+        kt["epoch_host_ms"]["boundary_rest"] = float(np.mean([x[1] for x in bm]))
     kt["ncf_train_step_per_launch_b2b"] = eng.time_train_kernel(50)
     from ncf_amd import ops
     import ncf_amd._lib as L

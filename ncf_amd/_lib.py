@@ -31,6 +31,7 @@ MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
 DZ_BCE, DZ_DLOGIT, DZ_KD = 0, 1, 2
 ABI_VERSION = 9  # include/ncf_hip.h NCF_ABI_VERSION
 PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
+LAYOUT_PER_ROW_L0, LAYOUT_WG_SHIFT, LAYOUT_WG_MASK = 0x1, 8, 0xFFF  # ncf_layout.flags (ncf_layout_tune)
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
 
 c_i64 = ctypes.c_int64

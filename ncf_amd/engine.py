@@ -137,7 +137,13 @@ class TrainEngine:
         self.batch_size = None
         self._graph = None
         self._graph_k = None
-        self._graph_key = None
+        # captured step graphs per epoch-stream buffer (the epoch pipeline alternates
+        # two): key (batch_size, n_total, rows pointer) -> (graph(s), k-step graph)
+        self._graphs = {}
+        # other epoch-stream buffers this engine will be handed (same layout as
+        # the current one): captured together with it, so a buffer switch at an
+        # epoch boundary replays graphs already built
+        self.stream_buffers = []
 
     # ------------------------------------------------------------------ data
     def set_epoch_stream(self, rows, batch_size, checked=False):
@@ -153,7 +159,7 @@ class TrainEngine:
         self.rows = rows
         self.n_total = n
         if self.batch_size != batch_size or self.ws is None:
-            self._graph = None
+            self._drop_graphs()
             per = (int(batch_size) + self.world_size - 1) // self.world_size
             # launch shape for this batch size: workgroups = its 128-row tiles (up to
             # one per CU), per-row layer 0 for batches small against the tables
@@ -164,10 +170,15 @@ class TrainEngine:
             # the optimizer launches write loss_hist[b % num_batches]: one slot per
             # batch of the epoch (a captured graph holds the old pointer: re-capture)
             self.loss_hist = torch.zeros(self.num_batches, dtype=torch.float32, device=self.device)
-            self._graph = None
-        self.ctl[0] = 0
-        self.ctl[2] = n
-        self.ctl[3] = 0
+            self._drop_graphs()
+        # device-side fills (an assignment from a host scalar is a pageable copy that
+        # blocks the host until the stream drains, i.e. until the previous epoch ends)
+        if n != getattr(self, "_ctl_n", None):
+            self.ctl[0:4:3].zero_()
+            self.ctl[2:3].fill_(n)
+            self._ctl_n = n
+        else:
+            self.ctl[0:1].zero_()
         self._hb = 0  # host copy of the batch index (the sparse exchange needs the batch's rows)
         if self.distill is not None:
             # the frozen teacher's logit for every row of the epoch stream (one
@@ -387,8 +398,27 @@ class TrainEngine:
         else:
             self._graph = (self._graph_of(self._compute), self._graph_of(self._optimize))
             self._graph_k = None
-        self._graph_key = (self.batch_size, self.n_total, self.rows.data_ptr())
+        self._graphs[(self.batch_size, self.n_total, self.rows.data_ptr())] = (self._graph, self._graph_k)
         return self._graph
+
+    def _capture_buffers(self):
+        """Capture for every registered stream buffer not captured yet (the
+        launches read the rows pointer only when replayed)."""
+        cur = (self.rows, self._graph, self._graph_k)
+        try:
+            for buf in self.stream_buffers:
+                key = (self.batch_size, self.n_total, buf.data_ptr())
+                if (buf.numel() != self.n_total or buf.dtype != torch.int64 or buf.device != self.device
+                        or key in self._graphs):
+                    continue
+                self.rows = buf
+                self.capture()
+        finally:
+            self.rows, self._graph, self._graph_k = cur
+
+    def _drop_graphs(self):
+        self._graph = self._graph_k = None
+        self._graphs = {}
 
     def _replay(self):
         if len(self._graph) == 1:
@@ -407,13 +437,15 @@ class TrainEngine:
             return
         key = (self.batch_size, self.n_total, self.rows.data_ptr())
         done = 0
-        if self._graph is None or self._graph_key != key:
+        self._graph, self._graph_k = self._graphs.get(key, (None, None))
+        if self._graph is None:
             # eager first step also sets kernel attributes outside the capture
             self._step_body()
             done = 1
             if n_steps <= 1:
                 return
             self.capture()  # captured launches are recorded, not executed
+            self._capture_buffers()
         left = n_steps - done
         if self._graph_k is not None:
             k = self.GRAPH_STEPS

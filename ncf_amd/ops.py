@@ -136,19 +136,24 @@ class EpochPrep:
         self.ws = None
         self.out = None
 
-    def __call__(self, rows, perm, batch_size, item_num):
+    def __call__(self, rows, perm, batch_size, item_num, out=None):
+        """On the current stream; into `out` (n int64 on the device) if given."""
         n = rows.numel()
         need = int(L.hip().ncf_prepare_epoch_workspace(n, int(batch_size), int(item_num)))
         if need < 0:
             raise ValueError("bad ncf_prepare_epoch sizes")
         if self.ws is None or self.ws.numel() < need:
             self.ws = torch.empty(need, dtype=torch.uint8, device=self.device)
-        if self.out is None or self.out.numel() != n:
-            self.out = torch.empty(n, dtype=torch.int64, device=self.device)
+        if out is None:
+            if self.out is None or self.out.numel() != n:
+                self.out = torch.empty(n, dtype=torch.int64, device=self.device)
+            out = self.out
+        elif out.numel() != n or out.dtype != torch.int64 or not out.is_contiguous():
+            raise ValueError("prepare_epoch out: n contiguous int64")
         L.check(L.hip().ncf_prepare_epoch(rows.data_ptr(), perm.data_ptr(), n, int(batch_size), int(item_num),
-                                          self.out.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
+                                          out.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
                                           L.stream_ptr(self.device)), "ncf_prepare_epoch")
-        return self.out
+        return out
 
 
 def _ws(owner, attr, nbytes, dev):

@@ -21,14 +21,16 @@ Prefetch: epoch e+1's negatives are drawn from the NumPy state epoch e left, on 
 host thread, while epoch e trains; its sampler seed is *peeked* (the torch state
 is saved, the metrics() pass's draw and the next two DataLoader draws are made,
 the state restored) and its permutation words generated on a second thread; its
-rows and permutation are then built on a side stream, under epoch e's steps, so
-the epoch boundary is left with the grouping by item only.
+rows, permutation and grouping by item are then built on a side stream, under
+epoch e's steps, into the other of two output buffers (the step graphs are
+captured once per buffer), so the epoch boundary is one stream wait.
 When epoch e+1 starts, the real draws are made and compared with what was used;
 a mismatch (someone else consumed either generator in between) discards the
 prefetch, and the epoch is built synchronously.
 """
 from __future__ import annotations
 
+import collections
 import threading
 import time
 
@@ -59,20 +61,28 @@ def torch_words(seed, n, out):
 
 
 class _Staged:
-    """One epoch's host products (negatives, permutation words) and their upload."""
+    """One epoch's host products (negatives, permutation words), their upload and
+    device build."""
 
-    def __init__(self, key, pos, seed):
-        self.key, self.pos, self.seed = key, pos, seed
+    def __init__(self, slot, key, pos, seed):
+        self.slot, self.key, self.pos, self.seed = slot, key, pos, seed
         self.end_key = self.end_pos = None  # NumPy state after the epoch's ng_sample
         self.event = None   # uploads done
-        self.ready = None   # rows + permutation built
         self.t0 = None
+        self.built = None   # rows + permutation built
+        self.ready = None   # grouped epoch stream written
         self.error = None
         self.host_ms = {}
+        self.thread = None
+        self.sampled = threading.Event()   # end_key / end_pos known (or error)
+        self.enqueued = threading.Event()  # device build issued (or error)
 
 
 class EpochPipeline:
-    def __init__(self, dataset, device, batch_size, item_num, user_num=None, prefetch=True):
+    """depth: epochs staged ahead (host draws, uploads and device build); slots =
+    depth + 1 sets of buffers, one being trained from."""
+
+    def __init__(self, dataset, device, batch_size, item_num, user_num=None, prefetch=True, depth=2):
         self.ds = dataset
         self.device = torch.device(device)
         self.batch_size = int(batch_size)
@@ -92,91 +102,88 @@ class EpochPipeline:
         self.pi = torch.as_tensor(pi, dtype=torch.int32).to(dev)
         self.S = self.P * self.ng
         self.n = self.P + self.S
+        self.depth = max(1, int(depth)) if prefetch else 0
+        self.prefetch = prefetch
+        K = self.depth + 1
+        # shared by the builds (issued in epoch order on one stream)
         self.rows = torch.empty(self.n, dtype=torch.int64, device=dev)
         self.perm = torch.empty(self.n, dtype=torch.int64, device=dev)
         self.fy_ws = torch.empty(int(L.hip().ncf_randperm_workspace(self.n)), dtype=torch.uint8, device=dev)
         self.prep = ops.EpochPrep(dev)
+        # per slot
+        self._out = [torch.empty(self.n, dtype=torch.int64, device=dev) for _ in range(K)]
+        self._neg_host = [torch.empty(max(1, self.S), dtype=torch.int32).pin_memory() for _ in range(K)]
+        self._words_host = [torch.empty(max(1, self.n - 1), dtype=torch.int32).pin_memory() for _ in range(K)]
+        self._neg_dev = [torch.empty(max(1, self.S), dtype=torch.int32, device=dev) for _ in range(K)]
+        self._words_dev = [torch.empty(max(1, self.n - 1), dtype=torch.int32, device=dev) for _ in range(K)]
+        self._uploaded = [None] * K  # the uploads last issued from the slot's pinned buffers
+        self._free = [None] * K      # main-stream point after which the slot's last epoch is done
+        self._next_slot = 0
+        self._cur_slot = None
+        self._pending = collections.deque()  # staged epochs, in epoch order
         self.copy_stream = torch.cuda.Stream(device=dev)
-        # two slots: one being consumed by the device, one being filled by the host
-        self._neg_host = [torch.empty(max(1, self.S), dtype=torch.int32).pin_memory() for _ in range(2)]
-        self._words_host = [torch.empty(max(1, self.n - 1), dtype=torch.int32).pin_memory() for _ in range(2)]
-        self._neg_dev = [torch.empty(max(1, self.S), dtype=torch.int32, device=dev) for _ in range(2)]
-        self._words_dev = [torch.empty(max(1, self.n - 1), dtype=torch.int32, device=dev) for _ in range(2)]
-        self._slot = 0
-        self.prefetch = prefetch
-        self._pending = None
-        self._threads = []
         self.side_stream = torch.cuda.Stream(device=dev)
         self.stats = {"epochs": 0, "prefetch_hits": 0}
-        self.events = None  # (start, rows+perm ready, grouped) of the last epoch
+        self.events = None  # (start, rows+perm built, grouped) of the last epoch
 
     # ---------------------------------------------------------------- host part
-    def _stage(self, slot, key, pos, seed, before_upload=None):
-        """Negatives from NumPy state (key, pos) and the permutation words of
-        `seed`, staged in pinned memory and uploaded (runs on worker threads)."""
-        s = _Staged(key.copy(), int(pos), seed)
+    def _take_slot(self):
+        k = self._next_slot
+        self._next_slot = (k + 1) % len(self._out)
+        return k
+
+    def _stage(self, s):
+        """Negatives from NumPy state (s.key, s.pos) and the permutation words of
+        s.seed, staged in the slot's pinned buffers and uploaded."""
+        slot = s.slot
         t_all = time.perf_counter()
         neg = self._neg_host[slot].numpy()
         words = self._words_host[slot].numpy().view(np.uint32)
 
-        def draw_negatives():
+        def draw_words():
+            t0 = time.perf_counter()
+            torch_words(s.seed, self.n - 1, words[: self.n - 1])
+            s.host_ms["words"] = (time.perf_counter() - t0) * 1e3
+
+        prev, self._uploaded[slot] = self._uploaded[slot], None
+        if prev is not None:
+            prev.synchronize()  # the slot's pinned buffers are no longer being read
+        t = threading.Thread(target=draw_words)
+        t.start()
+        try:
             t0 = time.perf_counter()
             if self.S == 0:
                 s.end_key, s.end_pos = s.key.copy(), s.pos
-                return
-            k2, p2 = s.key.copy(), np.array([s.pos], dtype=np.int32)
-            self.ds._get_sampler().sample(self.num_item, self.ng, k2, p2, out=neg[: self.S])
-            s.end_key, s.end_pos = k2, int(p2[0])
+            else:
+                k2, p2 = s.key.copy(), np.array([s.pos], dtype=np.int32)
+                self.ds._get_sampler().sample(self.num_item, self.ng, k2, p2, out=neg[: self.S])
+                s.end_key, s.end_pos = k2, int(p2[0])
             s.host_ms["sample"] = (time.perf_counter() - t0) * 1e3
-
-        def draw_words():
-            t0 = time.perf_counter()
-            torch_words(seed, self.n - 1, words[: self.n - 1])
-            s.host_ms["words"] = (time.perf_counter() - t0) * 1e3
-
-        try:
-            t = threading.Thread(target=draw_words)
-            t.start()
-            draw_negatives()
-            t.join()
-            if before_upload is not None:
-                before_upload()
-            with torch.cuda.stream(self.copy_stream):
-                if self.S:
-                    self._neg_dev[slot][: self.S].copy_(self._neg_host[slot][: self.S], non_blocking=True)
-                if self.n > 1:
-                    self._words_dev[slot][: self.n - 1].copy_(self._words_host[slot][: self.n - 1],
-                                                              non_blocking=True)
-                s.event = torch.cuda.Event()
-                s.event.record(self.copy_stream)
-        except Exception as e:  # surfaced when the epoch is consumed
-            s.error = e
-        s.host_ms["stage"] = (time.perf_counter() - t_all) * 1e3
-        return s
-
-    # ---------------------------------------------------------------- API
-    def _peek_next_seed(self, eval_draw):
-        """The next epoch's RandomSampler seed, past this epoch's metrics() draw
-        if `eval_draw` (train_neumf.py:120), consuming nothing."""
-        state = torch.get_rng_state()
-        try:
-            if eval_draw:
-                torch.empty((), dtype=torch.int64).random_()   # the test loader's base_seed
-            return epoch_permutation_seed()                     # base_seed, sampler seed
         finally:
-            torch.set_rng_state(state)
-
-    def _join(self):
-        for t in self._threads:
+            s.sampled.set()
             t.join()
-        self._threads = []
+        with torch.cuda.stream(self.copy_stream):
+            if self._free[slot] is not None:
+                self.copy_stream.wait_event(self._free[slot])  # the slot's device buffers
+            if self.S:
+                self._neg_dev[slot][: self.S].copy_(self._neg_host[slot][: self.S], non_blocking=True)
+            if self.n > 1:
+                self._words_dev[slot][: self.n - 1].copy_(self._words_host[slot][: self.n - 1], non_blocking=True)
+            s.event = torch.cuda.Event()
+            s.event.record(self.copy_stream)
+            self._uploaded[slot] = s.event
+        s.host_ms["stage"] = (time.perf_counter() - t_all) * 1e3
 
-    def _device_build(self, staged, slot, stream):
-        """On `stream` (after the staged uploads): the epoch's packed rows and its
-        permutation.  Records staged.ready."""
+    def _device_build(self, staged, stream):
+        """On `stream`, after the staged uploads and after the main stream let go of
+        the slot: the epoch's packed rows, its permutation and the batch stream
+        grouped by item, into the slot's output.  Records staged.built / .ready."""
         lib = L.hip()
+        slot = staged.slot
         st = stream.cuda_stream
         stream.wait_event(staged.event)
+        if self._free[slot] is not None:
+            stream.wait_event(self._free[slot])
         staged.t0 = torch.cuda.Event(enable_timing=True)
         staged.t0.record(stream)
         L.check(lib.ncf_build_rows(self.pu.data_ptr(), self.pi.data_ptr(), self.P,
@@ -184,81 +191,140 @@ class EpochPipeline:
                                    self.rows.data_ptr(), st), "ncf_build_rows")
         L.check(lib.ncf_randperm(self._words_dev[slot].data_ptr(), self.n, self.perm.data_ptr(),
                                  self.fy_ws.data_ptr(), self.fy_ws.numel(), st), "ncf_randperm")
+        staged.built = torch.cuda.Event(enable_timing=True)
+        staged.built.record(stream)
+        with torch.cuda.stream(stream):
+            self.prep(self.rows, self.perm, self.batch_size, self.item_num, out=self._out[slot])
         staged.ready = torch.cuda.Event(enable_timing=True)
         staged.ready.record(stream)
+
+    def _launch(self, seed, prev, key=None, pos=None):
+        """Stage the epoch after `prev` (or from (key, pos)) on a worker thread."""
+        s = _Staged(self._take_slot(), None if key is None else key.copy(), pos, seed)
+
+        def work():
+            try:
+                if s.key is None:
+                    prev.sampled.wait()
+                    if prev.end_key is None:
+                        raise RuntimeError("the previous epoch's prefetch failed")
+                    s.key, s.pos = prev.end_key.copy(), prev.end_pos
+                self._stage(s)
+                if prev is not None:
+                    prev.enqueued.wait()  # builds are issued to the side stream in epoch order
+                self._device_build(s, self.side_stream)
+            except Exception as e:  # surfaced when the epoch is consumed
+                s.error = e
+            finally:
+                s.sampled.set()
+                s.enqueued.set()
+        s.thread = threading.Thread(target=work, daemon=True)
+        s.thread.start()
+        self._pending.append(s)
+        return s
+
+    def _discard_pending(self):
+        """Drop every staged epoch (their builds still write shared buffers: wait)."""
+        first = None
+        while self._pending:
+            s = self._pending.popleft()
+            s.thread.join()
+            if s.ready is not None:
+                s.ready.synchronize()
+            first = s.slot if first is None else first
+        if first is not None:
+            self._next_slot = first
+
+    # ---------------------------------------------------------------- API
+    def _peek_seeds(self, eval_draw, count):
+        """The RandomSampler seeds of the next `count` epochs, each past a metrics()
+        draw if `eval_draw` (train_neumf.py:120), consuming nothing."""
+        state = torch.get_rng_state()
+        out = []
+        try:
+            for _ in range(count):
+                if eval_draw:
+                    torch.empty((), dtype=torch.int64).random_()   # the test loader's base_seed
+                out.append(epoch_permutation_seed())              # base_seed, sampler seed
+        finally:
+            torch.set_rng_state(state)
+        return out
 
     def next_epoch(self, peek_eval_draw=True):
         """The epoch's packed stream in batch order (device), consuming the NumPy
         global stream (ng_sample) and the torch global generator (DataLoader)
         exactly like the reference's epoch.  peek_eval_draw: a metrics() pass
-        (one torch draw) follows this epoch before the next next_epoch().
+        (one torch draw) follows each epoch before the next next_epoch().
 
-        With a prefetch hit the rows and the permutation were built on a side
-        stream while the previous epoch trained; what is left here is the
-        grouping by item (ncf_prepare_epoch) on the current stream."""
-        self._join()
+        With a prefetch hit the whole stream was built on a side stream while
+        earlier epochs trained: the current stream only waits for it.  The result
+        is one of depth + 1 rotating buffers, valid for `depth` further calls."""
+        t_enter = time.perf_counter()
         key, pos = _mt_state()
         seed = epoch_permutation_seed()  # the DataLoader's two draws
-        staged, self._pending = self._pending, None
-        if staged is not None and staged.error is not None:
-            raise staged.error
-        slot = self._slot
+        staged = self._pending.popleft() if self._pending else None
+        if staged is not None:
+            staged.thread.join()
+        t_joined = time.perf_counter()
         dev = self.device
         cur = torch.cuda.current_stream(dev)
-        if (staged is not None and staged.seed == seed and staged.pos == pos
+        if (staged is not None and staged.error is None and staged.seed == seed and staged.pos == pos
                 and np.array_equal(staged.key, key)):
             self.stats["prefetch_hits"] += 1
         else:
-            if staged is not None and staged.ready is not None:
-                staged.ready.synchronize()  # a discarded prefetch still writes rows / perm: let it finish
-            staged = self._stage(slot, key, pos, seed)
-            if staged.error is not None:
+            if staged is not None:
+                if staged.ready is not None:
+                    staged.ready.synchronize()
+                self._pending.appendleft(staged)
+            self._discard_pending()
+            if staged is not None and staged.error is not None:
                 raise staged.error
-            self._device_build(staged, slot, cur)
+            staged = _Staged(self._take_slot(), key.copy(), pos, seed)
+            try:
+                self._stage(staged)
+                self._device_build(staged, cur)
+            finally:
+                staged.sampled.set()
+                staged.enqueued.set()
+            # the builds share rows / perm / workspaces: later side-stream builds after this one
+            self.side_stream.wait_stream(cur)
         np.random.set_state(("MT19937", staged.end_key, staged.end_pos, 0, 0.0))
         cur.wait_event(staged.ready)
-        e1 = torch.cuda.Event(enable_timing=True)
-        out = self.prep(self.rows, self.perm, self.batch_size, self.item_num)
-        e1.record(cur)
-        self.events = (staged.t0, staged.ready, e1)
+        # everything that read the previous epoch's slot (its steps; a build on this
+        # stream) is enqueued before this point
+        if self._cur_slot is not None:
+            free = torch.cuda.Event()
+            free.record(cur)
+            self._free[self._cur_slot] = free
+        self._cur_slot = staged.slot
+        self.events = (staged.t0, staged.built, staged.ready)
         self.stats.setdefault("host_ms", []).append(dict(staged.host_ms))
         # the dataset's host view of this epoch's negatives (fetched only if asked for)
-        self.ds._set_device_negatives(self._neg_dev[slot][: self.S] if self.S else None)
+        self.ds._set_device_negatives(self._neg_dev[staged.slot][: self.S] if self.S else None)
         self.stats["epochs"] += 1
-        if self.prefetch:
-            nkey, npos = staged.end_key, staged.end_pos
-            nseed = self._peek_next_seed(peek_eval_draw)
-            nslot = slot ^ 1
+        if self.depth:
+            seeds = self._peek_seeds(peek_eval_draw, self.depth)
+            prev = self._pending[-1] if self._pending else staged
+            for sd in seeds[len(self._pending):]:
+                prev = self._launch(sd, prev)
+        t_out = time.perf_counter()
+        self.stats.setdefault("boundary_ms", []).append(((t_joined - t_enter) * 1e3, (t_out - t_joined) * 1e3))
+        return self._out[staged.slot]
 
-            def work():
-                # host draws first; the uploads and the device build wait until this
-                # epoch's grouping has read rows / perm (the other slot's buffers were
-                # read by the epoch before)
-                s = self._stage(nslot, nkey, npos, nseed, before_upload=e1.synchronize)
-                if s.error is None:
-                    try:
-                        self._device_build(s, nslot, self.side_stream)
-                    except Exception as e:  # surfaced when the epoch is consumed
-                        s.error = e
-                self._pending = s
-            t = threading.Thread(target=work, daemon=True)
-            t.start()
-            self._threads.append(t)
-            self._slot = nslot
-        return out
+    @property
+    def buffers(self):
+        """The output buffers next_epoch() rotates through."""
+        return list(self._out)
 
     def device_ms(self):
-        """(rows + permutation, grouping) device milliseconds of the last epoch: the
-        first runs on the side stream under the previous epoch's steps when the
-        prefetch hit, the second on the current stream at the boundary."""
+        """(rows + permutation, grouping) device milliseconds of the last epoch's
+        build (on the side stream, under earlier epochs' steps, when the prefetch
+        hit)."""
         if self.events is None:
             return None
-        t0, ready, e1 = self.events
-        e1.synchronize()
-        return t0.elapsed_time(ready), ready.elapsed_time(e1)
+        t0, built, ready = self.events
+        ready.synchronize()
+        return t0.elapsed_time(built), built.elapsed_time(ready)
 
     def close(self):
-        self._join()
-        if self._pending is not None and self._pending.ready is not None:
-            self._pending.ready.synchronize()
-        self._pending = None
+        self._discard_pending()

@@ -75,6 +75,7 @@ class Trainer:
                 from .pipeline import EpochPipeline
                 self._pipe = EpochPipeline(self.ds, self.device, self.batch_size, int(self.model.item_num),
                                                  user_num=int(self.model.user_num))
+                self.engine.stream_buffers = self._pipe.buffers  # step graphs captured for both
             # fit() evaluates after every epoch (one torch draw): the next epoch's
             # sampler seed is peeked past it
             return self._pipe.next_epoch(peek_eval_draw=True)

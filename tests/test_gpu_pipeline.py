@@ -65,8 +65,10 @@ def test_randperm_structured_words(kind):
     assert np.array_equal(_randperm(w, n).numpy(), _fisher_yates(w, n))
 
 
-def test_pipeline_epochs_equal_host_path():
-    """Three epochs with prefetch and an eval draw between them, vs the host path."""
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_pipeline_epochs_equal_host_path(depth):
+    """Five epochs with prefetch `depth` epochs ahead and an eval draw between
+    them, vs the host path (rotating output buffers: each checked when returned)."""
     from ncf_amd import ops
     from ncf_amd.data import consume_test_pass, epoch_permutation
     from ncf_amd.pipeline import EpochPipeline
@@ -77,7 +79,8 @@ def test_pipeline_epochs_equal_host_path():
     torch.manual_seed(3)
     ds = _dataset(pu, pi, I, 4)
     exp = []
-    for _ in range(3):
+    E = 5
+    for _ in range(E):
         ds.ng_sample()
         u, i, y = ds.arrays()
         perm = epoch_permutation(len(u)).numpy()
@@ -87,14 +90,14 @@ def test_pipeline_epochs_equal_host_path():
     np.random.seed(3)
     torch.manual_seed(3)
     ds2 = _dataset(pu, pi, I, 4)
-    pipe = EpochPipeline(ds2, DEV, B, I, user_num=U)
-    for e in range(3):
+    pipe = EpochPipeline(ds2, DEV, B, I, user_num=U, depth=depth)
+    for e in range(E):
         got = pipe.next_epoch(peek_eval_draw=True).cpu().numpy()
         for b0 in range(0, len(got), B):
             assert np.array_equal(np.sort(got[b0:b0 + B]), np.sort(exp[e][b0:b0 + B])), (e, b0)
         consume_test_pass()
     pipe.close()
-    assert pipe.stats["prefetch_hits"] == 2
+    assert pipe.stats["prefetch_hits"] == E - 1
     u2, i2, _ = ds2.arrays()  # host views of the device negatives
     assert np.array_equal(ops.pack_rows_host(u2, i2, ds2.arrays()[2]), ops.pack_rows_host(*ds.arrays()))
     st = np.random.get_state()
@@ -137,3 +140,31 @@ def test_pipeline_discards_prefetch_after_foreign_draws():
             torch.rand(3)
     pipe.close()
     assert pipe.stats["prefetch_hits"] == 0
+
+
+def test_engine_captures_every_pipeline_buffer_once():
+    """The engine captures the step graphs for all of the pipeline's rotating
+    output buffers at its first capture; later epoch boundaries replay them."""
+    from ncf_amd import synthetic
+    from ncf_amd.engine import TrainEngine
+    from ncf_amd.models import NCF
+    from ncf_amd.pipeline import EpochPipeline
+    d = synthetic.make_dataset("ml-100k", seed=2)
+    pu, pi, I, U, B = d["train_users"], d["train_items"], d["item_num"], d["user_num"], 8192
+    np.random.seed(5)
+    torch.manual_seed(5)
+    model = NCF(U, I, 8, 3, 0.0, "NeuMF-end").to(DEV)
+    pipe = EpochPipeline(_dataset(pu, pi, I, 4), DEV, B, I, user_num=U, depth=2)
+    eng = TrainEngine(model, lr=1e-3)
+    eng.stream_buffers = pipe.buffers
+    seen = set()
+    for _ in range(5):
+        rows = pipe.next_epoch(peek_eval_draw=False)
+        seen.add(rows.data_ptr())
+        eng.set_epoch_stream(rows, B, checked=True)
+        eng.run(eng.num_batches)
+        assert len(eng._graphs) == len(pipe.buffers)
+    pipe.close()
+    torch.cuda.synchronize()
+    assert seen == {b.data_ptr() for b in pipe.buffers}
+    assert np.isfinite(eng.epoch_losses()).all()
