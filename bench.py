@@ -70,8 +70,9 @@ def gather_scatter_bytes_per_row(f, L):
 def adam_info(kt, eng, model):
     """The optimizer launch and the bytes it moves.  Dense Adam over the embedding
     tables: 32 B/param (read p, g, m, v; write p, m, v, g = 0).  ncf_reduce_adam_step
-    also reads the per-workgroup tower slab (fused path: ncf_slab_rows rows; layered:
-    one row) and, on the factored path, the expansion's dW0 partials, and runs Adam
+    also reads the tower slab (ncf_reduce_rows rows: the fused step's workgroups, or
+    the layered path's atomic-spreading rows) and, on the factored path, the
+    expansion's dW0 partials (ncf_fact_partials_bytes), and runs Adam
     on the tower straight from those sums (24 B/param: read p, m, v; write p, m, v)."""
     import ncf_amd._lib as L
     from ncf_amd import ops
@@ -80,13 +81,10 @@ def adam_info(kt, eng, model):
     emb = sum(p.numel() for p, act in zip(list(model.ordered_params())[:4], ops.active_mask(model)[:4]) if act)
     tower = sum(p.numel() for p in list(model.ordered_params())[4:])
     stride = int(lib.ncf_slab_stride(L.ctypes.byref(lay)))
-    fused = L.supported(model.model_type, model.factor_num, model.num_layers) == L.PATH_FUSED
-    wg = (int(lay.flags) >> L.LAYOUT_WG_SHIFT) & L.LAYOUT_WG_MASK  # ncf_layout_tune's workgroup count
-    slab_rows = (wg if 0 < wg < int(lib.ncf_slab_rows()) else int(lib.ncf_slab_rows())) if fused else 1
-    partial = 0
+    slab_rows = int(lib.ncf_reduce_rows(L.ctypes.byref(lay)))
+    partial = int(lib.ncf_fact_partials_bytes(L.ctypes.byref(lay)))
     slab_cols = stride
     if ops.fact_mode(lay):
-        partial = int(lib.ncf_workspace_bytes(L.ctypes.byref(lay), 1)) - int(lib.ncf_slab_rows()) * stride * 4
         slab_cols = stride - (int(lay.b[0]) - int(lay.w[0]))  # W0's columns come from the partials
     if "ncf_reduce_adam_step" in kt:
         b = 32 * emb + 24 * tower + slab_rows * slab_cols * 4 + partial
@@ -191,6 +189,12 @@ def make_train_data(cfg, seed=0):
     ds = synthetic.make_dataset(shape, seed=seed)
     train = NCFData(np.stack([ds["train_users"], ds["train_items"]], 1), ds["item_num"], None, 4, True)
     return ds, train
+
+
+def engine_for(cfg, dev, global_batch, world=1, rank=0, group=None):
+    """(engine, model, pipeline) of config `cfg` at `global_batch` (diagnostic scripts)."""
+    ds, train = make_train_data(cfg)
+    return setup_engine(cfg, ds, train, world, rank, dev, group, global_batch)
 
 
 def setup_engine(cfg, ds, train, world, rank, dev, group, global_batch, seed=0):

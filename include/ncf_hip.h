@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 9
+#define NCF_ABI_VERSION 10
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -193,9 +193,10 @@ int ncf_pack_rows(const int32_t *users, const int32_t *items, const float *label
                   uint64_t *rows_out, void *stream);
 
 /*
- * Factored layer 0 (MLP shapes with a fused kernel and user_num + item_num <= 32768):
- * there the fused kernel scatter-adds, per row, the layer-0 pre-activation gradient
- * D0 (width dm) into the user and item rows of grads[um] / grads[im] instead of
+ * Factored layer 0 (MLP shapes with user_num + item_num <= 32768 and dm in
+ * {8, 16, 32, 64, 128}, unless NCF_LAYOUT_PER_ROW_L0; ncf_fact_mode says whether it
+ * runs): the step scatter-adds, per row, the layer-0 pre-activation gradient D0
+ * (width dm) into the user and item rows of grads[um] / grads[im] instead of
  * forming the layer-0 weight and data gradients per row, and a second launch turns
  * those row sums into the true gradients (from the same params the step used):
  *   dUm = G W0[:, :dm],  dIm = H W0[:, dm:]   (in place),
@@ -209,6 +210,20 @@ int ncf_pack_rows(const int32_t *users, const int32_t *items, const float *label
  * (NCF_OK) so an ABI-7 sequence that still calls it trains correctly.
  */
 int ncf_expand_grads(const ncf_layout *lay, const float *params, float *grads, void *workspace, void *stream);
+
+/* 1 if ncf_train_step runs the factored layer 0 for this layout (fused path, or
+ * since ABI 10 the layered path too: there the layer-0 forward is a per-step
+ * projection of both tables through W0, P = [Um W0[:, :dm]^T ; Im W0[:, dm:]^T],
+ * gathered per row), else 0.  The train workspace then holds the dW0 partials after
+ * the slab (ncf_workspace_bytes includes them). */
+int ncf_fact_mode(const ncf_layout *lay);
+
+/* Rows of the partial slab ncf_reduce_slab / ncf_reduce_adam_step sum for this
+ * layout (fused: the step's workgroups, ncf_layout_tune; layered: up to 16 rows the
+ * weight-gradient and predict blocks spread their atomics over), and the bytes of
+ * dW0 partials after it (0 unless ncf_fact_mode).  Since ABI 10. */
+int ncf_reduce_rows(const ncf_layout *lay);
+int64_t ncf_fact_partials_bytes(const ncf_layout *lay);
 
 /* p[0 .. n) = 0 with a kernel (no memset node in a captured graph); p 16-byte aligned,
  * n a multiple of 4.  Zeroes the local gradient bucket after the data-parallel

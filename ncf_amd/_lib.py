@@ -29,7 +29,7 @@ NCF_E_ARG = -2
 NCF_E_LAUNCH = -3
 MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
 DZ_BCE, DZ_DLOGIT, DZ_KD = 0, 1, 2
-ABI_VERSION = 9  # include/ncf_hip.h NCF_ABI_VERSION
+ABI_VERSION = 10  # include/ncf_hip.h NCF_ABI_VERSION
 PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 LAYOUT_PER_ROW_L0, LAYOUT_WG_SHIFT, LAYOUT_WG_MASK = 0x1, 8, 0xFFF  # ncf_layout.flags (ncf_layout_tune)
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
@@ -92,6 +92,9 @@ _HIP_PROTOS = {
     "ncf_prepare_epoch_workspace": (c_i64, [c_i64, c_i64, ctypes.c_int]),
     "ncf_prepare_epoch": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, ctypes.c_int, c_vp, c_vp, c_i64, c_vp]),
     "ncf_hr_ndcg": (ctypes.c_int, [c_vp, c_vp, c_i64, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
+    "ncf_fact_mode": (ctypes.c_int, [c_vp]),
+    "ncf_reduce_rows": (ctypes.c_int, [c_vp]),
+    "ncf_fact_partials_bytes": (c_i64, [c_vp]),
     "ncf_randperm_workspace": (c_i64, [c_i64]),
     "ncf_randperm": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "ncf_build_rows": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, ctypes.c_int, c_vp, c_vp]),

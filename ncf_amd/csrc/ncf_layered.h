@@ -11,6 +11,17 @@ constexpr int LYR_MAX_FACTOR = 256;  // predict kernel: <= 4 features per lane
 
 static inline int64_t rup64(int64_t x) { return (x + 63) / 64 * 64; }
 
+// Rows of the layered path's partial slab [rows][tower_len + 64]: blocks that add
+// the same tower partials (weight-gradient row splits, predict blocks) spread their
+// float atomics over the rows (block index mod rows) instead of queueing on one
+// address; the reductions sum the rows in a fixed order.  As many rows as fit
+// 4M floats, at most 16.
+__host__ __device__ static inline int lyr_slab_rows(const ncf_layout* lay) {
+    const int64_t stride = lay->tower_len + 64;
+    int64_t r = ((int64_t)4 << 20) / stride;
+    return (int)(r < 1 ? 1 : (r > 16 ? 16 : r));
+}
+
 struct LyrArgs {
     ncf_layout lay;
     const float* params;
@@ -21,15 +32,18 @@ struct LyrArgs {
     int64_t batch_global, fwd_n;
     int world, rank, dz_mode;
     float kd_wt, kd_wr, kd_temp;  // NCF_DZ_KD: task / response weights, temperature; dlogit = teacher logits
-    float* slab;             // one row [tower_len + 64] of tower/predict partials (+ loss)
+    float* slab;             // lyr_slab_rows() rows [tower_len + 64] of tower/predict partials (+ loss)
     float* logits_out;       // optional per-row logits
+    int64_t fact_part_floats;  // train: >= 0 factored layer 0 (that many floats of dW0 partials
+                               // follow the slab row, filled by fact_expand_kernel); -1 per-row
 };
 
 // p[0 .. n) = 0 (n % 4 == 0, p 16-byte aligned) on stream st.
 int launch_zero_f32(float* p, int64_t n, hipStream_t st);
 
-// Workspace floats for `rows` rows per launch (slab row + activations [+ dY buffers]).
-int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train);
+// Workspace floats for `rows` rows per launch: slab row [+ dW0 partials + table
+// projections (factored layer 0, fact_part_floats >= 0)] + activations [+ dY buffers].
+int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train, int64_t fact_part_floats);
 
 // Launch the layered forward (train = false) or forward + BCE + backward (train = true)
 // over at most R rows; ws = lyr_workspace_floats(lay, R, train) floats.

@@ -13,6 +13,16 @@
 //   lyr_bwd_data<FIRST>   dY_{k-1} = (dY_k W_k) * [H_k > 0], or for k = 0 the
 //                         Um/Im embedding scatter-add
 //
+// Factored layer 0 (train, tables of at most FACT_MAX_ROWS rows, ncf_ops.hip
+// fact_mode): with W0 = [W0u | W0i] the layer-0 pre-activation of a row is
+// Um[u] W0u^T + Im[i] W0i^T, so
+//   lyr_proj              P = [Um W0u^T ; Im W0i^T]     (U + I rows, once per step)
+//   lyr_fwd0_fact         H_1 = ReLU(P[u] + P[U + i] + b_0)   (a gather per row)
+//   lyr_scatter0          dY_0 rows scatter-added into the user / item rows of the
+//                         gradient buffer (item runs summed first), db_0
+// and fact_expand_kernel (ncf_ops.hip) turns those per-row-sum rows into dUm, dIm
+// and the dW0 partials -- three (U + I)-row GEMMs in place of three B-row ones.
+//
 // All three GEMM shapes run on one MFMA core: v_mfma_f32_16x16x4f32 (exact
 // fp32), 256 threads = 4 waves, 64x64 block tile, each wave a 32x32 sub-tile
 // (2x2 MFMA tiles), K in steps of 16 through double-buffered LDS.  Operand
@@ -258,7 +268,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
     if (r1 > s.nloc) r1 = s.nloc;  // padding rows carry dY = 0
     if (r0 >= r1) return;          // block-uniform
     const float* prm = a.params;
-    float* slab = a.slab;
+    float* slab = a.slab + (int64_t)(blockIdx.z % lyr_slab_rows(&lay)) * (lay.tower_len + 64);
     const int64_t tb = lay.tower_begin;
     auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
 #pragma unroll
@@ -315,6 +325,142 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
             return c == K ? 1.f : Ain[m * K + c];
         };
         gemm_block<false, false>(j0, c0, r0, r1, ga, gb, ep);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Factored layer 0.  Projection: P[r][n] = sum_c X[r][c] W0[n][koff + c] over the
+// user rows (blocks [0, nbu), X = Um, koff = 0) then the item rows (X = Im,
+// koff = DM); grid (nbu + nbi, ceil(DM / 64)).
+__global__ __launch_bounds__(GNT) void lyr_proj_kernel(LyrArgs a, float* __restrict__ P, int nbu) {
+    const ncf_layout& lay = a.lay;
+    const int DM = lay.factor_num << (lay.num_layers - 1);
+    const bool user = (int)blockIdx.x < nbu;
+    const int64_t nrows = user ? lay.user_num : lay.item_num;
+    const int64_t m0 = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * GBM;
+    const int n0 = blockIdx.y * GBN;
+    const float* X = a.params + (user ? lay.um : lay.im);
+    const float* W = a.params + lay.w[0] + (user ? 0 : DM);  // row stride 2 DM
+    float* Pout = P + (user ? 0 : (int64_t)lay.user_num * DM);
+    auto ga = [&](int r, int64_t c) -> float {
+        const int64_t m = m0 + r;
+        return (m < nrows && c < DM) ? X[m * DM + c] : 0.f;
+    };
+    auto gb = [&](int64_t c, int n) -> float {
+        const int nn = n0 + n;
+        return (nn < DM && c < DM) ? W[(int64_t)nn * 2 * DM + c] : 0.f;
+    };
+    auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) {
+                const int n = n0 + wn + 16 * tj + (l & 15);
+                if (n >= DM) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t m = m0 + wm + 16 * ti + 4 * (l >> 4) + r;
+                    if (m < nrows) Pout[m * DM + n] = lane_get(acc[ti][tj], r);
+                }
+            }
+    };
+    gemm_block<true, true>(m0, n0, 0, DM, ga, gb, ep);
+}
+
+// H_1[m][n] = ReLU(P[u_m][n] + P[U + i_m][n] + b_0[n]), four outputs per thread
+// (padding rows gather id 0, as lyr_fwd_kernel<true>).
+__global__ __launch_bounds__(GNT) void lyr_fwd0_fact_kernel(LyrArgs a, const float* __restrict__ P,
+                                                            float* __restrict__ H1, int64_t R) {
+    const Sel s = select_rows(a);
+    const ncf_layout& lay = a.lay;
+    const int DM = lay.factor_num << (lay.num_layers - 1);
+    const int q4 = DM / 4;
+    const float* b0 = a.params + lay.b[0];
+    const float* Pi = P + (int64_t)lay.user_num * DM;
+    for (int64_t e = (int64_t)blockIdx.x * GNT + threadIdx.x; e < R * q4; e += (int64_t)gridDim.x * GNT) {
+        const int64_t m = e / q4;
+        const int n = 4 * (int)(e - m * q4);
+        int u, it;
+        row_ids(a, s, m, u, it);
+        u = u < 0 ? 0 : u;
+        it = it < 0 ? 0 : it;
+        const f4 pu = *reinterpret_cast<const f4*>(P + (int64_t)u * DM + n);
+        const f4 pi = *reinterpret_cast<const f4*>(Pi + (int64_t)it * DM + n);
+        const f4 bb = *reinterpret_cast<const f4*>(b0 + n);
+        f4 h;
+        h.x = fmaxf(pu.x + pi.x + bb.x, 0.f);
+        h.y = fmaxf(pu.y + pi.y + bb.y, 0.f);
+        h.z = fmaxf(pu.z + pi.z + bb.z, 0.f);
+        h.w = fmaxf(pu.w + pi.w + bb.w, 0.f);
+        *reinterpret_cast<f4*>(H1 + m * DM + n) = h;
+    }
+}
+
+// dY_0 rows -> grads[um][u] and grads[im][i] (width DM), db_0 -> slab.  A walker of
+// 32 lanes takes SC_ROWS consecutive rows (lane = feature, + 32 per column group):
+// its rows' values are loaded first, then the walk sums runs of equal items (each
+// batch is grouped by item, ncf_prepare_epoch) before their atomics; users add per
+// row.  db_0: walker sums -> LDS -> one atomic per feature per block.
+constexpr int SC_LANES = 32, SC_ROWS = 16, SC_COLS = 4;  // DM <= 128
+__global__ __launch_bounds__(GNT) void lyr_scatter0_kernel(LyrArgs a, const float* __restrict__ D0) {
+    __shared__ float sdb[GNT / SC_LANES][SC_LANES * SC_COLS];
+    const Sel s = select_rows(a);
+    const ncf_layout& lay = a.lay;
+    const int DM = lay.factor_num << (lay.num_layers - 1);
+    const int lane = threadIdx.x % SC_LANES, wk = threadIdx.x / SC_LANES;
+    const int64_t r0 = ((int64_t)blockIdx.x * (GNT / SC_LANES) + wk) * SC_ROWS;
+    float db[SC_COLS];
+#pragma unroll
+    for (int q = 0; q < SC_COLS; ++q) db[q] = 0.f;
+    if (r0 < s.nloc) {
+        const int nr = (int)(s.nloc - r0 < SC_ROWS ? s.nloc - r0 : SC_ROWS);
+        int us[SC_ROWS], is[SC_ROWS];
+        float v[SC_ROWS][SC_COLS];
+#pragma unroll
+        for (int k = 0; k < SC_ROWS; ++k) {
+            const int64_t m = r0 + (k < nr ? k : 0);
+            const uint64_t rw = a.rows[s.base + m];
+            us[k] = (int)(uint32_t)rw;
+            is[k] = us[k] < 0 ? -1 : (int)((rw >> 32) & 0x7fffffffu);  // row_ids: padding rows add nothing
+#pragma unroll
+            for (int q = 0; q < SC_COLS; ++q) {
+                const int n = lane + SC_LANES * q;
+                v[k][q] = (n < DM) ? D0[m * DM + n] : 0.f;
+            }
+        }
+        float run[SC_COLS];
+#pragma unroll
+        for (int q = 0; q < SC_COLS; ++q) run[q] = 0.f;
+#pragma unroll
+        for (int k = 0; k < SC_ROWS; ++k) {
+            const bool in = k < nr;
+            const bool end = k + 1 >= nr || is[k + 1 < SC_ROWS ? k + 1 : k] != is[k];  // item run ends here
+#pragma unroll
+            for (int q = 0; q < SC_COLS; ++q) {
+                const int n = lane + SC_LANES * q;
+                if (in && n < DM) {
+                    db[q] += v[k][q];
+                    if (us[k] >= 0) atomicAdd(a.grads + lay.um + (int64_t)us[k] * DM + n, v[k][q]);
+                    run[q] += v[k][q];
+                    if (end) {
+                        if (is[k] >= 0) atomicAdd(a.grads + lay.im + (int64_t)is[k] * DM + n, run[q]);
+                        run[q] = 0.f;
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < SC_COLS; ++q) sdb[wk][lane + SC_LANES * q] = db[q];
+    __syncthreads();
+    for (int n = threadIdx.x; n < DM; n += GNT) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < GNT / SC_LANES; ++k) t += sdb[k][n];
+        if (t != 0.f)
+            atomicAdd(a.slab + (int64_t)(blockIdx.x % lyr_slab_rows(&lay)) * (lay.tower_len + 64) +
+                          (lay.b[0] - lay.tower_begin) + n,
+                      t);
     }
 }
 
@@ -428,7 +574,7 @@ __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float
             const float v = red[e];
             if (v == 0.f) continue;
             const int64_t off = e < P ? (lay.wp - tb) + e : (e == P ? (lay.bp - tb) : lay.tower_len);
-            atomicAdd(a.slab + off, v);
+            atomicAdd(a.slab + (int64_t)(blockIdx.x % lyr_slab_rows(&lay)) * (lay.tower_len + 64) + off, v);
         }
     }
 }
@@ -436,10 +582,12 @@ __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float
 }  // namespace
 
 // ---------------------------------------------------------------------------
-int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train) {
-    int64_t fl = rup64(lay->tower_len + 64);
+int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train, int64_t fact_part_floats) {
+    int64_t fl = rup64((int64_t)lyr_slab_rows(lay) * (lay->tower_len + 64));
     if (lay->model_type == NCF_MODEL_GMF) return fl;
     const int DM = lay->factor_num << (lay->num_layers - 1);
+    if (train && fact_part_floats >= 0)  // dW0 partials, table projections
+        fl += rup64(fact_part_floats) + rup64(((int64_t)lay->user_num + lay->item_num) * DM);
     for (int k = 1; k <= lay->num_layers; ++k) fl += rup64(rows * ((2 * DM) >> k));
     if (train) fl += 2 * rup64(rows * DM);
     return fl;
@@ -457,7 +605,15 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
     float* H[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     float* Da = nullptr;
     float* Db = nullptr;
-    int64_t off = rup64(lay.tower_len + 64);
+    const int64_t slab_floats = (int64_t)lyr_slab_rows(&lay) * (lay.tower_len + 64);
+    int64_t off = rup64(slab_floats);
+    const bool fact = train && mlp && a.fact_part_floats >= 0;
+    float* Pj = nullptr;  // factored layer 0: table projections
+    if (fact) {
+        off += rup64(a.fact_part_floats);  // dW0 partials (ncf_ops.hip fact_partials)
+        Pj = ws + off;
+        off += rup64(((int64_t)lay.user_num + lay.item_num) * DM);
+    }
     if (mlp) {
         for (int k = 1; k <= L; ++k) {
             H[k] = ws + off;
@@ -469,13 +625,20 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             Db = ws + off;
         }
     }
-    if (train && launch_zero_f32(slab, lay.tower_len + 64, st) != NCF_OK) return NCF_E_LAUNCH;
+    if (train && launch_zero_f32(slab, slab_floats, st) != NCF_OK) return NCF_E_LAUNCH;
     const unsigned mt = (unsigned)((R + GBM - 1) / GBM);
     if (mlp) {
         for (int k = 0; k < L; ++k) {
             const int N = (2 * DM) >> (k + 1);
             const dim3 grid(mt, (unsigned)((N + GBN - 1) / GBN));
-            if (k == 0)
+            if (k == 0 && fact) {
+                const int nbu = (int)((lay.user_num + GBM - 1) / GBM), nbi = (int)((lay.item_num + GBM - 1) / GBM);
+                hipLaunchKernelGGL(lyr_proj_kernel, dim3((unsigned)(nbu + nbi), (unsigned)((DM + GBN - 1) / GBN)),
+                                   dim3(GNT), 0, st, a, Pj, nbu);
+                int64_t g0 = (R * (DM / 4) + GNT - 1) / GNT;
+                if (g0 > 8192) g0 = 8192;
+                hipLaunchKernelGGL(lyr_fwd0_fact_kernel, dim3((unsigned)g0), dim3(GNT), 0, st, a, Pj, H[1], R);
+            } else if (k == 0)
                 hipLaunchKernelGGL(lyr_fwd_kernel<true>, grid, dim3(GNT), 0, st, a, k, nullptr, H[1], R);
             else
                 hipLaunchKernelGGL(lyr_fwd_kernel<false>, grid, dim3(GNT), 0, st, a, k, H[k], H[k + 1], R);
@@ -501,6 +664,12 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
     float* Dnext = Db;
     for (int k = L - 1; k >= 0; --k) {
         const int K = (2 * DM) >> k, J = K / 2;
+        if (k == 0 && fact) {  // dY_0 into the table rows; dW0 / dUm / dIm by fact_expand_kernel
+            const int64_t per_block = (int64_t)(GNT / SC_LANES) * SC_ROWS;
+            hipLaunchKernelGGL(lyr_scatter0_kernel, dim3((unsigned)((R + per_block - 1) / per_block)), dim3(GNT), 0,
+                               st, a, Dcur);
+            break;
+        }
         // weight gradient: split the rows so the launch has ~512 blocks
         const int64_t tiles = (int64_t)((J + GBM - 1) / GBM) * ((K + 1 + GBN - 1) / GBN);
         int64_t splits = 1024 / tiles;

@@ -769,7 +769,7 @@ __global__ __launch_bounds__(256) void kd_feature_kernel(KdFeatArgs a) {
 // ---------------------------------------------------------------------------
 // Factored layer 0 (ncf_train.hip, FACT): the step left G_u = sum of the D0 rows
 // of user u in grads[um] and H_i in grads[im] (width DM = S(1)).  fact_expand_kernel
-// turns them into the true gradients; one block per FX_CH-row chunk of one table X
+// turns them into the true gradients; one block per cpb consecutive CH-row chunks of one table X
 // (X = Um with koff = 0, or Im with koff = DM), its G and X rows and the W0 half it
 // needs staged in LDS once, 16 waves each owning output tiles:
 //   dX = G W0[:, koff : koff + DM]   (16 x 16 tiles), written over G
@@ -779,94 +779,132 @@ __global__ __launch_bounds__(256) void kd_feature_kernel(KdFeatArgs a) {
 // partials of each half in block order (deterministic, no atomics: every block's
 // partial covers the same 16 KB of W0, so float atomics would serialise on it).  v_mfma_f32_16x16x4_f32 throughout:
 // (U + I)/16 tile GEMMs per step in place of the per-row layer-0 dgrad / wgrad of B/16.
-constexpr int FX_WAVES = 16;  // one 16x16 output tile of dW0 and one of dX per wave (DM = 64)
-constexpr int FX_CH = 64;     // table rows per block
+constexpr int FX_WAVES = 16;  // 16 waves: dW0 / dX output tiles dealt round-robin
+
+// Chunk rows per LDS pass: 64 up to DM = 64, 32 at DM = 128 (W0 half + 3 chunk
+// images = 118 KB).  A block walks `cpb` consecutive chunks of one table with the
+// W0 half staged once and its dW0 partial held in registers across them.
+template <int DM>
+struct FxShape {
+    static constexpr int CH = DM <= 64 ? 64 : 32;
+    static constexpr int ST = DM + 4, NT = (DM + 15) / 16, Q4 = DM / 4;
+    static constexpr int TPW = (NT * NT + FX_WAVES - 1) / FX_WAVES;  // dW0 tiles per wave
+    static constexpr int64_t LDS = ((int64_t)DM * ST + 3LL * CH * ST) * 4;
+};
 
 template <int DM>
 __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout lay, const float* __restrict__ prm,
                                                                      float* __restrict__ grads,
-                                                                     float* __restrict__ partials, int nbu) {
-    constexpr int ST = DM + 4, NT = (DM + 15) / 16, Q4 = DM / 4;
+                                                                     float* __restrict__ partials, int nbu, int cpb) {
+    using X_ = FxShape<DM>;
+    constexpr int CH = X_::CH, ST = X_::ST, NT = X_::NT, Q4 = X_::Q4, TPW = X_::TPW;
     extern __shared__ __attribute__((aligned(16))) float fsm[];
-    float* sW = fsm;              // W0[:, koff : koff + DM]  [DM][ST]
-    float* sG = sW + DM * ST;     // G rows  [FX_CH][ST]
-    float* sX = sG + FX_CH * ST;  // X rows  [FX_CH][ST]
-    float* sO = sX + FX_CH * ST;  // dX rows [FX_CH][ST]
+    float* sW = fsm;           // W0[:, koff : koff + DM]  [DM][ST]
+    float* sG = sW + DM * ST;  // G rows  [CH][ST]
+    float* sX = sG + CH * ST;  // X rows  [CH][ST]
+    float* sO = sX + CH * ST;  // dX rows [CH][ST]
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, c = l & 15, g = l >> 4;
     const bool user = (int)blockIdx.x < nbu;
     const int64_t nrows = user ? lay.user_num : lay.item_num;
     const int64_t xoff = user ? lay.um : lay.im;
     const int koff = user ? 0 : DM;
-    const int64_t r0 = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * FX_CH;
-    {   // the W0 half, the chunk's G and X rows -> LDS: each thread's loads issued together
-        constexpr int NW4 = DM * Q4, PW = (NW4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
-        constexpr int NR4 = FX_CH * Q4, PR = (NR4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
-        f4 wv[PW], gv[PR], xv[PR];
+    const int64_t rb = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * cpb * CH;  // first row of the block
+    // the W0 half: loads issued here, stored to LDS behind the first chunk's loads
+    constexpr int NW4 = DM * Q4, PW = (NW4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
+    f4 wv[PW];
 #pragma unroll
-        for (int q = 0; q < PW; ++q) {
-            const int e4 = tid + q * FX_WAVES * 64, j = e4 / Q4, k4 = e4 - j * Q4;
-            wv[q] = e4 < NW4 ? *reinterpret_cast<const f4*>(prm + lay.w[0] + (int64_t)j * 2 * DM + koff + 4 * k4)
-                             : f4{0.f, 0.f, 0.f, 0.f};
-        }
+    for (int q = 0; q < PW; ++q) {
+        const int e4 = tid + q * FX_WAVES * 64, j = e4 / Q4, k4 = e4 - j * Q4;
+        wv[q] = e4 < NW4 ? *reinterpret_cast<const f4*>(prm + lay.w[0] + (int64_t)j * 2 * DM + koff + 4 * k4)
+                         : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    f4 accw[TPW];
 #pragma unroll
-        for (int q = 0; q < PR; ++q) {
-            const int e4 = tid + q * FX_WAVES * 64, row = e4 / Q4, k4 = e4 - row * Q4;
-            const bool ok = e4 < NR4 && r0 + row < nrows;
-            gv[q] = ok ? *reinterpret_cast<const f4*>(grads + xoff + (r0 + row) * DM + 4 * k4) : f4{0.f, 0.f, 0.f, 0.f};
-            xv[q] = ok ? *reinterpret_cast<const f4*>(prm + xoff + (r0 + row) * DM + 4 * k4) : f4{0.f, 0.f, 0.f, 0.f};
-        }
+    for (int q = 0; q < TPW; ++q) accw[q] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int ch = 0; ch < cpb; ++ch) {
+        const int64_t r0 = rb + (int64_t)ch * CH;
+        if (r0 >= nrows) break;  // block-uniform
+        if (ch > 0) __syncthreads();  // the previous chunk's images are consumed
+        {   // the chunk's G and X rows -> LDS (each thread's loads issued together)
+            constexpr int NR4 = CH * Q4, PR = (NR4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
+            f4 gv[PR], xv[PR];
 #pragma unroll
-        for (int q = 0; q < PW; ++q) {
-            const int e4 = tid + q * FX_WAVES * 64, j = e4 / Q4, k4 = e4 - j * Q4;
-            if (e4 < NW4) *reinterpret_cast<f4*>(sW + j * ST + 4 * k4) = wv[q];
-        }
+            for (int q = 0; q < PR; ++q) {
+                const int e4 = tid + q * FX_WAVES * 64, row = e4 / Q4, k4 = e4 - row * Q4;
+                const bool ok = e4 < NR4 && r0 + row < nrows;
+                gv[q] = ok ? *reinterpret_cast<const f4*>(grads + xoff + (r0 + row) * DM + 4 * k4)
+                           : f4{0.f, 0.f, 0.f, 0.f};
+                xv[q] = ok ? *reinterpret_cast<const f4*>(prm + xoff + (r0 + row) * DM + 4 * k4)
+                           : f4{0.f, 0.f, 0.f, 0.f};
+            }
+            if (ch == 0) {
 #pragma unroll
-        for (int q = 0; q < PR; ++q) {
-            const int e4 = tid + q * FX_WAVES * 64, row = e4 / Q4, k4 = e4 - row * Q4;
-            if (e4 < NR4) {
-                *reinterpret_cast<f4*>(sG + row * ST + 4 * k4) = gv[q];
-                *reinterpret_cast<f4*>(sX + row * ST + 4 * k4) = xv[q];
+                for (int q = 0; q < PW; ++q) {
+                    const int e4 = tid + q * FX_WAVES * 64, j = e4 / Q4, k4 = e4 - j * Q4;
+                    if (e4 < NW4) *reinterpret_cast<f4*>(sW + j * ST + 4 * k4) = wv[q];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < PR; ++q) {
+                const int e4 = tid + q * FX_WAVES * 64, row = e4 / Q4, k4 = e4 - row * Q4;
+                if (e4 < NR4) {
+                    *reinterpret_cast<f4*>(sG + row * ST + 4 * k4) = gv[q];
+                    *reinterpret_cast<f4*>(sX + row * ST + 4 * k4) = xv[q];
+                }
             }
         }
-    }
-    __syncthreads();
-    // dW0 partial, tiles (mt, nt) dealt round-robin to the waves:
-    // A[i = j][k = row] = G[row][j],  B[k = row][n = k'] = X[row][k']
-    for (int tt = w; tt < NT * NT; tt += FX_WAVES) {
-        const int mt = tt / NT, nt = tt - mt * NT;
-        const bool jok = 16 * mt + c < DM, kok = 16 * nt + c < DM;
-        f4 a0 = f4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+        __syncthreads();
+        // dW0 partial, tiles (mt, nt) dealt round-robin to the waves:
+        // A[i = j][k = row] = G[row][j],  B[k = row][n = k'] = X[row][k']
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            const int tt = w + q * FX_WAVES;
+            if (tt >= NT * NT) break;
+            const int mt = tt / NT, nt = tt - mt * NT;
+            const bool jok = 16 * mt + c < DM, kok = 16 * nt + c < DM;
+            f4 a0 = accw[q], a1 = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-        for (int s4 = 0; s4 < FX_CH / 4; s4 += 2) {
-            const int ra = 4 * s4 + g, rb = ra + 4;
-            a0 = MFMA4(jok ? sG[ra * ST + 16 * mt + c] : 0.f, kok ? sX[ra * ST + 16 * nt + c] : 0.f, a0);
-            a1 = MFMA4(jok ? sG[rb * ST + 16 * mt + c] : 0.f, kok ? sX[rb * ST + 16 * nt + c] : 0.f, a1);
+            for (int s4 = 0; s4 < CH / 4; s4 += 2) {
+                const int ra = 4 * s4 + g, rb2 = ra + 4;
+                a0 = MFMA4(jok ? sG[ra * ST + 16 * mt + c] : 0.f, kok ? sX[ra * ST + 16 * nt + c] : 0.f, a0);
+                a1 = MFMA4(jok ? sG[rb2 * ST + 16 * mt + c] : 0.f, kok ? sX[rb2 * ST + 16 * nt + c] : 0.f, a1);
+            }
+            a0.x += a1.x; a0.y += a1.y; a0.z += a1.z; a0.w += a1.w;
+            accw[q] = a0;
         }
-        a0.x += a1.x; a0.y += a1.y; a0.z += a1.z; a0.w += a1.w;
-        float* pb = partials + (int64_t)blockIdx.x * DM * DM;
+        // dX = G W0h, tiles (rt, nt): A[i = row][k = j] = G[row][j],  B[k = j][n = k'] = W0h[j][k']
+        for (int tt = w; tt < (CH / 16) * NT; tt += FX_WAVES) {
+            const int rt = tt / NT, nt = tt - rt * NT;
+            const bool nok = 16 * nt + c < DM;
+            f4 d = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int j = 16 * mt + 4 * g + q;
-            if (j < DM && kok) pb[j * DM + 16 * nt + c] = lane_get(a0, q);
+            for (int kk = 0; kk < DM / 4; ++kk)
+                d = MFMA4(sG[(16 * rt + c) * ST + 4 * kk + g], nok ? sW[(4 * kk + g) * ST + 16 * nt + c] : 0.f, d);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (nok) sO[(16 * rt + 4 * g + q) * ST + 16 * nt + c] = lane_get(d, q);
+        }
+        __syncthreads();
+        for (int e = tid; e < CH * Q4; e += FX_WAVES * 64) {
+            const int row = e / Q4, q = e - row * Q4;
+            if (r0 + row < nrows)
+                *reinterpret_cast<f4*>(grads + xoff + (r0 + row) * DM + 4 * q) =
+                    *reinterpret_cast<const f4*>(sO + row * ST + 4 * q);
         }
     }
-    // dX = G W0h, tiles (rt, nt): A[i = row][k = j] = G[row][j],  B[k = j][n = k'] = W0h[j][k']
-    for (int tt = w; tt < (FX_CH / 16) * NT; tt += FX_WAVES) {
-        const int rt = tt / NT, nt = tt - rt * NT;
-        const bool nok = 16 * nt + c < DM;
-        f4 d = f4{0.f, 0.f, 0.f, 0.f};
+    // the block's dW0 partial: plain stores (every block covers the same W0 half)
+    float* pb = partials + (int64_t)blockIdx.x * DM * DM;
 #pragma unroll
-        for (int kk = 0; kk < DM / 4; ++kk)
-            d = MFMA4(sG[(16 * rt + c) * ST + 4 * kk + g], nok ? sW[(4 * kk + g) * ST + 16 * nt + c] : 0.f, d);
+    for (int q = 0; q < TPW; ++q) {
+        const int tt = w + q * FX_WAVES;
+        if (tt >= NT * NT) break;
+        const int mt = tt / NT, nt = tt - mt * NT;
+        const bool kok = 16 * nt + c < DM;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (nok) sO[(16 * rt + 4 * g + q) * ST + 16 * nt + c] = lane_get(d, q);
-    }
-    __syncthreads();
-    for (int e = tid; e < FX_CH * Q4; e += FX_WAVES * 64) {
-        const int row = e / Q4, q = e - row * Q4;
-        if (r0 + row < nrows)
-            *reinterpret_cast<f4*>(grads + xoff + (r0 + row) * DM + 4 * q) = *reinterpret_cast<const f4*>(sO + row * ST + 4 * q);
+        for (int r = 0; r < 4; ++r) {
+            const int j = 16 * mt + 4 * g + r;
+            if (j < DM && kok) pb[j * DM + 16 * nt + c] = lane_get(accw[q], r);
+        }
     }
 }
 
@@ -880,10 +918,12 @@ int launch_zero_f32(float* p, int64_t n, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
 }
 
-// Factored layer 0 for this layout?  Fused MLP shapes whose two embedding tables
-// have fewer rows than FACT_MAX_ROWS (the expand pass works on U + I rows per step,
-// the per-row layer-0 gradients on B rows: at ml-1m 9.7K vs 65K; at ml-20m the
-// tables have 165K rows and the per-row form stays).
+// Factored layer 0 for this layout?  MLP shapes whose two embedding tables have
+// fewer rows than FACT_MAX_ROWS (the expand pass works on U + I rows per step, the
+// per-row layer-0 gradients on B rows: at ml-1m 9.7K vs 65K; at ml-20m the tables
+// have 165K rows and the per-row form stays), on the fused path or, for DM up to
+// 128, the layered one (there the layer-0 forward is a per-step projection of the
+// tables too, ncf_layered.hip).
 #ifndef NCF_FACT_MAX_ROWS
 #define NCF_FACT_MAX_ROWS 32768
 #endif
@@ -894,10 +934,15 @@ static const KernelEntry* fused_entry(const ncf_layout* lay) {
     if (!e) return nullptr;
     return train_lds_floats(e, lay) * 4 <= LDS_LIMIT_BYTES ? e : nullptr;
 }
+static int fact_dm(const ncf_layout* lay) { return lay->factor_num << (lay->num_layers - 1); }
 static bool fact_mode(const ncf_layout* lay) {
+    if (lay->model_type == NCF_MODEL_GMF || (lay->flags & NCF_LAYOUT_PER_ROW_L0)) return false;
+    if ((int64_t)lay->user_num + lay->item_num > FACT_MAX_ROWS) return false;
+    const int dm = fact_dm(lay);
+    if (dm != 8 && dm != 16 && dm != 32 && dm != 64 && dm != 128) return false;  // fact_expand_kernel<DM>
     const KernelEntry* e = fused_entry(lay);
-    return e != nullptr && e->train_fact != nullptr && lay->model_type != NCF_MODEL_GMF &&
-           (int64_t)lay->user_num + lay->item_num <= FACT_MAX_ROWS && !(lay->flags & NCF_LAYOUT_PER_ROW_L0);
+    if (e) return e->train_fact != nullptr;
+    return lay->factor_num <= LYR_MAX_FACTOR;
 }
 
 // Workgroups of the fused step = rows of the slab the reductions read.
@@ -913,8 +958,12 @@ static int slab_lo(const ncf_layout* lay) {
     return 0;
 }
 
+static int fact_ch(const ncf_layout* lay) { return fact_dm(lay) <= 64 ? 64 : 32; }  // FxShape<DM>::CH
+static int fact_cpb(const ncf_layout* lay) { return fact_dm(lay) <= 64 ? 1 : 4; }   // chunks per block
+
 static int fact_blocks(const ncf_layout* lay, int* nbu) {
-    const int bu = (int)((lay->user_num + FX_CH - 1) / FX_CH), bi = (int)((lay->item_num + FX_CH - 1) / FX_CH);
+    const int64_t per = (int64_t)fact_ch(lay) * fact_cpb(lay);
+    const int bu = (int)((lay->user_num + per - 1) / per), bi = (int)((lay->item_num + per - 1) / per);
     *nbu = bu;
     return bu + bi;
 }
@@ -925,11 +974,23 @@ static int64_t fact_partials_floats(const ncf_layout* lay) {
     return (int64_t)fact_blocks(lay, &nbu) * DM * DM;
 }
 
+// The dW0 partials in the train workspace: after the fused path's slab rows, or
+// after the layered path's single slab row (ncf_layered.hip).
+static float* fact_partials(const ncf_layout* lay, void* workspace) {
+    const int64_t stride = lay->tower_len + 64;
+    return static_cast<float*>(workspace) +
+           (fused_entry(lay) ? (int64_t)SLAB_ROWS * stride : rup64((int64_t)lyr_slab_rows(lay) * stride));
+}
+
+// Rows of the partial slab the reductions sum: the fused step's workgroups, or the
+// layered path's lyr_slab_rows.
+static int reduce_rows(const ncf_layout* lay) { return fused_entry(lay) ? slab_rows_of(lay) : lyr_slab_rows(lay); }
+
 static W0Part w0_part(const ncf_layout* lay, const void* workspace) {
     W0Part wp;
     memset(&wp, 0, sizeof(wp));
     if (!fact_mode(lay)) return wp;
-    wp.p = static_cast<const float*>(workspace) + (int64_t)SLAB_ROWS * (lay->tower_len + 64);
+    wp.p = fact_partials(lay, const_cast<void*>(workspace));
     wp.nblk = fact_blocks(lay, &wp.nbu);
     wp.dm = lay->factor_num << (lay->num_layers - 1);
     wp.cols = (int)(lay->b[0] - lay->w[0]);
@@ -940,18 +1001,19 @@ static int launch_fact_expand(const ncf_layout* lay, const float* params, float*
                               hipStream_t st) {
     const int DM = lay->factor_num << (lay->num_layers - 1);
     const void* fe;
+    int64_t lds;
     switch (DM) {
-#define NCF_FX(D) case D: fe = reinterpret_cast<const void*>(&fact_expand_kernel<D>); break;
-        NCF_FX(8) NCF_FX(16) NCF_FX(32) NCF_FX(64)
+#define NCF_FX(D) case D: fe = reinterpret_cast<const void*>(&fact_expand_kernel<D>); lds = FxShape<D>::LDS; break;
+        NCF_FX(8) NCF_FX(16) NCF_FX(32) NCF_FX(64) NCF_FX(128)
 #undef NCF_FX
         default: return NCF_E_UNSUPPORTED;
     }
     ncf_layout l = *lay;
     int nbu;
     int nblk = fact_blocks(lay, &nbu);
-    const int64_t lds = ((int64_t)DM * (DM + 4) + 3LL * FX_CH * (DM + 4)) * 4;
+    int cpb = fact_cpb(lay);
     if (ensure_lds(fe, lds) != NCF_OK) return NCF_E_LAUNCH;
-    void* ae[] = {&l, (void*)&params, (void*)&grads, (void*)&partials, &nbu};
+    void* ae[] = {&l, (void*)&params, (void*)&grads, (void*)&partials, &nbu, &cpb};
     if (hipLaunchKernel(fe, dim3((unsigned)nblk), dim3(FX_WAVES * 64), ae, (size_t)lds, st) != hipSuccess)
         return NCF_E_LAUNCH;
     return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
@@ -976,6 +1038,14 @@ int ncf_debug_set_stamps(unsigned long long* dev_buf) {
 }
 
 int ncf_slab_rows(void) { return SLAB_ROWS; }
+
+int ncf_fact_mode(const ncf_layout* lay) { return lay && fact_mode(lay) ? 1 : 0; }
+
+int ncf_reduce_rows(const ncf_layout* lay) { return lay ? reduce_rows(lay) : -1; }
+
+int64_t ncf_fact_partials_bytes(const ncf_layout* lay) {
+    return lay && fact_mode(lay) ? fact_partials_floats(lay) * 4 : 0;
+}
 
 int ncf_layout_tune(ncf_layout* lay, int64_t rows) {
     if (!lay || rows <= 0) return NCF_E_ARG;
@@ -1028,13 +1098,13 @@ int64_t ncf_workspace_bytes(const ncf_layout* lay, int64_t rows) {
     if (!lay || rows < 0) return -1;
     if (fused_entry(lay))
         return ((int64_t)SLAB_ROWS * ncf_slab_stride(lay) + (fact_mode(lay) ? fact_partials_floats(lay) : 0)) * 4;
-    return lyr_workspace_floats(lay, rows, true) * 4;
+    return lyr_workspace_floats(lay, rows, true, fact_mode(lay) ? fact_partials_floats(lay) : -1) * 4;
 }
 
 int64_t ncf_forward_workspace_bytes(const ncf_layout* lay, int64_t n) {
     if (!lay || n < 0) return -1;
     if (fused_entry(lay)) return 0;
-    return lyr_workspace_floats(lay, n, false) * 4;
+    return lyr_workspace_floats(lay, n, false, -1) * 4;
 }
 
 static int train_step_impl(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
@@ -1067,7 +1137,10 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
         la.kd_wr = kd_wr;
         la.kd_temp = kd_temp;
         la.logits_out = logits_out;
-        return lyr_run(la, slab, rows_max, true, (hipStream_t)stream);
+        la.fact_part_floats = fact_mode(lay) ? fact_partials_floats(lay) : -1;
+        const int rc = lyr_run(la, slab, rows_max, true, (hipStream_t)stream);
+        if (rc != NCF_OK || la.fact_part_floats < 0) return rc;
+        return launch_fact_expand(lay, params, grads, fact_partials(lay, workspace), (hipStream_t)stream);
     }
     const int64_t lds = train_lds_floats(e, lay) * 4;
     if (lds > LDS_LIMIT_BYTES) return NCF_E_UNSUPPORTED;
@@ -1100,8 +1173,7 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
     const int rc = launch_status();
     if (rc != NCF_OK || !fact_mode(lay)) return rc;
     // factored layer 0: the per-user / per-item D0 sums -> dUm, dIm, dW0 partials
-    float* partials = slab + (int64_t)SLAB_ROWS * ncf_slab_stride(lay);
-    return launch_fact_expand(lay, params, grads, partials, (hipStream_t)stream);
+    return launch_fact_expand(lay, params, grads, fact_partials(lay, workspace), (hipStream_t)stream);
 }
 
 int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
@@ -1175,6 +1247,7 @@ int ncf_forward(const ncf_layout* lay, const float* params, const uint64_t* rows
         la.fwd_n = n;
         la.world = 1;
         la.logits_out = logits;
+        la.fact_part_floats = -1;
         return lyr_run(la, static_cast<float*>(workspace), n, false, (hipStream_t)stream);
     }
     const int64_t lds = (int64_t)(e->w_total + e->misc) * 4;
@@ -1204,7 +1277,7 @@ int ncf_reduce_slab(const ncf_layout* lay, const void* workspace, float* grads, 
     const int stride = (int)ncf_slab_stride(lay);
     const int lo = slab_lo(lay);
     const int blocks = (stride - lo + 63) / 64;
-    const int rows = fused_entry(lay) ? slab_rows_of(lay) : 1;  // the layered path accumulates into one row
+    const int rows = reduce_rows(lay);
     hipLaunchKernelGGL(reduce_slab_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab,
                        grads + lay->tower_begin, lo, stride, rows, ctl, w0_part(lay, workspace));
     return launch_status();
@@ -1256,7 +1329,7 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
     const int stride = (int)ncf_slab_stride(lay);
     const int lo = slab_lo(lay);
     const int nA = (stride - lo + 63) / 64;
-    const int rows = fused_entry(lay) ? slab_rows_of(lay) : 1;
+    const int rows = reduce_rows(lay);
     const int64_t etotal = RE.prefix[RE.n];
     int64_t nB = (etotal + 255) / 256;
     if (nB > 2048) nB = 2048;

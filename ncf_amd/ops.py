@@ -181,12 +181,9 @@ def forward_logits(flat, lay, rows, out=None, ws_owner=None):
 
 
 def fact_mode(lay):
-    """Whether the factored layer-0 path runs for this layout (its train workspace
-    holds the expansion's dW0 partials after the slab; include/ncf_hip.h)."""
-    lib = L.hip()
-    slab = lib.ncf_slab_rows() * lib.ncf_slab_stride(L.ctypes.byref(lay)) * 4
-    return L.supported(int(lay.model_type), int(lay.factor_num), int(lay.num_layers)) == L.PATH_FUSED and \
-        lib.ncf_workspace_bytes(L.ctypes.byref(lay), 1) > slab
+    """Whether the factored layer-0 path runs for this layout (include/ncf_hip.h
+    ncf_fact_mode; fused or layered path)."""
+    return bool(L.hip().ncf_fact_mode(L.ctypes.byref(lay)))
 
 
 def new_workspace(lay, rows, dev):

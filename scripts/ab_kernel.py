@@ -21,7 +21,7 @@ def child(cfg):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     per = bench.CONFIGS[cfg][3]
-    eng, _, _, _ = bench.setup_engine(cfg, 1, 0, dev, None, per)
+    eng, _, _ = bench.engine_for(cfg, dev, per)
     eng.run(3, use_graph=False)
     ts = sorted(eng.time_train_kernel(40) for _ in range(5))
     print("RESULT", ts[len(ts) // 2])

@@ -22,8 +22,8 @@ def main():
     torch.cuda.set_device(dev)
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
     res = {}
-    for rows in (65536, 16384):
-        eng, model, ds, _ = bench.setup_engine(cfg, 1, 0, dev, None, rows)
+    for rows in ([int(x) for x in sys.argv[2].split(',')] if len(sys.argv) > 2 else (65536, 16384)):
+        eng, model, _ = bench.engine_for(cfg, dev, rows)
         eng.run(3, use_graph=False)
         torch.cuda.synchronize()
         variants = {"full": 0, "no_wgrad": 2, "no_user_scatter": 8, "no_item_scatter": 16,

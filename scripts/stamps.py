@@ -32,10 +32,12 @@ def main():
     import ncf_amd._lib as L
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    rows = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-    eng, model, ds, _ = bench.setup_engine("c3", 1, 0, dev, None, rows)
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    rows = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+    eng, model, _ = bench.engine_for(cfg, dev, rows)
     eng.run(5, use_graph=False)
-    nwg = L.hip().ncf_slab_rows()
+    wg = (int(eng.lay.flags) >> L.LAYOUT_WG_SHIFT) & L.LAYOUT_WG_MASK
+    nwg = wg if wg else L.hip().ncf_slab_rows()
     buf = torch.zeros(nwg * 64, dtype=torch.int64, device=dev)
     since = {}
     spread = []
@@ -62,7 +64,7 @@ def main():
         res[name] = {"delta_cycles_median": t - prev, "since_start": t}
         prev = t
     sp = np.median(np.array(spread), axis=0).tolist() if spread else []
-    print(json.dumps({"rows": rows, "phases": res,
+    print(json.dumps({"config": cfg, "rows": rows, "workgroups": int(nwg), "phases": res,
                       "wg_duration_cycles_p0_p10_p50_p90_max": sp}))
 
 

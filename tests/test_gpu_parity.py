@@ -135,8 +135,9 @@ def _fact_mode(lay):
     return ops.fact_mode(lay)
 
 
-def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3):
-    """Logits, loss and every gradient of one fused step vs the oracle."""
+def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3, flags=0):
+    """Logits, loss and every gradient of one fused step vs the oracle.  flags: OR-ed
+    into a copy of the layout (e.g. NCF_LAYOUT_PER_ROW_L0)."""
     import ncf_amd._lib as L
     from ncf_amd import ops
     ref, m = _models(mt, f, Lyr, U=U, I=I, seed=seed)
@@ -146,6 +147,9 @@ def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3):
     labels = (rng.random(B) < 0.2).astype(np.int64)
     logits_ref, loss_ref, grads_ref = O.forward_backward(ref, users, items, labels)
     flat, lay = ops.ensure_flat(m)
+    if flags:
+        lay = type(lay).from_buffer_copy(lay)
+        lay.flags |= flags
     gflat = torch.zeros(int(lay.total), device=DEV)
     ws = ops.new_workspace(lay, B, DEV)
     ctl = ops.new_ctl(B, DEV)
@@ -162,10 +166,17 @@ def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3):
     torch.cuda.synchronize()
     np.testing.assert_allclose(logits.cpu().numpy(), logits_ref.numpy(), rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(gflat[lay.loss_slot].item(), loss_ref, rtol=1e-5)
+    fact = ops.fact_mode(lay)
     for (p, off), (name, _) in zip(ops._segments(m, lay), m.named_parameters()):
         got = gflat[off:off + p.numel()].view_as(p).cpu().numpy()
         if name in grads_ref:
             hot = int(np.bincount(items).max()) if "item" in name else int(np.bincount(users).max())
+            if fact and name == "MLP_layers.1.weight":
+                # factored layer 0: dW0 = sum_u G_u^T Um[u] (+ items), G_u summed by float
+                # atomics in arrival order -- the embedding tables' rounding model
+                hot = max(int(np.bincount(items).max()), int(np.bincount(users).max()))
+                _close_grad(got, grads_ref[name].numpy(), name, terms=hot)
+                continue
             _close_grad(got, grads_ref[name].numpy(), name, terms=hot if "embed" in name else None)
         else:  # unused in this model type (reference grad None): nothing may be written
             assert not got.any(), name
@@ -198,6 +209,46 @@ def test_one_step_fact_boundary(U, I, fact):
     per-row layer-0 kernels give the same gradients."""
     lay = _one_step("NeuMF-end", 16, 3, 8192, U, I, seed=14)
     assert _fact_mode(lay) == fact
+
+
+@pytest.mark.parametrize("mt,f,Lyr,B", [("NeuMF-end", 32, 3, 65536), ("NeuMF-end", 32, 3, 8192),
+                                        ("MLP", 32, 3, 8192), ("NeuMF-end", 16, 4, 8192)])
+def test_one_step_layered_factored_layer0(mt, f, Lyr, B):
+    """Layered path with the factored layer 0 (ABI 10: table projections through W0,
+    per-row gather, D0 row sums expanded by fact_expand_kernel; dm = 128 for
+    NCF(32,3) and NCF(16,4)) at ml-1m ids, and the same shape forced per-row
+    (NCF_LAYOUT_PER_ROW_L0): both vs the oracle."""
+    import ncf_amd._lib as L
+    assert L.supported(mt, f, Lyr) == L.PATH_LAYERED
+    lay = _one_step(mt, f, Lyr, B, 6041, 3707, seed=19)
+    assert _fact_mode(lay)
+    lay = _one_step(mt, f, Lyr, min(B, 8192), 6041, 3707, seed=19, flags=L.LAYOUT_PER_ROW_L0)
+    assert not _fact_mode(lay)
+
+
+def test_engine_layered_factored_trajectory_vs_oracle():
+    """NCF(32,3) (the CLI default shape) on the factored layered path at ml-1m ids:
+    6 engine Adam steps of 8,192 rows (hipGraph) free-running
+    (_assert_trajectory_close), then every step teacher-forced."""
+    T, B = 6, 8192
+    ref, m, eng = _engine_for("NeuMF-end", 32, 3, 6041, 3707, 23)
+    rng = np.random.default_rng(47)
+    users = rng.integers(0, 6041, (T, B))
+    items = np.minimum(rng.zipf(1.3, (T, B)) - 1, 3706)
+    labels = (rng.random((T, B)) < 0.2).astype(np.int64)
+    _stream(eng, users, items, labels, B)
+    assert _fact_mode(eng.lay)
+    ref0 = {k: v.clone() for k, v in ref.state_dict().items()}
+    eng.run(T, use_graph=True)
+    torch.cuda.synchronize()
+    got_losses = eng.epoch_losses()[:T].copy()
+    got = {k: v.cpu().numpy().copy() for k, v in m.state_dict().items()}
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    np.testing.assert_allclose(got_losses, O.train_steps(ref, opt, users, items, labels), rtol=1e-5)
+    for k, r in ref.state_dict().items():
+        _assert_trajectory_close(got[k], r.numpy(), T, 1e-3, k)
+    ref.load_state_dict(ref0)
+    _teacher_forced_steps(ref, m, eng, users, items, labels)
 
 
 def _assert_trajectory_close(got, exp, T, lr, name):

@@ -55,7 +55,18 @@ def test_abi_version_and_layout():
     ws = L.hip().ncf_workspace_bytes(ctypes.byref(lay), 65536)
     dm = 64 * 8
     acts = 65536 * (dm + dm // 2 + dm // 4 + dm // 8) + 2 * 65536 * dm
-    assert acts * 4 <= ws <= (acts + lay.tower_len + 64 * 8) * 4
+    rows = L.hip().ncf_reduce_rows(ctypes.byref(lay))  # layered: slab rows the atomics spread over
+    assert 1 <= rows <= 16 and L.hip().ncf_fact_partials_bytes(ctypes.byref(lay)) == 0  # dm 512: per-row layer 0
+    assert acts * 4 <= ws <= (acts + rows * (lay.tower_len + 64) + 64 * 8) * 4
+    # NCF(32,3) at ml-1m: factored layer 0 on the layered path (ABI 10): the
+    # workspace adds the dW0 partials and the two tables' projections
+    lay = L.layout(6041, 3707, 32, 3, "NeuMF-end")
+    assert L.hip().ncf_fact_mode(ctypes.byref(lay)) == 1
+    pb = L.hip().ncf_fact_partials_bytes(ctypes.byref(lay))
+    assert pb > 0 and pb % (128 * 128 * 4) == 0
+    ws = L.hip().ncf_workspace_bytes(ctypes.byref(lay), 65536)
+    acts = 65536 * (128 + 64 + 32) + 2 * 65536 * 128 + (6041 + 3707) * 128
+    assert ws >= acts * 4 + pb
     assert L.hip().ncf_forward_workspace_bytes(ctypes.byref(L.layout(6041, 3707, 16, 3, "NeuMF-end")), 10 ** 6) == 0
 
 
