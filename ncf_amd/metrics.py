@@ -30,6 +30,16 @@ def _hr_ndcg_device(logits, items_i32, batch, top_k):
     return hr, nd
 
 
+def evaluate_rows_device(model, rows, items_i32, batch, top_k):
+    """Per-batch HR (int32) and NDCG (float32) on the device for a packed candidate
+    stream whose ids the caller has checked; nothing is synchronised."""
+    from . import ops
+    flat, lay = ops.ensure_flat(model)
+    with torch.no_grad():
+        logits = ops.forward_logits(flat, lay, rows, ws_owner=model)
+    return _hr_ndcg_device(logits, items_i32, batch, top_k)
+
+
 def evaluate_arrays(model, users, items, batch, top_k):
     """HR/NDCG lists for a flat candidate stream cut into `batch`-row batches."""
     from . import ops

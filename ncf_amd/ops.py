@@ -13,6 +13,8 @@ module's ``state_dict`` / stock optimizers keep working.
 """
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 import torch
 
@@ -26,6 +28,23 @@ def _segments(model, lay):
         offs += [lay.w[k], lay.b[k]]
     offs += [lay.wp, lay.bp]
     return list(zip(model.ordered_params(), offs))
+
+
+@contextlib.contextmanager
+def params_view(model, flat_snapshot):
+    """The model's parameters temporarily viewing `flat_snapshot` (a copy of its
+    flat buffer): e.g. a checkpoint of the parameters as an earlier step left them
+    while later steps are already queued.  Nothing may repack the model inside."""
+    lay = model._ncf_layout
+    segs = _segments(model, lay)
+    saved = [p.data for p, _ in segs]
+    try:
+        for p, off in segs:
+            p.data = flat_snapshot[off:off + p.numel()].view_as(p)
+        yield model
+    finally:
+        for (p, _), d in zip(segs, saved):
+            p.data = d
 
 
 def active_mask(model):

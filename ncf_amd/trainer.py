@@ -30,7 +30,7 @@ import torch
 from . import ops
 from .data import NCFData, consume_test_pass, epoch_permutation
 from .engine import TrainEngine
-from .metrics import evaluate_arrays
+from .metrics import evaluate_rows_device
 
 
 class Trainer:
@@ -110,13 +110,28 @@ class Trainer:
                               int(sizes[0]))
         return self._test
 
+    def _test_device(self):
+        """The test candidate stream packed on the device, ids checked once
+        (nn.Embedding's IndexError, models.py:108-112)."""
+        if getattr(self, "_test_dev", None) is None:
+            u, i, bs = self._test_arrays()
+            ops.check_ids(u, i, int(self.model.user_num), int(self.model.item_num))
+            ud = torch.as_tensor(u, dtype=torch.int32).to(self.device)
+            idv = torch.as_tensor(i, dtype=torch.int32).to(self.device)
+            self._test_dev = (ops.pack_rows(ud, idv), idv, bs)
+        return self._test_dev
+
+    def _evaluate_device(self, top_k=None):
+        k = self.top_k if top_k is None else int(top_k)
+        rows, items, bs = self._test_device()
+        consume_test_pass()  # the test DataLoader iteration's base_seed draw
+        return evaluate_rows_device(self.model, rows, items, bs, k)
+
     # ------------------------------------------------------------------ API
     def evaluate(self, top_k=None):
         """metrics(model, test_loader, top_k) (metrics.py:4-25): per-batch HR/NDCG lists."""
-        k = self.top_k if top_k is None else int(top_k)
-        u, i, bs = self._test_arrays()
-        consume_test_pass()  # the test DataLoader iteration's base_seed draw
-        return evaluate_arrays(self.model, u, i, bs, k)
+        hr, nd = self._evaluate_device(top_k)
+        return hr.cpu().tolist(), nd.double().cpu().tolist()
 
     def train_epoch(self):
         rows = self._epoch_stream()
@@ -124,28 +139,75 @@ class Trainer:
         self.engine.run(self.engine.num_batches, use_graph=self.use_graph)
         return float(np.mean(self.engine.epoch_losses()))
 
-    def fit(self, epochs, model_type=None, pretraining=False, save_fn=None):
-        best_hr = best_ndcg = 0
-        best_epoch = 0
-        for epoch in range(int(epochs)):
-            self.model.train()
-            t0 = time.time()
-            avg_loss = self.train_epoch()
-            self.model.eval()
-            if self.rank == 0:
-                HR, NDCG = self.evaluate()
-                hr, ndcg = float(np.mean(HR)), float(np.mean(NDCG))
-            else:
-                consume_test_pass()
-                hr = ndcg = 0.0
-            el = time.time() - t0
-            self.history.append({"epoch": epoch + 1, "loss": avg_loss, "hr": hr, "ndcg": ndcg, "time": el})
-            if self.verbose:
-                print(f"Epoch {epoch + 1:03d}: Loss={avg_loss:.4f}, HR={hr:.3f}, NDCG={ndcg:.3f}, Time={el:.1f}s")
-            if hr > best_hr:
-                best_hr, best_ndcg, best_epoch = hr, ndcg, epoch + 1
-                if save_fn is not None and self.rank == 0:
+    def _report(self, epoch, avg_loss, hr, ndcg, el, save_fn, snap):
+        self.history.append({"epoch": epoch + 1, "loss": avg_loss, "hr": hr, "ndcg": ndcg, "time": el})
+        if self.verbose:
+            print(f"Epoch {epoch + 1:03d}: Loss={avg_loss:.4f}, HR={hr:.3f}, NDCG={ndcg:.3f}, Time={el:.1f}s")
+        if hr > self._best[0]:
+            self._best = [hr, ndcg, epoch + 1]
+            if save_fn is not None and self.rank == 0:
+                if snap is None:
                     save_fn(self.model)
+                else:
+                    with ops.params_view(self.model, snap):  # the parameters as that epoch ended
+                        save_fn(self.model)
+
+    def _report_pending(self, pending, save_fn):
+        epoch, ev0, ev1, out, snap = pending
+        ev1.synchronize()
+        avg_loss = float(np.mean(out["loss"].numpy().astype(np.float64)))
+        hr = float(np.mean(out["hr"].numpy().astype(np.float64)))
+        ndcg = float(np.mean(out["nd"].numpy().astype(np.float64)))
+        self._report(epoch, avg_loss, hr, ndcg, ev0.elapsed_time(ev1) / 1e3, save_fn, snap)
+
+    def fit(self, epochs, model_type=None, pretraining=False, save_fn=None):
+        """The reference loop (train_neumf.py:98-144).  Single rank: epoch e's loss,
+        HR and NDCG are copied to pinned host buffers as the epoch ends (and, with a
+        save_fn, the parameters to a device snapshot), epoch e + 1 is enqueued, and
+        only then is epoch e read back, printed and checkpointed -- the same values,
+        the same generator draws in the same order, no idle device between epochs.
+        Time= is the epoch's device time (steps + evaluation)."""
+        self._best = [0, 0, 0]  # hr, ndcg, epoch
+        if self.world_size > 1:  # the loss readback is a collective there: in line
+            for epoch in range(int(epochs)):
+                self.model.train()
+                t0 = time.time()
+                avg_loss = self.train_epoch()
+                self.model.eval()
+                if self.rank == 0:
+                    HR, NDCG = self.evaluate()
+                    hr, ndcg = float(np.mean(HR)), float(np.mean(NDCG))
+                else:
+                    consume_test_pass()
+                    hr = ndcg = 0.0
+                self._report(epoch, avg_loss, hr, ndcg, time.time() - t0, save_fn, None)
+        else:
+            pending = None
+            for epoch in range(int(epochs)):
+                self.model.train()
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
+                rows = self._epoch_stream()
+                self.engine.set_epoch_stream(rows, self.batch_size, checked=True)
+                self.engine.run(self.engine.num_batches, use_graph=self.use_graph)
+                self.model.eval()
+                nb = self.engine.num_batches
+                out = {"loss": torch.empty(nb, dtype=torch.float32).pin_memory()}
+                out["loss"].copy_(self.engine.loss_hist[:nb], non_blocking=True)
+                hr_d, nd_d = self._evaluate_device()
+                out["hr"] = torch.empty(hr_d.numel(), dtype=torch.int32).pin_memory()
+                out["nd"] = torch.empty(nd_d.numel(), dtype=torch.float32).pin_memory()
+                out["hr"].copy_(hr_d, non_blocking=True)
+                out["nd"].copy_(nd_d, non_blocking=True)
+                snap = self.engine.flat.clone() if save_fn is not None else None
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record()
+                if pending is not None:
+                    self._report_pending(pending, save_fn)
+                pending = (epoch, ev0, ev1, out, snap)
+            if pending is not None:
+                self._report_pending(pending, save_fn)
+        best_hr, best_ndcg, best_epoch = self._best
         n_params = sum(p.numel() for p in self.model.parameters() if p.requires_grad)
         return {
             "best_hr": best_hr,
