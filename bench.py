@@ -279,7 +279,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--skip-cpu-baseline", action="store_true")
     ap.add_argument("--skip-eval", action="store_true")
-    ap.add_argument("--e2e-epochs", type=int, default=4, help="Trainer.fit epochs for the e2e figure (0: skip)")
+    ap.add_argument("--e2e-epochs", type=int, default=8, help="Trainer.fit epochs for the e2e figure (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

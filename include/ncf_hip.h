@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 10
+#define NCF_ABI_VERSION 11
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -65,6 +65,9 @@ typedef struct ncf_layout {
     int64_t total; /* floats in the flat buffer, loss slot included */
     int32_t user_num, item_num, factor_num, num_layers, model_type;
     int32_t flags; /* 0 from ncf_layout_init; ncf_layout_tune sets the launch shape */
+    float dropout;         /* training steps: nn.Dropout(p) before every tower Linear (0: none) */
+    uint32_t dropout_seed; /* keep mask of (seed, adam_t, layer, epoch-stream row, column):
+                              ncf_dropout_keep; since ABI 11 */
 } ncf_layout;
 
 /* ncf_layout.flags (set by ncf_layout_tune; every entry point reads them from the
@@ -223,6 +226,22 @@ int ncf_fact_mode(const ncf_layout *lay);
  * weight-gradient and predict blocks spread their atomics over), and the bytes of
  * dW0 partials after it (0 unless ncf_fact_mode).  Since ABI 10. */
 int ncf_reduce_rows(const ncf_layout *lay);
+
+/*
+ * Dropout (models.py:23, nn.Dropout(p) before each of the L tower Linears; p > 0 in
+ * lay->dropout): training steps (ncf_train_step[_kd]) with p > 0 run the layered
+ * path with per-row layer 0; element (row r of the epoch stream, column c) of the
+ * input of tower layer k is kept, at optimizer step t = ctl->adam_t, when
+ * ncf_dropout_hash(seed, t, k, r, c) >= p * 2^32, and scaled by 1.0f / (1.0f - p)
+ * (torch's inverted dropout).  The mask depends on the global row, so every rank
+ * and every batch split sees the same one.  torch's own dropout draws from its
+ * Philox stream, which is not reproduced: masks are not the reference's bits (parity
+ * of the arithmetic given a mask is tested; the mask's statistics too).
+ *   h = seed << 32 ^ t * 0x9E3779B97F4A7C15 ^ r * 0xBF58476D1CE4E5B9
+ *       ^ (k << 16 | c) * 0x94D049BB133111EB  (64-bit wrap), then the splitmix64
+ *   finalizer; the hash is its upper 32 bits.  Host-side: the same function.
+ */
+uint32_t ncf_dropout_hash(uint32_t seed, uint32_t t, uint32_t layer, int64_t row, uint32_t col);
 int64_t ncf_fact_partials_bytes(const ncf_layout *lay);
 
 /* p[0 .. n) = 0 with a kernel (no memset node in a captured graph); p 16-byte aligned,

@@ -29,7 +29,7 @@ NCF_E_ARG = -2
 NCF_E_LAUNCH = -3
 MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
 DZ_BCE, DZ_DLOGIT, DZ_KD = 0, 1, 2
-ABI_VERSION = 10  # include/ncf_hip.h NCF_ABI_VERSION
+ABI_VERSION = 11  # include/ncf_hip.h NCF_ABI_VERSION
 PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 LAYOUT_PER_ROW_L0, LAYOUT_WG_SHIFT, LAYOUT_WG_MASK = 0x1, 8, 0xFFF  # ncf_layout.flags (ncf_layout_tune)
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
@@ -44,7 +44,8 @@ class NcfLayout(ctypes.Structure):
                 ("w", c_i64 * 4), ("b", c_i64 * 4), ("wp", c_i64), ("bp", c_i64),
                 ("tower_begin", c_i64), ("tower_len", c_i64), ("total", c_i64),
                 ("user_num", c_i32), ("item_num", c_i32), ("factor_num", c_i32),
-                ("num_layers", c_i32), ("model_type", c_i32), ("flags", c_i32)]
+                ("num_layers", c_i32), ("model_type", c_i32), ("flags", c_i32),
+                ("dropout", ctypes.c_float), ("dropout_seed", ctypes.c_uint32)]
 
     @property
     def loss_slot(self) -> int:
@@ -94,6 +95,8 @@ _HIP_PROTOS = {
     "ncf_hr_ndcg": (ctypes.c_int, [c_vp, c_vp, c_i64, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
     "ncf_fact_mode": (ctypes.c_int, [c_vp]),
     "ncf_reduce_rows": (ctypes.c_int, [c_vp]),
+    "ncf_dropout_hash": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, c_i64,
+                                           ctypes.c_uint32]),
     "ncf_fact_partials_bytes": (c_i64, [c_vp]),
     "ncf_randperm_workspace": (c_i64, [c_i64]),
     "ncf_randperm": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),

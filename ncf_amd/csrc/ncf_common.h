@@ -29,6 +29,20 @@ __device__ __forceinline__ float bce_loss(float x, float y) {
 }
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Dropout keep hash (include/ncf_hip.h ncf_dropout_hash): splitmix64 finalizer of
+// the mixed (seed, step, layer, row, column), upper 32 bits.
+__host__ __device__ __forceinline__ uint32_t dropout_hash(uint32_t seed, uint32_t t, uint32_t layer, int64_t row,
+                                                          uint32_t col) {
+    uint64_t x = ((uint64_t)seed << 32) ^ ((uint64_t)t * 0x9E3779B97F4A7C15ull) ^
+                 ((uint64_t)row * 0xBF58476D1CE4E5B9ull) ^ ((uint64_t)((layer << 16) | col) * 0x94D049BB133111EBull);
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return (uint32_t)(x >> 32);
+}
+
 // Distillation response term of one row (src/distillation/base.py:27-34 with T > 0,
 // response.py:28-32 with T <= 0): *r = its per-row loss, returns d r / d z.
 __device__ __forceinline__ float kd_response(float z, float t, float T, float* r) {

@@ -60,6 +60,29 @@ __device__ __forceinline__ Sel select_rows(const LyrArgs& a) {
     return Sel{b0 + lo, hi - lo, (float)gb};
 }
 
+// Dropout of the input of tower layer k (training steps with lay.dropout > 0):
+// element (epoch-stream row r, column c) is multiplied by 1 / (1 - p) when kept,
+// else 0 (ncf_hip.h ncf_dropout_hash).  Off for forward-only launches (ctl null).
+struct Drop {
+    bool on;
+    uint32_t seed, t, thr;
+    float scale;
+};
+__device__ __forceinline__ Drop drop_of(const LyrArgs& a) {
+    Drop d{false, 0, 0, 0, 1.f};
+    if (a.ctl == nullptr || !(a.lay.dropout > 0.f)) return d;
+    const float p = a.lay.dropout;
+    d.on = true;
+    d.seed = a.lay.dropout_seed;
+    d.t = (uint32_t)a.ctl->adam_t;
+    d.thr = p >= 1.f ? 0xffffffffu : (uint32_t)((double)p * 4294967296.0);
+    d.scale = p >= 1.f ? 0.f : 1.0f / (1.0f - p);
+    return d;
+}
+__device__ __forceinline__ float drop_mul(const Drop& d, int k, int64_t row, int c) {
+    return dropout_hash(d.seed, d.t, (uint32_t)k, row, (uint32_t)c) >= d.thr ? d.scale : 0.f;
+}
+
 __device__ __forceinline__ void row_ids(const LyrArgs& a, const Sel& s, int64_t m, int& u, int& it) {
     if (m < s.nloc) {
         const uint64_t r = a.rows[s.base + m];
@@ -155,14 +178,17 @@ __global__ __launch_bounds__(GNT) void lyr_fwd_kernel(LyrArgs a, int k, const fl
         si[threadIdx.x] = it < 0 ? 0 : it;
     }
     if (FIRST) __syncthreads();
+    const Drop dr = drop_of(a);
     auto ga = [&](int r, int64_t c) -> float {
         const int64_t m = m0 + r;
         if (m >= R || c >= K) return 0.f;
+        float v;
         if constexpr (FIRST) {
-            return c < DM ? prm[lay.um + (int64_t)su[r] * DM + c] : prm[lay.im + (int64_t)si[r] * DM + (c - DM)];
+            v = c < DM ? prm[lay.um + (int64_t)su[r] * DM + c] : prm[lay.im + (int64_t)si[r] * DM + (c - DM)];
         } else {
-            return Ain[m * K + c];
+            v = Ain[m * K + c];
         }
+        return dr.on ? v * drop_mul(dr, k, s.base + m, (int)c) : v;
     };
     auto gb = [&](int64_t c, int n) -> float {
         const int nn = n0 + n;
@@ -210,6 +236,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, con
         si[threadIdx.x] = it;
     }
     if (FIRST) __syncthreads();
+    const Drop dr = drop_of(a);
     auto ga = [&](int r, int64_t j) -> float {
         const int64_t m = m0 + r;
         return (m < R && j < J) ? D[m * J + j] : 0.f;
@@ -230,7 +257,8 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, con
                     const int rr = wm + 16 * ti + 4 * (l >> 4) + r;
                     const int64_t m = m0 + rr;
                     if (m >= R) continue;
-                    const float v = lane_get(acc[ti][tj], r);
+                    float v = lane_get(acc[ti][tj], r);
+                    if (dr.on) v *= drop_mul(dr, k, s.base + m, n);  // through layer k's input dropout
                     if constexpr (FIRST) {
                         const int id = n < DM ? su[rr] : si[rr];
                         if (id >= 0)
@@ -270,6 +298,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
     const float* prm = a.params;
     float* slab = a.slab + (int64_t)(blockIdx.z % lyr_slab_rows(&lay)) * (lay.tower_len + 64);
     const int64_t tb = lay.tower_begin;
+    const Drop dr = drop_of(a);
     auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
@@ -310,7 +339,9 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
                 if (m >= q1 || c > K) return 0.f;
                 if (c == K) return 1.f;
                 const int e = (int)(m - q0);
-                return c < DM ? prm[lay.um + (int64_t)su[e] * DM + c] : prm[lay.im + (int64_t)si[e] * DM + (c - DM)];
+                const float v =
+                    c < DM ? prm[lay.um + (int64_t)su[e] * DM + c] : prm[lay.im + (int64_t)si[e] * DM + (c - DM)];
+                return dr.on ? v * drop_mul(dr, k, s.base + m, c) : v;
             };
             auto ga2 = [&](int jr, int64_t m) -> float {
                 const int j = j0 + jr;
@@ -322,7 +353,9 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
         auto gb = [&](int64_t m, int cr) -> float {
             const int c = c0 + cr;
             if (m >= r1 || c > K) return 0.f;
-            return c == K ? 1.f : Ain[m * K + c];
+            if (c == K) return 1.f;
+            const float v = Ain[m * K + c];
+            return dr.on ? v * drop_mul(dr, k, s.base + m, c) : v;
         };
         gemm_block<false, false>(j0, c0, r0, r1, ga, gb, ep);
     }

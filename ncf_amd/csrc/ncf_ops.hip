@@ -787,6 +787,7 @@ constexpr int FX_WAVES = 16;  // 16 waves: dW0 / dX output tiles dealt round-rob
 template <int DM>
 struct FxShape {
     static constexpr int CH = DM <= 64 ? 64 : 32;
+    static constexpr int CPB = DM <= 64 ? 1 : 4;  // chunks per block
     static constexpr int ST = DM + 4, NT = (DM + 15) / 16, Q4 = DM / 4;
     static constexpr int TPW = (NT * NT + FX_WAVES - 1) / FX_WAVES;  // dW0 tiles per wave
     static constexpr int64_t LDS = ((int64_t)DM * ST + 3LL * CH * ST) * 4;
@@ -795,9 +796,9 @@ struct FxShape {
 template <int DM>
 __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout lay, const float* __restrict__ prm,
                                                                      float* __restrict__ grads,
-                                                                     float* __restrict__ partials, int nbu, int cpb) {
+                                                                     float* __restrict__ partials, int nbu) {
     using X_ = FxShape<DM>;
-    constexpr int CH = X_::CH, ST = X_::ST, NT = X_::NT, Q4 = X_::Q4, TPW = X_::TPW;
+    constexpr int CH = X_::CH, ST = X_::ST, NT = X_::NT, Q4 = X_::Q4, TPW = X_::TPW, cpb = X_::CPB;
     extern __shared__ __attribute__((aligned(16))) float fsm[];
     float* sW = fsm;           // W0[:, koff : koff + DM]  [DM][ST]
     float* sG = sW + DM * ST;  // G rows  [CH][ST]
@@ -821,6 +822,7 @@ __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout l
     f4 accw[TPW];
 #pragma unroll
     for (int q = 0; q < TPW; ++q) accw[q] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
     for (int ch = 0; ch < cpb; ++ch) {
         const int64_t r0 = rb + (int64_t)ch * CH;
         if (r0 >= nrows) break;  // block-uniform
@@ -934,13 +936,18 @@ static const KernelEntry* fused_entry(const ncf_layout* lay) {
     if (!e) return nullptr;
     return train_lds_floats(e, lay) * 4 <= LDS_LIMIT_BYTES ? e : nullptr;
 }
+// Fused kernel of a training step: none with dropout (the layered path applies it).
+static const KernelEntry* train_fused(const ncf_layout* lay) {
+    return lay->dropout > 0.f ? nullptr : fused_entry(lay);
+}
 static int fact_dm(const ncf_layout* lay) { return lay->factor_num << (lay->num_layers - 1); }
 static bool fact_mode(const ncf_layout* lay) {
     if (lay->model_type == NCF_MODEL_GMF || (lay->flags & NCF_LAYOUT_PER_ROW_L0)) return false;
+    if (lay->dropout > 0.f) return false;  // masks per row: layer 0 does not factor per entity
     if ((int64_t)lay->user_num + lay->item_num > FACT_MAX_ROWS) return false;
     const int dm = fact_dm(lay);
     if (dm != 8 && dm != 16 && dm != 32 && dm != 64 && dm != 128) return false;  // fact_expand_kernel<DM>
-    const KernelEntry* e = fused_entry(lay);
+    const KernelEntry* e = train_fused(lay);
     if (e) return e->train_fact != nullptr;
     return lay->factor_num <= LYR_MAX_FACTOR;
 }
@@ -959,7 +966,7 @@ static int slab_lo(const ncf_layout* lay) {
 }
 
 static int fact_ch(const ncf_layout* lay) { return fact_dm(lay) <= 64 ? 64 : 32; }  // FxShape<DM>::CH
-static int fact_cpb(const ncf_layout* lay) { return fact_dm(lay) <= 64 ? 1 : 4; }   // chunks per block
+static int fact_cpb(const ncf_layout* lay) { return fact_dm(lay) <= 64 ? 1 : 4; }   // FxShape<DM>::CPB
 
 static int fact_blocks(const ncf_layout* lay, int* nbu) {
     const int64_t per = (int64_t)fact_ch(lay) * fact_cpb(lay);
@@ -979,12 +986,12 @@ static int64_t fact_partials_floats(const ncf_layout* lay) {
 static float* fact_partials(const ncf_layout* lay, void* workspace) {
     const int64_t stride = lay->tower_len + 64;
     return static_cast<float*>(workspace) +
-           (fused_entry(lay) ? (int64_t)SLAB_ROWS * stride : rup64((int64_t)lyr_slab_rows(lay) * stride));
+           (train_fused(lay) ? (int64_t)SLAB_ROWS * stride : rup64((int64_t)lyr_slab_rows(lay) * stride));
 }
 
 // Rows of the partial slab the reductions sum: the fused step's workgroups, or the
 // layered path's lyr_slab_rows.
-static int reduce_rows(const ncf_layout* lay) { return fused_entry(lay) ? slab_rows_of(lay) : lyr_slab_rows(lay); }
+static int reduce_rows(const ncf_layout* lay) { return train_fused(lay) ? slab_rows_of(lay) : lyr_slab_rows(lay); }
 
 static W0Part w0_part(const ncf_layout* lay, const void* workspace) {
     W0Part wp;
@@ -1011,9 +1018,8 @@ static int launch_fact_expand(const ncf_layout* lay, const float* params, float*
     ncf_layout l = *lay;
     int nbu;
     int nblk = fact_blocks(lay, &nbu);
-    int cpb = fact_cpb(lay);
     if (ensure_lds(fe, lds) != NCF_OK) return NCF_E_LAUNCH;
-    void* ae[] = {&l, (void*)&params, (void*)&grads, (void*)&partials, &nbu, &cpb};
+    void* ae[] = {&l, (void*)&params, (void*)&grads, (void*)&partials, &nbu};
     if (hipLaunchKernel(fe, dim3((unsigned)nblk), dim3(FX_WAVES * 64), ae, (size_t)lds, st) != hipSuccess)
         return NCF_E_LAUNCH;
     return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
@@ -1042,6 +1048,10 @@ int ncf_slab_rows(void) { return SLAB_ROWS; }
 int ncf_fact_mode(const ncf_layout* lay) { return lay && fact_mode(lay) ? 1 : 0; }
 
 int ncf_reduce_rows(const ncf_layout* lay) { return lay ? reduce_rows(lay) : -1; }
+
+uint32_t ncf_dropout_hash(uint32_t seed, uint32_t t, uint32_t layer, int64_t row, uint32_t col) {
+    return dropout_hash(seed, t, layer, row, col);
+}
 
 int64_t ncf_fact_partials_bytes(const ncf_layout* lay) {
     return lay && fact_mode(lay) ? fact_partials_floats(lay) * 4 : 0;
@@ -1096,7 +1106,7 @@ int ncf_supported(int mode, int F, int L) {
 
 int64_t ncf_workspace_bytes(const ncf_layout* lay, int64_t rows) {
     if (!lay || rows < 0) return -1;
-    if (fused_entry(lay))
+    if (train_fused(lay))
         return ((int64_t)SLAB_ROWS * ncf_slab_stride(lay) + (fact_mode(lay) ? fact_partials_floats(lay) : 0)) * 4;
     return lyr_workspace_floats(lay, rows, true, fact_mode(lay) ? fact_partials_floats(lay) : -1) * 4;
 }
@@ -1119,7 +1129,7 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
     const int64_t rows_max = (batch_global + world - 1) / world;
     if (workspace_bytes < ncf_workspace_bytes(lay, rows_max)) return NCF_E_ARG;
     float* slab = static_cast<float*>(workspace);
-    const KernelEntry* e = fused_entry(lay);
+    const KernelEntry* e = train_fused(lay);
     if (!e) {
         LyrArgs la;
         memset(&la, 0, sizeof(la));

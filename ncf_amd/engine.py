@@ -88,6 +88,10 @@ class TrainEngine:
         self.flat, lay0 = ops.ensure_flat(model, n)
         # the engine's own copy: ncf_layout_tune shapes it for the batch size
         self.lay = type(lay0).from_buffer_copy(lay0)
+        # nn.Dropout(p) before every tower Linear (models.py:23): training steps with
+        # p > 0 run the layered path, keep masks hashed from (seed, step, layer, row,
+        # column) -- include/ncf_hip.h ncf_dropout_hash
+        ops.set_dropout(self.lay, model)
         dev = self.flat.device
         self.device = dev
         n = self.flat.numel()

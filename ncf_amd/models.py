@@ -121,9 +121,7 @@ class NCF(nn.Module):
     def forward(self, user, item):
         if self.embed_user_GMF.weight.is_cuda:
             from . import ops
-            if self.training and self.dropout > 0:
-                raise NotImplementedError("dropout > 0 is not implemented by the HIP tower kernel")
-            return ops.ncf_forward(self, user, item)
+            return ops.ncf_forward(self, user, item)  # dropout: ops._dropout_layout
         return self._forward_cpu(user, item)
 
     def _forward_cpu(self, user, item):

@@ -237,12 +237,63 @@ def new_ctl(n_total, dev, batch=0, adam_t=0):
     return torch.tensor([batch, adam_t, n_total, 0, 0, 0], dtype=torch.int64, device=dev)
 
 
+def dropout_seed(dev):
+    """The dropout hash seed: the device generator's seed (torch.manual_seed sets it)."""
+    return int(torch.cuda.initial_seed()) & 0xFFFFFFFF
+
+
+def set_dropout(lay, model):
+    """Copy the model's tower dropout into a training layout (GMF has no tower)."""
+    p = float(getattr(model, "dropout", 0.0) or 0.0)
+    if p > 0 and model.model_type != "GMF":
+        lay.dropout = p
+        lay.dropout_seed = dropout_seed(model.embed_user_GMF.weight.device)
+    else:
+        lay.dropout = 0.0
+
+
+def _dropout_layout(model):
+    """Training-mode layout with the model's dropout, or None when dropout is off."""
+    if not model.training:
+        return None
+    lay = type(model._ncf_layout).from_buffer_copy(model._ncf_layout)
+    set_dropout(lay, model)
+    if not lay.dropout > 0:
+        return None
+    model._ncf_drop_t = getattr(model, "_ncf_drop_t", -1) + 1  # a fresh mask per forward
+    return lay, model._ncf_drop_t
+
+
+def _dropout_logits(model, rows, drop):
+    """Training-mode logits under dropout: the train step with dL/dlogit = 0 (same
+    masks as the backward, which reruns it with the same step index)."""
+    lay, t = drop
+    flat = model._ncf_flat
+    dev = flat.device
+    n = rows.numel()
+    logits = torch.empty(n, dtype=torch.float32, device=dev)
+    scratch = torch.zeros(int(lay.total), dtype=torch.float32, device=dev)
+    ws = new_workspace(lay, n, dev)
+    ctl = new_ctl(n, dev, adam_t=t)
+    dl = torch.zeros(n, dtype=torch.float32, device=dev)
+    L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), scratch.data_ptr(), rows.data_ptr(),
+                                   dl.data_ptr(), ctl.data_ptr(), int(n), 1, 0, L.DZ_DLOGIT,
+                                   ws.data_ptr(), ws.numel() * 4, logits.data_ptr(), L.stream_ptr(dev)),
+            "ncf_train_step")
+    return logits
+
+
 class _NCFFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, rows, model, *params):
         flat, lay = model._ncf_flat, model._ncf_layout
-        logits = forward_logits(flat, lay, rows, ws_owner=model)
+        drop = _dropout_layout(model)
+        if drop is None:
+            logits = forward_logits(flat, lay, rows, ws_owner=model)
+        else:
+            logits = _dropout_logits(model, rows, drop)
         ctx.model = model
+        ctx.drop = drop
         ctx.save_for_backward(rows)
         return logits
 
@@ -251,10 +302,12 @@ class _NCFFunction(torch.autograd.Function):
         (rows,) = ctx.saved_tensors
         model = ctx.model
         flat, lay = model._ncf_flat, model._ncf_layout
+        if ctx.drop is not None:
+            lay = ctx.drop[0]
         dev = flat.device
         gflat = torch.zeros(int(lay.total), dtype=torch.float32, device=dev)
         ws = new_workspace(lay, rows.numel(), dev)
-        ctl = new_ctl(rows.numel(), dev)
+        ctl = new_ctl(rows.numel(), dev, adam_t=ctx.drop[1] if ctx.drop is not None else 0)
         dlogit = grad_out.contiguous().to(torch.float32)
         fused_backward(flat, lay, rows, dlogit, gflat, ws, ctl)
         grads = []
@@ -279,4 +332,7 @@ def ncf_forward(model, user, item):
     rows = pack_rows(u, i)
     if torch.is_grad_enabled() and any(p.requires_grad for p in model.ordered_params()):
         return _NCFFunction.apply(rows, model, *model.ordered_params())
+    drop = _dropout_layout(model)  # train mode: nn.Dropout applies under no_grad too
+    if drop is not None:
+        return _dropout_logits(model, rows, drop)
     return forward_logits(flat, lay, rows, ws_owner=model)

@@ -23,6 +23,9 @@ What it restates (reference = YonkaMayonkaZ/NCF, paths relative to its root):
                         ``randperm`` on a fresh generator; a metrics() pass over
                         the test loader costs one more draw.
 * ``metrics_np``     -- ``src/training/metrics.py:4-25`` in numpy.
+* ``dropout_masks`` / ``forward_masked`` -- the tower's ``nn.Dropout`` (models.py:23)
+                        with the device path's hashed masks (parity of the
+                        arithmetic given a mask; the mask bits are not torch's).
 
 Pinning: every function here is checked against the reference's own outputs
 (``tests/golden/*.npz``, produced by ``tests/golden/make_golden.py`` importing
@@ -138,6 +141,61 @@ def forward_backward(model, users, items, labels):
     loss.backward()
     grads = {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
     return logits.detach(), float(loss.item()), grads
+
+
+# --------------------------------------------------------------------------- dropout
+# nn.Dropout(p) before every tower Linear (models.py:23).  torch draws the masks from
+# its Philox stream, which nothing here reproduces; the device path hashes them
+# (include/ncf_hip.h ncf_dropout_hash) and this restates that hash, so the
+# arithmetic given a mask is checked exactly ("parity unpinned" for the mask bits).
+_C0, _C1, _C2 = np.uint64(0x9E3779B97F4A7C15), np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB)
+
+
+def dropout_hash(seed, t, layer, rows, cols):
+    """ncf_dropout_hash over rows x cols (uint64 arithmetic wraps like C)."""
+    r = np.asarray(rows, dtype=np.int64).astype(np.uint64)[:, None]
+    c = np.asarray(cols, dtype=np.uint64)[None, :]
+    with np.errstate(over="ignore"):
+        x = (np.uint64(seed) << np.uint64(32)) ^ (np.uint64(t) * _C0) ^ (r * _C1) ^ \
+            ((np.uint64(layer << 16) | c) * _C2)
+        x ^= x >> np.uint64(30)
+        x *= _C1
+        x ^= x >> np.uint64(27)
+        x *= _C2
+        x ^= x >> np.uint64(31)
+    return (x >> np.uint64(32)).astype(np.uint32)
+
+
+def dropout_masks(model, seed, t, rows, p):
+    """Per tower layer k, the multiplier of each element of its input for the given
+    epoch-stream rows at step t: 1 / (1 - p) in fp32 where kept, else 0."""
+    p32 = np.float32(p)
+    thr = np.uint32(0xFFFFFFFF) if p32 >= 1 else np.uint32(int(float(p32) * 4294967296.0))
+    scale = np.float32(0) if p32 >= 1 else np.float32(1) / (np.float32(1) - p32)
+    widths = [m.in_features for m in model.MLP_layers if isinstance(m, nn.Linear)]
+    return [torch.from_numpy(np.where(dropout_hash(seed, t, k, rows, np.arange(w)) >= thr, scale,
+                                      np.float32(0)).astype(np.float32)) for k, w in enumerate(widths)]
+
+
+def forward_masked(model, user, item, masks):
+    """OracleNCF.forward with the tower's Dropout modules replaced by `masks`."""
+    def tower(x):
+        k = 0
+        for m in model.MLP_layers:
+            if isinstance(m, nn.Dropout):
+                x = x * masks[k]
+                k += 1
+            else:
+                x = m(x)
+        return x
+    if model.model_type == "GMF":
+        out = model.embed_user_GMF(user) * model.embed_item_GMF(item)
+    elif model.model_type == "MLP":
+        out = tower(torch.cat((model.embed_user_MLP(user), model.embed_item_MLP(item)), -1))
+    else:
+        gmf = model.embed_user_GMF(user) * model.embed_item_GMF(item)
+        out = torch.cat((gmf, tower(torch.cat((model.embed_user_MLP(user), model.embed_item_MLP(item)), -1))), -1)
+    return model.predict_layer(out).view(-1)
 
 
 # --------------------------------------------------------------------------- data stream

@@ -28,12 +28,12 @@ SHAPES = [(8, 3), (16, 3), (8, 1)]
 DEV = "cuda:0"
 
 
-def _models(mt, f, L, U=50, I=80, seed=1):
+def _models(mt, f, L, U=50, I=80, seed=1, dropout=0.0):
     from ncf_amd.models import NCF
     torch.manual_seed(seed)
-    ref = O.OracleNCF(U, I, f, L, 0.0, mt)
+    ref = O.OracleNCF(U, I, f, L, dropout, mt)
     torch.manual_seed(seed)
-    m = NCF(U, I, f, L, 0.0, mt)
+    m = NCF(U, I, f, L, dropout, mt)
     for (k1, v1), (k2, v2) in zip(ref.state_dict().items(), m.state_dict().items()):
         assert k1 == k2 and torch.equal(v1, v2)
     return ref, m.to(DEV)
@@ -84,9 +84,9 @@ def test_forward_edge_sizes():
         np.testing.assert_allclose(got, exp, rtol=1e-5, atol=1e-7)
 
 
-def _engine_for(mt, f, L, U, I, seed, optimizer="adam", lr=1e-3):
+def _engine_for(mt, f, L, U, I, seed, optimizer="adam", lr=1e-3, dropout=0.0):
     from ncf_amd.engine import TrainEngine
-    ref, m = _models(mt, f, L, U=U, I=I, seed=seed)
+    ref, m = _models(mt, f, L, U=U, I=I, seed=seed, dropout=dropout)
     eng = TrainEngine(m, lr=lr, optimizer=optimizer)
     return ref, m, eng
 
@@ -621,3 +621,128 @@ def test_engine_tuned_launch_shape_vs_oracle(B, per_row):
     np.testing.assert_allclose(got_losses, O.train_steps(ref, opt, users, items, labels), rtol=1e-5)
     ref.load_state_dict(ref0)
     _teacher_forced_steps(ref, m, eng, users, items, labels)
+
+
+# --------------------------------------------------------------------------- dropout
+# nn.Dropout(p) before every tower Linear (models.py:23): training steps with p > 0
+# run the layered path with hashed keep masks (include/ncf_hip.h ncf_dropout_hash);
+# the oracle applies the same masks (forward_masked), so everything but the mask
+# bits (torch's Philox stream, not reproduced: parity unpinned) is checked exactly.
+def _masked_step_ref(ref, users, items, labels, masks):
+    ref.zero_grad(set_to_none=True)
+    u = torch.as_tensor(np.asarray(users), dtype=torch.int64)
+    i = torch.as_tensor(np.asarray(items), dtype=torch.int64)
+    logits = O.forward_masked(ref, u, i, masks)
+    loss = O.bce_mean(logits, torch.as_tensor(np.asarray(labels)))
+    loss.backward()
+    return logits.detach(), float(loss.item()), {k: p.grad.detach().clone() for k, p in ref.named_parameters()
+                                                 if p.grad is not None}
+
+
+@pytest.mark.parametrize("mt,f,Lyr,p", [("NeuMF-end", 16, 3, 0.3), ("MLP", 8, 2, 0.5), ("NeuMF-end", 32, 3, 0.1)])
+def test_one_step_dropout_vs_masked_oracle(mt, f, Lyr, p):
+    """One training step with dropout p at ml-1m ids (B = 8,192; the fused shape
+    NCF(16,3) is routed to the layered path) vs the oracle under the same masks."""
+    import ncf_amd._lib as L
+    from ncf_amd import ops
+    U, I, B = 6041, 3707, 8192
+    ref, m = _models(mt, f, Lyr, U=U, I=I, seed=29, dropout=p)
+    rng = np.random.default_rng(5)
+    users = rng.integers(0, U, B)
+    items = np.minimum(rng.zipf(1.3, B) - 1, I - 1)
+    labels = (rng.random(B) < 0.2).astype(np.int64)
+    flat, lay0 = ops.ensure_flat(m)
+    lay = type(lay0).from_buffer_copy(lay0)
+    ops.set_dropout(lay, m)
+    assert lay.dropout > 0 and not ops.fact_mode(lay)
+    masks = O.dropout_masks(ref, int(lay.dropout_seed), 0, np.arange(B), p)
+    kept = float(np.mean([mk.numpy().astype(bool).mean() for mk in masks]))
+    assert abs(kept - (1 - p)) < 0.01
+    logits_ref, loss_ref, grads_ref = _masked_step_ref(ref, users, items, labels, masks)
+    gflat = torch.zeros(int(lay.total), device=DEV)
+    ws = ops.new_workspace(lay, B, DEV)
+    ctl = ops.new_ctl(B, DEV)
+    u = torch.as_tensor(users, dtype=torch.int32, device=DEV)
+    it = torch.as_tensor(items, dtype=torch.int32, device=DEV)
+    y = torch.as_tensor(labels, dtype=torch.float32, device=DEV)
+    rows = ops.pack_rows(u, it, y)
+    logits = torch.empty(B, device=DEV)
+    st = L.stream_ptr()
+    L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(), None,
+                                   ctl.data_ptr(), B, 1, 0, L.DZ_BCE, ws.data_ptr(), ws.numel() * 4,
+                                   logits.data_ptr(), st), "train")
+    L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), ws.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st),
+            "reduce")
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(logits.cpu().numpy(), logits_ref.numpy(), rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(gflat[lay.loss_slot].item(), loss_ref, rtol=1e-5)
+    for (q, off), (name, _) in zip(ops._segments(m, lay), m.named_parameters()):
+        got = gflat[off:off + q.numel()].view_as(q).cpu().numpy()
+        if name in grads_ref:
+            hot = int(np.bincount(items).max()) if "item" in name else int(np.bincount(users).max())
+            _close_grad(got, grads_ref[name].numpy(), name, terms=hot if "embed" in name else None)
+
+
+def test_engine_dropout_trajectory_vs_masked_oracle():
+    """TrainEngine (hipGraph) with dropout 0.2 on NCF(16,3): step t masks the rows
+    t*B .. of the epoch stream at Adam step t; 6 steps vs torch.optim.Adam on the
+    oracle under the same masks (losses rtol 1e-5, parameters per
+    _assert_trajectory_close)."""
+    from ncf_amd import ops
+    T, B, p = 6, 4096, 0.2
+    ref, m, eng = _engine_for("NeuMF-end", 16, 3, 6041, 3707, 31, dropout=p)
+    assert eng.lay.dropout == np.float32(p) and not ops.fact_mode(eng.lay)
+    rng = np.random.default_rng(53)
+    users = rng.integers(0, 6041, (T, B))
+    items = np.minimum(rng.zipf(1.3, (T, B)) - 1, 3706)
+    labels = (rng.random((T, B)) < 0.2).astype(np.int64)
+    _stream(eng, users, items, labels, B)
+    eng.run(T, use_graph=True)
+    torch.cuda.synchronize()
+    got_losses = eng.epoch_losses()[:T].copy()
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    losses = []
+    for t in range(T):
+        masks = O.dropout_masks(ref, int(eng.lay.dropout_seed), t, t * B + np.arange(B), p)
+        opt.zero_grad()
+        loss = O.bce_mean(O.forward_masked(ref, torch.as_tensor(users[t]), torch.as_tensor(items[t]), masks),
+                          torch.as_tensor(labels[t]))
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    np.testing.assert_allclose(got_losses, losses, rtol=1e-5)
+    for k, r in ref.state_dict().items():
+        _assert_trajectory_close(m.state_dict()[k].cpu().numpy(), r.numpy(), T, 1e-3, k)
+
+
+def test_module_forward_dropout_train_and_eval():
+    """NCF.forward on the device with dropout 0.4: train mode applies the masks of
+    its own step index in forward and backward (= the oracle under those masks); a
+    fresh mask per call; eval mode is the plain forward."""
+    from ncf_amd import ops
+    p, n = 0.4, 3000
+    ref, m = _models("NeuMF-end", 16, 3, U=400, I=700, seed=37, dropout=p)
+    rng = np.random.default_rng(9)
+    users, items = rng.integers(0, 400, n), rng.integers(0, 700, n)
+    labels = (rng.random(n) < 0.3).astype(np.int64)
+    m.train()
+    pred = m(torch.as_tensor(users, device=DEV), torch.as_tensor(items, device=DEV))
+    t = m._ncf_drop_t
+    masks = O.dropout_masks(ref, ops.dropout_seed(DEV), t, np.arange(n), p)
+    lg_ref, loss_ref, g_ref = _masked_step_ref(ref, users, items, labels, masks)
+    np.testing.assert_allclose(pred.detach().cpu().numpy(), lg_ref.numpy(), rtol=1e-5, atol=1e-7)
+    loss = torch.nn.BCEWithLogitsLoss()(pred, torch.as_tensor(labels, dtype=torch.float32, device=DEV))
+    np.testing.assert_allclose(loss.item(), loss_ref, rtol=1e-5)
+    loss.backward()
+    for k, q in m.named_parameters():
+        if k in g_ref:
+            _close_grad(q.grad.cpu().numpy(), g_ref[k].numpy(), k)
+    with torch.no_grad():
+        again = m(torch.as_tensor(users, device=DEV), torch.as_tensor(items, device=DEV))
+    assert m._ncf_drop_t == t + 1 and not torch.equal(again, pred.detach())
+    m.eval()
+    ref.eval()
+    with torch.no_grad():
+        ev = m(torch.as_tensor(users, device=DEV), torch.as_tensor(items, device=DEV))
+        ev_ref = ref(torch.as_tensor(users), torch.as_tensor(items))
+    np.testing.assert_allclose(ev.cpu().numpy(), ev_ref.numpy(), rtol=1e-5, atol=1e-7)

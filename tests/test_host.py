@@ -213,3 +213,28 @@ def test_pipelined_sampler_many_blocks_matches_oracle():
     s.sample(I, 4)
     assert np.array_equal(s.sample(I, 4), d._ng_i)
     assert np.array_equal(np.random.randint(1 << 30, size=4), after)
+
+
+def test_dropout_hash_restatement_and_statistics():
+    """include/ncf_hip.h ncf_dropout_hash (host export of the device function) ==
+    the oracle's numpy restatement; keep rates match 1 - p per layer, step and
+    column block; masks of different steps / layers / rows are uncorrelated."""
+    import ncf_amd._lib as L
+    from oracle import ncf_oracle as O
+    rng = np.random.default_rng(1)
+    for _ in range(4):
+        seed, t, k = int(rng.integers(0, 2**32)), int(rng.integers(0, 2**31)), int(rng.integers(0, 4))
+        rows = rng.integers(0, 2**40, 8)
+        h = O.dropout_hash(seed, t, k, rows, np.arange(5))
+        for a in range(8):
+            for c in range(5):
+                assert int(h[a, c]) == L.hip().ncf_dropout_hash(seed, t, k, int(rows[a]), c)
+    rows, cols = np.arange(50000), np.arange(64)
+    for p in (0.1, 0.5, 0.9):
+        thr = np.uint32(int(float(np.float32(p)) * 4294967296.0))
+        keep = [O.dropout_hash(3, t, k, rows, cols) >= thr for t, k in ((0, 0), (1, 0), (0, 1))]
+        for kp in keep:
+            assert abs(kp.mean() - (1 - p)) < 0.005
+            assert abs(kp[:, :8].mean() - (1 - p)) < 0.01
+        for a, b in ((0, 1), (0, 2)):
+            assert abs(np.corrcoef(keep[a].ravel(), keep[b].ravel())[0, 1]) < 0.01
