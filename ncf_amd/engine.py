@@ -72,8 +72,8 @@ class TrainEngine:
         self.world_size, self.rank, self.group = int(world_size), int(rank), process_group
         if dp_mode is None:
             dp_mode = os.environ.get("NCF_DP_MODE", "zero1") if self.world_size > 1 else "single"
-        if self.world_size == 1:
-            dp_mode = "single"
+        # an explicit exchange mode stands at world 1 (a one-rank group still runs the
+        # real collectives: how the captured-collective graph is tested on one GPU)
         if dp_mode not in ("single", "zero1", "allreduce", "sparse"):
             raise ValueError(f"dp_mode {dp_mode!r}")
         self.dp_mode = dp_mode
@@ -205,7 +205,7 @@ class TrainEngine:
         """Launch 3 (world > 1): gradient exchange over ranks (RCCL on ROCm).
         zero1: reduce-scatter of the flat gradient into this rank's shard;
         allreduce: in-place sum of the whole flat gradient."""
-        if self.world_size == 1:
+        if self.dp_mode == "single":
             return
         if self.dp_mode == "zero1":
             D.reduce_scatter_flat(self.gshard, self.grads, self.rank, self.group)
@@ -273,7 +273,7 @@ class TrainEngine:
     def _fused_optimizer(self):
         """Single process + Adam: slab reduction and Adam in one launch
         (ncf_reduce_adam_step); otherwise reduce, [all-reduce], optimizer."""
-        return self.world_size == 1 and self.optimizer == "adam" and os.environ.get("NCF_FUSED_ADAM", "1") == "1"
+        return self.dp_mode == "single" and self.optimizer == "adam" and os.environ.get("NCF_FUSED_ADAM", "1") == "1"
 
     def _train_launch(self):
         st = L.stream_ptr(self.device)
@@ -370,9 +370,11 @@ class TrainEngine:
         default for world > 1: the step is then two graphs (compute, optimizer)
         with the collective issued eagerly between them, which needs nothing of
         the process group beyond a plain all_reduce (any backend)."""
+        if self.dp_mode == "single":
+            return True
         if self.dp_mode == "sparse":  # bucket sizes go through the host every step
-            return self.world_size == 1
-        return self.world_size == 1 or os.environ.get("NCF_CAPTURE_ALLREDUCE", "0") == "1"
+            return False
+        return os.environ.get("NCF_CAPTURE_ALLREDUCE", "0") == "1"
 
     def _graph_of(self, fn):
         g = torch.cuda.CUDAGraph()

@@ -96,3 +96,36 @@ def test_two_ranks_match_single_rank(mt, f, nl, use_graph, dp_mode):
     flat1, losses1 = _run(1, 0, None, mt, f, nl, use_graph)
     np.testing.assert_allclose(res[0][1], losses1, rtol=1e-5)
     np.testing.assert_allclose(res[0][0], flat1, rtol=1e-4, atol=1e-6)
+
+
+def _rccl_worker(port, dp_mode, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["NCF_CAPTURE_ALLREDUCE"] = "1"
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        flat, losses = _run(1, 0, dist.group.WORLD, "NeuMF-end", 16, 3, True, dp_mode)
+        q.put((flat, losses))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dp_mode", ["zero1", "allreduce"])
+def test_rccl_collective_captured_in_step_graph(dp_mode):
+    """NCF_CAPTURE_ALLREDUCE=1 on backend nccl (RCCL): the gradient exchange is
+    captured inside the step graphs.  One GPU holds one RCCL rank, so a one-rank
+    group with an explicit dp_mode runs the real RCCL reduce-scatter / all-gather /
+    all-reduce kernels through the captured graph; the result must equal the
+    single-process engine (no collective) to fp32 summation order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), dp_mode, q))
+    p.start()
+    flat, losses = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    flat1, losses1 = _run(1, 0, None, "NeuMF-end", 16, 3, True)
+    np.testing.assert_allclose(losses, losses1, rtol=1e-5)
+    np.testing.assert_allclose(flat, flat1, rtol=1e-4, atol=1e-6)
