@@ -158,7 +158,7 @@ __device__ __forceinline__ void gemm_block(int64_t m0, int64_t n0, int64_t kbeg,
 // ---------------------------------------------------------------------------
 // Forward layer k: H_{k+1}[m][n] = ReLU(sum_c A[m][c] W_k[n][c] + b_k[n]).
 // grid (ceil(R/64), ceil(N/64)).
-template <bool FIRST>
+template <bool FIRST, bool DROP>
 __global__ __launch_bounds__(GNT) void lyr_fwd_kernel(LyrArgs a, int k, const float* __restrict__ Ain,
                                                       float* __restrict__ Hout, int64_t R) {
     __shared__ int su[GBM], si[GBM];
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(GNT) void lyr_fwd_kernel(LyrArgs a, int k, const fl
         si[threadIdx.x] = it < 0 ? 0 : it;
     }
     if (FIRST) __syncthreads();
-    const Drop dr = drop_of(a);
+    const Drop dr = DROP ? drop_of(a) : Drop{false, 0, 0, 0, 1.f};
     auto ga = [&](int r, int64_t c) -> float {
         const int64_t m = m0 + r;
         if (m >= R || c >= K) return 0.f;
@@ -188,7 +188,8 @@ __global__ __launch_bounds__(GNT) void lyr_fwd_kernel(LyrArgs a, int k, const fl
         } else {
             v = Ain[m * K + c];
         }
-        return dr.on ? v * drop_mul(dr, k, s.base + m, (int)c) : v;
+        if constexpr (DROP) v *= drop_mul(dr, k, s.base + m, (int)c);
+        return v;
     };
     auto gb = [&](int64_t c, int n) -> float {
         const int nn = n0 + n;
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(GNT) void lyr_fwd_kernel(LyrArgs a, int k, const fl
 //   k > 0: dY_{k-1}[m][n] = C * [H_k[m][n] > 0]
 //   k = 0: scatter-add C into grad Um[u_m] (n < dm) / Im[i_m] (n >= dm)
 // grid (ceil(R/64), ceil(s_k/64)).
-template <bool FIRST>
+template <bool FIRST, bool DROP>
 __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, const float* __restrict__ D,
                                                            const float* __restrict__ Hk, float* __restrict__ Dout,
                                                            int64_t R) {
@@ -236,7 +237,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, con
         si[threadIdx.x] = it;
     }
     if (FIRST) __syncthreads();
-    const Drop dr = drop_of(a);
+    const Drop dr = DROP ? drop_of(a) : Drop{false, 0, 0, 0, 1.f};
     auto ga = [&](int r, int64_t j) -> float {
         const int64_t m = m0 + r;
         return (m < R && j < J) ? D[m * J + j] : 0.f;
@@ -258,7 +259,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, con
                     const int64_t m = m0 + rr;
                     if (m >= R) continue;
                     float v = lane_get(acc[ti][tj], r);
-                    if (dr.on) v *= drop_mul(dr, k, s.base + m, n);  // through layer k's input dropout
+                    if constexpr (DROP) v *= drop_mul(dr, k, s.base + m, n);  // through layer k's input dropout
                     if constexpr (FIRST) {
                         const int id = n < DM ? su[rr] : si[rr];
                         if (id >= 0)
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, con
 //   db_k[j]    += sum_m dY_k[m][j]             (the extra column c = s_k of ones)
 // into the slab (tower partials, reduced by ncf_reduce_slab).
 // grid (ceil(J/64), ceil((s_k+1)/64), splits).
-template <bool FIRST>
+template <bool FIRST, bool DROP>
 __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const float* __restrict__ D,
                                                         const float* __restrict__ Ain, int64_t R, int64_t chunk) {
     __shared__ int su[GBK * 64], si[GBK * 64];  // ids of up to 1024 rows of the chunk (FIRST)
@@ -298,7 +299,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
     const float* prm = a.params;
     float* slab = a.slab + (int64_t)(blockIdx.z % lyr_slab_rows(&lay)) * (lay.tower_len + 64);
     const int64_t tb = lay.tower_begin;
-    const Drop dr = drop_of(a);
+    const Drop dr = DROP ? drop_of(a) : Drop{false, 0, 0, 0, 1.f};
     auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
@@ -339,9 +340,9 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
                 if (m >= q1 || c > K) return 0.f;
                 if (c == K) return 1.f;
                 const int e = (int)(m - q0);
-                const float v =
-                    c < DM ? prm[lay.um + (int64_t)su[e] * DM + c] : prm[lay.im + (int64_t)si[e] * DM + (c - DM)];
-                return dr.on ? v * drop_mul(dr, k, s.base + m, c) : v;
+                float v = c < DM ? prm[lay.um + (int64_t)su[e] * DM + c] : prm[lay.im + (int64_t)si[e] * DM + (c - DM)];
+                if constexpr (DROP) v *= drop_mul(dr, k, s.base + m, c);
+                return v;
             };
             auto ga2 = [&](int jr, int64_t m) -> float {
                 const int j = j0 + jr;
@@ -354,8 +355,9 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
             const int c = c0 + cr;
             if (m >= r1 || c > K) return 0.f;
             if (c == K) return 1.f;
-            const float v = Ain[m * K + c];
-            return dr.on ? v * drop_mul(dr, k, s.base + m, c) : v;
+            float v = Ain[m * K + c];
+            if constexpr (DROP) v *= drop_mul(dr, k, s.base + m, c);
+            return v;
         };
         gemm_block<false, false>(j0, c0, r0, r1, ga, gb, ep);
     }
@@ -641,6 +643,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
     const int64_t slab_floats = (int64_t)lyr_slab_rows(&lay) * (lay.tower_len + 64);
     int64_t off = rup64(slab_floats);
     const bool fact = train && mlp && a.fact_part_floats >= 0;
+    const bool drop = train && mlp && lay.dropout > 0.f;  // dropout-masked kernel instantiations
     float* Pj = nullptr;  // factored layer 0: table projections
     if (fact) {
         off += rup64(a.fact_part_floats);  // dW0 partials (ncf_ops.hip fact_partials)
@@ -672,9 +675,15 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
                 if (g0 > 8192) g0 = 8192;
                 hipLaunchKernelGGL(lyr_fwd0_fact_kernel, dim3((unsigned)g0), dim3(GNT), 0, st, a, Pj, H[1], R);
             } else if (k == 0)
-                hipLaunchKernelGGL(lyr_fwd_kernel<true>, grid, dim3(GNT), 0, st, a, k, nullptr, H[1], R);
+                {
+                if (drop) hipLaunchKernelGGL((lyr_fwd_kernel<true, true>), grid, dim3(GNT), 0, st, a, k, nullptr, H[1], R);
+                else hipLaunchKernelGGL((lyr_fwd_kernel<true, false>), grid, dim3(GNT), 0, st, a, k, nullptr, H[1], R);
+            }
             else
-                hipLaunchKernelGGL(lyr_fwd_kernel<false>, grid, dim3(GNT), 0, st, a, k, H[k], H[k + 1], R);
+                {
+                if (drop) hipLaunchKernelGGL((lyr_fwd_kernel<false, true>), grid, dim3(GNT), 0, st, a, k, H[k], H[k + 1], R);
+                else hipLaunchKernelGGL((lyr_fwd_kernel<false, false>), grid, dim3(GNT), 0, st, a, k, H[k], H[k + 1], R);
+            }
         }
     }
     int G = 1;
@@ -714,14 +723,26 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
         splits = (R + chunk - 1) / chunk;
         const dim3 gw((unsigned)((J + GBM - 1) / GBM), (unsigned)((K + 1 + GBN - 1) / GBN), (unsigned)splits);
         if (k == 0)
-            hipLaunchKernelGGL(lyr_bwd_w_kernel<true>, gw, dim3(GNT), 0, st, a, k, Dcur, nullptr, R, chunk);
+            {
+                if (drop) hipLaunchKernelGGL((lyr_bwd_w_kernel<true, true>), gw, dim3(GNT), 0, st, a, k, Dcur, nullptr, R, chunk);
+                else hipLaunchKernelGGL((lyr_bwd_w_kernel<true, false>), gw, dim3(GNT), 0, st, a, k, Dcur, nullptr, R, chunk);
+            }
         else
-            hipLaunchKernelGGL(lyr_bwd_w_kernel<false>, gw, dim3(GNT), 0, st, a, k, Dcur, H[k], R, chunk);
+            {
+                if (drop) hipLaunchKernelGGL((lyr_bwd_w_kernel<false, true>), gw, dim3(GNT), 0, st, a, k, Dcur, H[k], R, chunk);
+                else hipLaunchKernelGGL((lyr_bwd_w_kernel<false, false>), gw, dim3(GNT), 0, st, a, k, Dcur, H[k], R, chunk);
+            }
         const dim3 gd(mt, (unsigned)((K + GBN - 1) / GBN));
         if (k == 0) {
-            hipLaunchKernelGGL(lyr_bwd_data_kernel<true>, gd, dim3(GNT), 0, st, a, k, Dcur, nullptr, nullptr, R);
+            {
+                if (drop) hipLaunchKernelGGL((lyr_bwd_data_kernel<true, true>), gd, dim3(GNT), 0, st, a, k, Dcur, nullptr, nullptr, R);
+                else hipLaunchKernelGGL((lyr_bwd_data_kernel<true, false>), gd, dim3(GNT), 0, st, a, k, Dcur, nullptr, nullptr, R);
+            }
         } else {
-            hipLaunchKernelGGL(lyr_bwd_data_kernel<false>, gd, dim3(GNT), 0, st, a, k, Dcur, H[k], Dnext, R);
+            {
+                if (drop) hipLaunchKernelGGL((lyr_bwd_data_kernel<false, true>), gd, dim3(GNT), 0, st, a, k, Dcur, H[k], Dnext, R);
+                else hipLaunchKernelGGL((lyr_bwd_data_kernel<false, false>), gd, dim3(GNT), 0, st, a, k, Dcur, H[k], Dnext, R);
+            }
             float* tmp = Dcur;
             Dcur = Dnext;
             Dnext = tmp;

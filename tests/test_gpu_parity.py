@@ -746,3 +746,29 @@ def test_module_forward_dropout_train_and_eval():
         ev = m(torch.as_tensor(users, device=DEV), torch.as_tensor(items, device=DEV))
         ev_ref = ref(torch.as_tensor(users), torch.as_tensor(items))
     np.testing.assert_allclose(ev.cpu().numpy(), ev_ref.numpy(), rtol=1e-5, atol=1e-7)
+
+
+def test_engine_loss_history_beyond_65536_batches():
+    """An epoch of 70,001 batches (2 rows each): the loss history grows to the
+    epoch's batch count (the kernels write loss_hist[b % num_batches]) -- the last
+    batch's loss lands in its own slot, nothing past the buffer."""
+    T, B = 3, 2
+    ref, m, eng = _engine_for("NeuMF-end", 8, 3, 50, 80, 41)
+    n = 140001
+    rng = np.random.default_rng(61)
+    users, items = rng.integers(0, 50, n), rng.integers(0, 80, n)
+    labels = (rng.random(n) < 0.3).astype(np.int64)
+    _stream(eng, users, items, labels, B)
+    assert eng.num_batches == 70001 and eng.loss_hist.numel() >= 70001
+    eng.run(T, use_graph=True)
+    eng.ctl[0] = eng.num_batches - 1  # the partial last batch (1 row)
+    eng.run(1, use_graph=False)
+    torch.cuda.synchronize()
+    h = eng.epoch_losses()
+    assert h.shape[0] == 70001 and np.isfinite(h).all()
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    exp = O.train_steps(ref, opt, users[:T * B].reshape(T, B), items[:T * B].reshape(T, B),
+                        labels[:T * B].reshape(T, B))
+    exp.append(O.train_steps(ref, opt, [users[-1:]], [items[-1:]], [labels[-1:]])[0])
+    np.testing.assert_allclose(h[:T], exp[:T], rtol=1e-5)
+    np.testing.assert_allclose(h[-1], exp[-1], rtol=1e-5)

@@ -238,3 +238,17 @@ def test_dropout_hash_restatement_and_statistics():
             assert abs(kp[:, :8].mean() - (1 - p)) < 0.01
         for a, b in ((0, 1), (0, 2)):
             assert abs(np.corrcoef(keep[a].ravel(), keep[b].ravel())[0, 1]) < 0.01
+
+
+def test_prepare_workspace_small_batches():
+    """ncf_prepare_epoch_workspace: batches under 4,096 rows are only shuffled, so no
+    per-batch item histogram is reserved (the reference default batch_size 256 at
+    ml-20m would otherwise reserve ~42 GB)."""
+    import ncf_amd._lib as L
+    n, items = 4970845, 3707
+    small = L.hip().ncf_prepare_epoch_workspace(n, 256, items)
+    assert 0 < small <= 256
+    big = L.hip().ncf_prepare_epoch_workspace(n, 65536, items)
+    nb = (n + 65535) // 65536
+    assert big >= n * 8 + nb * items * 4
+    assert L.hip().ncf_prepare_epoch_workspace(20_000_000, 256, 26744) <= 256
