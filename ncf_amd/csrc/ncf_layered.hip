@@ -500,12 +500,15 @@ __global__ __launch_bounds__(GNT) void lyr_scatter0_kernel(LyrArgs a, const floa
 }
 
 // ---------------------------------------------------------------------------
-// Predict + loss + GMF backward.  G lanes per row (G = min(64, pow2 >= F)),
-// feature f handled by lane f % G, slot f / G (< PSLOTS).  Each block loops over
-// row groups; dwp / dbp / loss accumulate in registers across its rows and are
-// combined once per block (LDS, then one global atomic per value).
-constexpr int PSLOTS = 4;  // F <= 256
-template <bool TRAIN>
+// Predict + loss + GMF backward.  A walker of G lanes (G = min(64, pow2 >= F);
+// feature f on lane f % G, slot f / G < NS) takes PR_ROWS consecutive rows: their
+// operands are loaded first, the G-lane logit reductions of all of them run
+// interleaved, and runs of equal items (each batch is grouped by item,
+// ncf_prepare_epoch) are summed before the GMF item-gradient atomics.  dwp / dbp /
+// loss: registers -> LDS -> one atomic per value per block, into slab row
+// blockIdx % lyr_slab_rows.
+constexpr int PR_ROWS = 8;  // NS <= 4: F <= 256 (LYR_MAX_FACTOR)
+template <bool TRAIN, int NS>
 __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float* __restrict__ HL,
                                                           float* __restrict__ Dout, int64_t R, int G) {
     extern __shared__ float red[];  // [P + 2]: dwp[P], dbp, loss
@@ -524,78 +527,118 @@ __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float
             a.ctl->snap_t = a.ctl->adam_t + 1;
         }
     }
-    const int rpb = GNT / G;
     const int gl = t % G;
-    float accG[PSLOTS], accM[PSLOTS];
+    const int64_t r0 = ((int64_t)blockIdx.x * (GNT / G) + t / G) * PR_ROWS;
+    float wpg[NS], wpm[NS];
 #pragma unroll
-    for (int q = 0; q < PSLOTS; ++q) accG[q] = accM[q] = 0.f;
-    float accB = 0.f, accL = 0.f;
-    const float bp = prm[lay.bp];
-    for (int64_t m0 = (int64_t)blockIdx.x * rpb; m0 < R; m0 += (int64_t)gridDim.x * rpb) {
-        const int64_t m = m0 + t / G;
-        int u, it;
-        row_ids(a, s, m, u, it);
-        const bool valid = m < R && u >= 0;
-        const int uu = u < 0 ? 0 : u, ii = it < 0 ? 0 : it;
-        float part = 0.f;
-        if (valid) {
+    for (int q = 0; q < NS; ++q) {
+        const int f = gl + q * G;
+        wpg[q] = (gmf && f < F) ? wp[f] : 0.f;
+        wpm[q] = (mlp && f < F) ? wp[Pg + f] : 0.f;
+    }
+    // the walker's rows and operands (row_ids: padding rows have user -1)
+    uint64_t rw[PR_ROWS];
+    int us[PR_ROWS], is_[PR_ROWS];
+    bool val[PR_ROWS];
+    float ug[PR_ROWS][NS], ig[PR_ROWS][NS], hv[PR_ROWS][NS];
 #pragma unroll
-            for (int q = 0; q < PSLOTS; ++q) {
-                const int f = gl + q * G;
-                if (f >= F) break;
-                if (gmf) part += wp[f] * (prm[lay.ug + (int64_t)uu * F + f] * prm[lay.ig + (int64_t)ii * F + f]);
-                if (mlp) part += wp[Pg + f] * HL[m * F + f];
-            }
-        }
-        for (int o = G >> 1; o >= 1; o >>= 1) part += __shfl_xor(part, o, 64);
-        const float z = part + bp;
-        if (valid && gl == 0 && a.logits_out != nullptr) a.logits_out[m] = z;
-        if constexpr (TRAIN) {
-            if (valid) {
-                float dz;
-                const uint64_t rw = a.rows[s.base + m];
-                if (a.dz_mode == NCF_DZ_BCE) {
-                    const float y = (float)(uint32_t)(rw >> 63);
-                    dz = (sigmoidf_(z) - y) / s.gb;
-                    if (gl == 0) accL += bce_loss(z, y) / s.gb;
-                } else if (a.dz_mode == NCF_DZ_KD) {
-                    const float y = (float)(uint32_t)(rw >> 63);
-                    float rl;
-                    const float rg = kd_response(z, a.dlogit[s.base + m], a.kd_temp, &rl);
-                    dz = (a.kd_wt * (sigmoidf_(z) - y) + a.kd_wr * rg) / s.gb;
-                    if (gl == 0) accL += (a.kd_wt * bce_loss(z, y) + a.kd_wr * rl) / s.gb;
-                } else {
-                    dz = a.dlogit[s.base + m];
-                }
-                if (gl == 0) accB += dz;
+    for (int k = 0; k < PR_ROWS; ++k) {
+        const int64_t m = r0 + k;
+        const bool in = m < s.nloc;
+        rw[k] = in ? a.rows[s.base + m] : 0;
+        const int u = in ? (int)(uint32_t)rw[k] : -1;
+        val[k] = m < R && u >= 0;
+        us[k] = u < 0 ? 0 : u;
+        is_[k] = val[k] ? (int)((rw[k] >> 32) & 0x7fffffffu) : -1;
+        const int ii = is_[k] < 0 ? 0 : is_[k];
 #pragma unroll
-                for (int q = 0; q < PSLOTS; ++q) {
-                    const int f = gl + q * G;
-                    if (f >= F) break;
-                    if (gmf) {
-                        const float ug = prm[lay.ug + (int64_t)uu * F + f], ig = prm[lay.ig + (int64_t)ii * F + f];
-                        accG[q] += dz * (ug * ig);
-                        const float dg = dz * wp[f];
-                        atomicAdd(a.grads + lay.ug + (int64_t)uu * F + f, dg * ig);
-                        atomicAdd(a.grads + lay.ig + (int64_t)ii * F + f, dg * ug);
-                    }
-                    if (mlp) {
-                        const float h = HL[m * F + f];
-                        accM[q] += dz * h;
-                        Dout[m * F + f] = h > 0.f ? dz * wp[Pg + f] : 0.f;
-                    }
-                }
-            } else if (mlp && m < R) {
-                for (int f = gl; f < F; f += G) Dout[m * F + f] = 0.f;
-            }
+        for (int q = 0; q < NS; ++q) {
+            const int f = gl + q * G;
+            const bool ok = val[k] && f < F;
+            ug[k][q] = (gmf && ok) ? prm[lay.ug + (int64_t)us[k] * F + f] : 0.f;
+            ig[k][q] = (gmf && ok) ? prm[lay.ig + (int64_t)ii * F + f] : 0.f;
+            hv[k][q] = (mlp && ok) ? HL[m * F + f] : 0.f;
         }
     }
+    float z[PR_ROWS];
+#pragma unroll
+    for (int k = 0; k < PR_ROWS; ++k) {
+        float part = 0.f;
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            if (gmf) part += wpg[q] * (ug[k][q] * ig[k][q]);
+            if (mlp) part += wpm[q] * hv[k][q];
+        }
+        z[k] = part;
+    }
+    for (int o = G >> 1; o >= 1; o >>= 1) {
+#pragma unroll
+        for (int k = 0; k < PR_ROWS; ++k) z[k] += __shfl_xor(z[k], o, 64);
+    }
+    const float bp = prm[lay.bp];
+#pragma unroll
+    for (int k = 0; k < PR_ROWS; ++k) {
+        z[k] += bp;
+        if (val[k] && gl == 0 && a.logits_out != nullptr) a.logits_out[r0 + k] = z[k];
+    }
     if constexpr (TRAIN) {
+        float accG[NS], accM[NS], run[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) accG[q] = accM[q] = run[q] = 0.f;
+        float accB = 0.f, accL = 0.f;
+#pragma unroll
+        for (int k = 0; k < PR_ROWS; ++k) {
+            const int64_t m = r0 + k;
+            if (!val[k]) {
+                if (mlp && m < R)
+#pragma unroll
+                    for (int q = 0; q < NS; ++q) {
+                        const int f = gl + q * G;
+                        if (f < F) Dout[m * F + f] = 0.f;
+                    }
+                continue;
+            }
+            float dz;
+            if (a.dz_mode == NCF_DZ_BCE) {
+                const float y = (float)(uint32_t)(rw[k] >> 63);
+                dz = (sigmoidf_(z[k]) - y) / s.gb;
+                if (gl == 0) accL += bce_loss(z[k], y) / s.gb;
+            } else if (a.dz_mode == NCF_DZ_KD) {
+                const float y = (float)(uint32_t)(rw[k] >> 63);
+                float rl;
+                const float rg = kd_response(z[k], a.dlogit[s.base + m], a.kd_temp, &rl);
+                dz = (a.kd_wt * (sigmoidf_(z[k]) - y) + a.kd_wr * rg) / s.gb;
+                if (gl == 0) accL += (a.kd_wt * bce_loss(z[k], y) + a.kd_wr * rl) / s.gb;
+            } else {
+                dz = a.dlogit[s.base + m];
+            }
+            if (gl == 0) accB += dz;
+            const bool end = k + 1 >= PR_ROWS || is_[k + 1 < PR_ROWS ? k + 1 : k] != is_[k];  // item run ends
+#pragma unroll
+            for (int q = 0; q < NS; ++q) {
+                const int f = gl + q * G;
+                if (f >= F) continue;
+                if (gmf) {
+                    accG[q] += dz * (ug[k][q] * ig[k][q]);
+                    const float dg = dz * wpg[q];
+                    atomicAdd(a.grads + lay.ug + (int64_t)us[k] * F + f, dg * ig[k][q]);
+                    run[q] += dg * ug[k][q];
+                    if (end) {
+                        atomicAdd(a.grads + lay.ig + (int64_t)is_[k] * F + f, run[q]);
+                        run[q] = 0.f;
+                    }
+                }
+                if (mlp) {
+                    accM[q] += dz * hv[k][q];
+                    Dout[m * F + f] = hv[k][q] > 0.f ? dz * wpm[q] : 0.f;
+                }
+            }
+        }
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < PSLOTS; ++q) {
+        for (int q = 0; q < NS; ++q) {
             const int f = gl + q * G;
-            if (f >= F) break;
+            if (f >= F) continue;
             if (gmf) atomicAdd(&red[f], accG[q]);
             if (mlp) atomicAdd(&red[Pg + f], accM[q]);
         }
@@ -605,11 +648,12 @@ __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float
         }
         __syncthreads();
         const int64_t tb = lay.tower_begin;
+        float* slab = a.slab + (int64_t)(blockIdx.x % lyr_slab_rows(&lay)) * (lay.tower_len + 64);
         for (int e = t; e < P + 2; e += GNT) {
             const float v = red[e];
             if (v == 0.f) continue;
             const int64_t off = e < P ? (lay.wp - tb) + e : (e == P ? (lay.bp - tb) : lay.tower_len);
-            atomicAdd(a.slab + (int64_t)(blockIdx.x % lyr_slab_rows(&lay)) * (lay.tower_len + 64) + off, v);
+            atomicAdd(slab + off, v);
         }
     }
 }
@@ -689,18 +733,26 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
     int G = 1;
     while (G < F && G < 64) G <<= 1;
     const int P = (lay.model_type == NCF_MODEL_NEUMF ? 2 : 1) * F;
-    const int64_t rpb = GNT / G;
-    int64_t pgl = (R + rpb - 1) / rpb;
-    if (pgl > 2048) pgl = 2048;  // blocks loop over row groups beyond this
-    const unsigned pg = (unsigned)pgl;
+    const int NS = (F + G - 1) / G;  // <= 4 (F <= 256)
+    const int64_t rows_per_block = (int64_t)(GNT / G) * PR_ROWS;
+    const unsigned pg = (unsigned)((R + rows_per_block - 1) / rows_per_block);
     const size_t lds = (size_t)(P + 2) * 4;
     float* Dtop = Da;
-    if (train)
-        hipLaunchKernelGGL(lyr_predict_kernel<true>, dim3(pg), dim3(GNT), lds, st, a, mlp ? H[L] : nullptr, Dtop, R,
-                           G);
-    else
-        hipLaunchKernelGGL(lyr_predict_kernel<false>, dim3(pg), dim3(GNT), lds, st, a, mlp ? H[L] : nullptr, nullptr,
-                           R, G);
+    float* HLp = mlp ? H[L] : nullptr;
+#define NCF_PRED(T, N) hipLaunchKernelGGL((lyr_predict_kernel<T, N>), dim3(pg), dim3(GNT), lds, st, a, HLp, \
+                                          T ? Dtop : nullptr, R, G)
+    switch (NS * 2 + (train ? 1 : 0)) {
+        case 2: NCF_PRED(false, 1); break;
+        case 3: NCF_PRED(true, 1); break;
+        case 4: NCF_PRED(false, 2); break;
+        case 5: NCF_PRED(true, 2); break;
+        case 6: NCF_PRED(false, 3); break;
+        case 7: NCF_PRED(true, 3); break;
+        case 8: NCF_PRED(false, 4); break;
+        case 9: NCF_PRED(true, 4); break;
+        default: return NCF_E_UNSUPPORTED;
+    }
+#undef NCF_PRED
     if (!train || !mlp) return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
     float* Dcur = Da;
     float* Dnext = Db;
