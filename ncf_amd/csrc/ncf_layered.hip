@@ -155,10 +155,74 @@ __device__ __forceinline__ void gemm_block(int64_t m0, int64_t n0, int64_t kbeg,
     ep(acc, wm, wn, l);
 }
 
+// Same tile and MFMA schedule with one 16-byte operand load per thread per K step:
+// ga4 / gb4 return four elements along the operand's contiguous dimension (KC: K,
+// else M/N), which must be a multiple of 4 with 16-byte aligned rows (factor_num
+// % 4 == 0).  KC tile [64][16]: thread t loads row t / 4, k 4 (t % 4) .. + 3;
+// otherwise [16][64]: k t / 16, columns 4 (t % 16) .. + 3 (one LDS f4 store).
+template <bool AKC, bool BKC, class GA, class GB, class EP>
+__device__ __forceinline__ void gemm_block_v(int64_t kbeg, int64_t kend, GA ga4, GB gb4, EP ep) {
+    __shared__ __attribute__((aligned(16))) float As[2][GBK][GBM + GPAD];
+    __shared__ __attribute__((aligned(16))) float Bs[2][GBK][GBN + GPAD];
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+    const int a_mn = AKC ? (t >> 2) : 4 * (t & 15), a_k = AKC ? 4 * (t & 3) : (t >> 4);
+    const int b_mn = BKC ? (t >> 2) : 4 * (t & 15), b_k = BKC ? 4 * (t & 3) : (t >> 4);
+    f4 ra, rb;
+    auto load = [&](int64_t k0) {
+        ra = ga4(a_mn, k0 + a_k);
+        rb = gb4(k0 + b_k, b_mn);
+    };
+    auto store = [&](int buf) {
+        if constexpr (AKC) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) As[buf][a_k + i][a_mn] = lane_get(ra, i);
+        } else {
+            *reinterpret_cast<f4*>(&As[buf][a_k][a_mn]) = ra;
+        }
+        if constexpr (BKC) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Bs[buf][b_k + i][b_mn] = lane_get(rb, i);
+        } else {
+            *reinterpret_cast<f4*>(&Bs[buf][b_k][b_mn]) = rb;
+        }
+    };
+    f4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    load(kbeg);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t k0 = kbeg; k0 < kend; k0 += GBK) {
+        const bool more = k0 + GBK < kend;
+        if (more) load(k0 + GBK);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int kk = 4 * s + (l >> 4);
+            const float a0 = As[buf][kk][wm + (l & 15)], a1 = As[buf][kk][wm + 16 + (l & 15)];
+            const float b0 = Bs[buf][kk][wn + (l & 15)], b1 = Bs[buf][kk][wn + 16 + (l & 15)];
+            acc[0][0] = MFMA4(a0, b0, acc[0][0]);
+            acc[0][1] = MFMA4(a0, b1, acc[0][1]);
+            acc[1][0] = MFMA4(a1, b0, acc[1][0]);
+            acc[1][1] = MFMA4(a1, b1, acc[1][1]);
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    ep(acc, wm, wn, l);
+}
+
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
+
 // ---------------------------------------------------------------------------
 // Forward layer k: H_{k+1}[m][n] = ReLU(sum_c A[m][c] W_k[n][c] + b_k[n]).
 // grid (ceil(R/64), ceil(N/64)).
-template <bool FIRST, bool DROP>
+template <bool FIRST, bool DROP, bool VEC>
 __global__ __launch_bounds__(GNT) void lyr_fwd_kernel(LyrArgs a, int k, const float* __restrict__ Ain,
                                                       float* __restrict__ Hout, int64_t R) {
     __shared__ int su[GBM], si[GBM];
@@ -210,7 +274,30 @@ __global__ __launch_bounds__(GNT) void lyr_fwd_kernel(LyrArgs a, int k, const fl
                 }
             }
     };
-    gemm_block<true, true>(m0, n0, 0, K, ga, gb, ep);
+    if constexpr (VEC) {
+        auto ga4 = [&](int r, int64_t c) -> f4 {
+            const int64_t m = m0 + r;
+            if (m >= R || c >= K) return zero4();
+            f4 v;
+            if constexpr (FIRST) {
+                v = c < DM ? ld4(prm + lay.um + (int64_t)su[r] * DM + c) : ld4(prm + lay.im + (int64_t)si[r] * DM + (c - DM));
+            } else {
+                v = ld4(Ain + m * K + c);
+            }
+            if constexpr (DROP) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] *= drop_mul(dr, k, s.base + m, (int)c + i);
+            }
+            return v;
+        };
+        auto gb4 = [&](int64_t c, int n) -> f4 {
+            const int nn = n0 + n;
+            return (nn < N && c < K) ? ld4(W + (int64_t)nn * K + c) : zero4();
+        };
+        gemm_block_v<true, true>(0, K, ga4, gb4, ep);
+    } else {
+        gemm_block<true, true>(m0, n0, 0, K, ga, gb, ep);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -218,7 +305,7 @@ __global__ __launch_bounds__(GNT) void lyr_fwd_kernel(LyrArgs a, int k, const fl
 //   k > 0: dY_{k-1}[m][n] = C * [H_k[m][n] > 0]
 //   k = 0: scatter-add C into grad Um[u_m] (n < dm) / Im[i_m] (n >= dm)
 // grid (ceil(R/64), ceil(s_k/64)).
-template <bool FIRST, bool DROP>
+template <bool FIRST, bool DROP, bool VEC>
 __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, const float* __restrict__ D,
                                                            const float* __restrict__ Hk, float* __restrict__ Dout,
                                                            int64_t R) {
@@ -272,7 +359,19 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, con
                 }
             }
     };
-    gemm_block<true, false>(m0, n0, 0, J, ga, gb, ep);
+    if constexpr (VEC) {
+        auto ga4 = [&](int r, int64_t j) -> f4 {
+            const int64_t m = m0 + r;
+            return (m < R && j < J) ? ld4(D + m * J + j) : zero4();
+        };
+        auto gb4 = [&](int64_t j, int n) -> f4 {
+            const int nn = n0 + n;
+            return (j < J && nn < N) ? ld4(W + j * N + nn) : zero4();
+        };
+        gemm_block_v<true, false>(0, J, ga4, gb4, ep);
+    } else {
+        gemm_block<true, false>(m0, n0, 0, J, ga, gb, ep);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -281,7 +380,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, con
 //   db_k[j]    += sum_m dY_k[m][j]             (the extra column c = s_k of ones)
 // into the slab (tower partials, reduced by ncf_reduce_slab).
 // grid (ceil(J/64), ceil((s_k+1)/64), splits).
-template <bool FIRST, bool DROP>
+template <bool FIRST, bool DROP, bool VEC>
 __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const float* __restrict__ D,
                                                         const float* __restrict__ Ain, int64_t R, int64_t chunk) {
     __shared__ int su[GBK * 64], si[GBK * 64];  // ids of up to 1024 rows of the chunk (FIRST)
@@ -348,7 +447,28 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
                 const int j = j0 + jr;
                 return (m < q1 && j < J) ? D[m * J + j] : 0.f;
             };
-            gemm_block<false, false>(j0, c0, q0, q1, ga2, gb, ep);
+            if constexpr (VEC) {
+                auto ga4 = [&](int jr, int64_t m) -> f4 {
+                    const int j = j0 + jr;
+                    return (m < q1 && j < J) ? ld4(D + m * J + j) : zero4();
+                };
+                auto gb4 = [&](int64_t m, int cr) -> f4 {
+                    const int c = c0 + cr;
+                    if (m >= q1 || c > K) return zero4();
+                    if (c == K) return f4{1.f, 0.f, 0.f, 0.f};  // the ones column of db
+                    const int e = (int)(m - q0);
+                    f4 v = c < DM ? ld4(prm + lay.um + (int64_t)su[e] * DM + c)
+                                  : ld4(prm + lay.im + (int64_t)si[e] * DM + (c - DM));
+                    if constexpr (DROP) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) v[i] *= drop_mul(dr, k, s.base + m, c + i);
+                    }
+                    return v;
+                };
+                gemm_block_v<false, false>(q0, q1, ga4, gb4, ep);
+            } else {
+                gemm_block<false, false>(j0, c0, q0, q1, ga2, gb, ep);
+            }
         }
     } else {
         auto gb = [&](int64_t m, int cr) -> float {
@@ -359,7 +479,26 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
             if constexpr (DROP) v *= drop_mul(dr, k, s.base + m, c);
             return v;
         };
-        gemm_block<false, false>(j0, c0, r0, r1, ga, gb, ep);
+        if constexpr (VEC) {
+            auto ga4 = [&](int jr, int64_t m) -> f4 {
+                const int j = j0 + jr;
+                return (m < r1 && j < J) ? ld4(D + m * J + j) : zero4();
+            };
+            auto gb4 = [&](int64_t m, int cr) -> f4 {
+                const int c = c0 + cr;
+                if (m >= r1 || c > K) return zero4();
+                if (c == K) return f4{1.f, 0.f, 0.f, 0.f};  // the ones column of db
+                f4 v = ld4(Ain + m * K + c);
+                if constexpr (DROP) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) v[i] *= drop_mul(dr, k, s.base + m, c + i);
+                }
+                return v;
+            };
+            gemm_block_v<false, false>(r0, r1, ga4, gb4, ep);
+        } else {
+            gemm_block<false, false>(j0, c0, r0, r1, ga, gb, ep);
+        }
     }
 }
 
@@ -399,7 +538,17 @@ __global__ __launch_bounds__(GNT) void lyr_proj_kernel(LyrArgs a, float* __restr
                 }
             }
     };
-    gemm_block<true, true>(m0, n0, 0, DM, ga, gb, ep);
+    auto ga4 = [&](int r, int64_t c) -> f4 {
+        const int64_t m = m0 + r;
+        return (m < nrows && c < DM) ? ld4(X + m * DM + c) : zero4();
+    };
+    auto gb4 = [&](int64_t c, int n) -> f4 {
+        const int nn = n0 + n;
+        return (nn < DM && c < DM) ? ld4(W + (int64_t)nn * 2 * DM + c) : zero4();
+    };
+    (void)ga;
+    (void)gb;
+    gemm_block_v<true, true>(0, DM, ga4, gb4, ep);  // factored path: dm in {8, ..., 128}
 }
 
 // H_1[m][n] = ReLU(P[u_m][n] + P[U + i_m][n] + b_0[n]), four outputs per thread
@@ -688,6 +837,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
     int64_t off = rup64(slab_floats);
     const bool fact = train && mlp && a.fact_part_floats >= 0;
     const bool drop = train && mlp && lay.dropout > 0.f;  // dropout-masked kernel instantiations
+    const bool vec = (F % 4) == 0;  // every tower width a multiple of 4: 16-byte operand loads
     float* Pj = nullptr;  // factored layer 0: table projections
     if (fact) {
         off += rup64(a.fact_part_floats);  // dW0 partials (ncf_ops.hip fact_partials)
@@ -720,13 +870,15 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
                 hipLaunchKernelGGL(lyr_fwd0_fact_kernel, dim3((unsigned)g0), dim3(GNT), 0, st, a, Pj, H[1], R);
             } else if (k == 0)
                 {
-                if (drop) hipLaunchKernelGGL((lyr_fwd_kernel<true, true>), grid, dim3(GNT), 0, st, a, k, nullptr, H[1], R);
-                else hipLaunchKernelGGL((lyr_fwd_kernel<true, false>), grid, dim3(GNT), 0, st, a, k, nullptr, H[1], R);
+                if (drop) hipLaunchKernelGGL((lyr_fwd_kernel<true, true, false>), grid, dim3(GNT), 0, st, a, k, nullptr, H[1], R);
+                else if (vec) hipLaunchKernelGGL((lyr_fwd_kernel<true, false, true>), grid, dim3(GNT), 0, st, a, k, nullptr, H[1], R);
+                else hipLaunchKernelGGL((lyr_fwd_kernel<true, false, false>), grid, dim3(GNT), 0, st, a, k, nullptr, H[1], R);
             }
             else
                 {
-                if (drop) hipLaunchKernelGGL((lyr_fwd_kernel<false, true>), grid, dim3(GNT), 0, st, a, k, H[k], H[k + 1], R);
-                else hipLaunchKernelGGL((lyr_fwd_kernel<false, false>), grid, dim3(GNT), 0, st, a, k, H[k], H[k + 1], R);
+                if (drop) hipLaunchKernelGGL((lyr_fwd_kernel<false, true, false>), grid, dim3(GNT), 0, st, a, k, H[k], H[k + 1], R);
+                else if (vec) hipLaunchKernelGGL((lyr_fwd_kernel<false, false, true>), grid, dim3(GNT), 0, st, a, k, H[k], H[k + 1], R);
+                else hipLaunchKernelGGL((lyr_fwd_kernel<false, false, false>), grid, dim3(GNT), 0, st, a, k, H[k], H[k + 1], R);
             }
         }
     }
@@ -776,24 +928,28 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
         const dim3 gw((unsigned)((J + GBM - 1) / GBM), (unsigned)((K + 1 + GBN - 1) / GBN), (unsigned)splits);
         if (k == 0)
             {
-                if (drop) hipLaunchKernelGGL((lyr_bwd_w_kernel<true, true>), gw, dim3(GNT), 0, st, a, k, Dcur, nullptr, R, chunk);
-                else hipLaunchKernelGGL((lyr_bwd_w_kernel<true, false>), gw, dim3(GNT), 0, st, a, k, Dcur, nullptr, R, chunk);
+                if (drop) hipLaunchKernelGGL((lyr_bwd_w_kernel<true, true, false>), gw, dim3(GNT), 0, st, a, k, Dcur, nullptr, R, chunk);
+                else if (vec) hipLaunchKernelGGL((lyr_bwd_w_kernel<true, false, true>), gw, dim3(GNT), 0, st, a, k, Dcur, nullptr, R, chunk);
+                else hipLaunchKernelGGL((lyr_bwd_w_kernel<true, false, false>), gw, dim3(GNT), 0, st, a, k, Dcur, nullptr, R, chunk);
             }
         else
             {
-                if (drop) hipLaunchKernelGGL((lyr_bwd_w_kernel<false, true>), gw, dim3(GNT), 0, st, a, k, Dcur, H[k], R, chunk);
-                else hipLaunchKernelGGL((lyr_bwd_w_kernel<false, false>), gw, dim3(GNT), 0, st, a, k, Dcur, H[k], R, chunk);
+                if (drop) hipLaunchKernelGGL((lyr_bwd_w_kernel<false, true, false>), gw, dim3(GNT), 0, st, a, k, Dcur, H[k], R, chunk);
+                else if (vec) hipLaunchKernelGGL((lyr_bwd_w_kernel<false, false, true>), gw, dim3(GNT), 0, st, a, k, Dcur, H[k], R, chunk);
+                else hipLaunchKernelGGL((lyr_bwd_w_kernel<false, false, false>), gw, dim3(GNT), 0, st, a, k, Dcur, H[k], R, chunk);
             }
         const dim3 gd(mt, (unsigned)((K + GBN - 1) / GBN));
         if (k == 0) {
             {
-                if (drop) hipLaunchKernelGGL((lyr_bwd_data_kernel<true, true>), gd, dim3(GNT), 0, st, a, k, Dcur, nullptr, nullptr, R);
-                else hipLaunchKernelGGL((lyr_bwd_data_kernel<true, false>), gd, dim3(GNT), 0, st, a, k, Dcur, nullptr, nullptr, R);
+                if (drop) hipLaunchKernelGGL((lyr_bwd_data_kernel<true, true, false>), gd, dim3(GNT), 0, st, a, k, Dcur, nullptr, nullptr, R);
+                else if (vec) hipLaunchKernelGGL((lyr_bwd_data_kernel<true, false, true>), gd, dim3(GNT), 0, st, a, k, Dcur, nullptr, nullptr, R);
+                else hipLaunchKernelGGL((lyr_bwd_data_kernel<true, false, false>), gd, dim3(GNT), 0, st, a, k, Dcur, nullptr, nullptr, R);
             }
         } else {
             {
-                if (drop) hipLaunchKernelGGL((lyr_bwd_data_kernel<false, true>), gd, dim3(GNT), 0, st, a, k, Dcur, H[k], Dnext, R);
-                else hipLaunchKernelGGL((lyr_bwd_data_kernel<false, false>), gd, dim3(GNT), 0, st, a, k, Dcur, H[k], Dnext, R);
+                if (drop) hipLaunchKernelGGL((lyr_bwd_data_kernel<false, true, false>), gd, dim3(GNT), 0, st, a, k, Dcur, H[k], Dnext, R);
+                else if (vec) hipLaunchKernelGGL((lyr_bwd_data_kernel<false, false, true>), gd, dim3(GNT), 0, st, a, k, Dcur, H[k], Dnext, R);
+                else hipLaunchKernelGGL((lyr_bwd_data_kernel<false, false, false>), gd, dim3(GNT), 0, st, a, k, Dcur, H[k], Dnext, R);
             }
             float* tmp = Dcur;
             Dcur = Dnext;
