@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 11
+#define NCF_ABI_VERSION 12
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -141,8 +141,13 @@ int64_t ncf_slab_stride(const ncf_layout *lay);
  * dz_mode NCF_DZ_BCE: the label is bit 63 of the row, `dlogit` is ignored (may be NULL).
  * dz_mode NCF_DZ_DLOGIT: dlogit[row] holds dL/dlogit per row (same indexing as rows).
  * logits_out (optional, may be NULL): per-row logits of this rank's rows.
+ * user_order (optional, may be NULL; since ABI 12): ncf_user_order of the same rows,
+ * batch_global and world.  Where ncf_uses_user_order(lay), the step then sums the
+ * user-side layer-0 gradients over runs of equal users before its atomics instead
+ * of adding per row (same gradient up to fp32 summation order).
  */
 int ncf_train_step(const ncf_layout *lay, const float *params, float *grads, const uint64_t *rows,
+                   const int64_t *user_order,
                    const float *dlogit, ncf_step_ctl *ctl, int64_t batch_global, int world,
                    int rank, int dz_mode, void *workspace, int64_t workspace_bytes,
                    float *logits_out, void *stream);
@@ -160,7 +165,7 @@ int ncf_train_step(const ncf_layout *lay, const float *params, float *grads, con
  * ncf_kd_feature_step.
  */
 int ncf_train_step_kd(const ncf_layout *lay, const float *params, float *grads, const uint64_t *rows,
-                      const float *teacher_logits, ncf_step_ctl *ctl, int64_t batch_global, int world,
+                      const int64_t *user_order, const float *teacher_logits, ncf_step_ctl *ctl, int64_t batch_global, int world,
                       int rank, float w_task, float w_resp, float temperature, void *workspace,
                       int64_t workspace_bytes,
                       float *logits_out, void *stream);
@@ -308,6 +313,21 @@ int64_t ncf_prepare_epoch_workspace(int64_t n, int64_t batch_global, int item_nu
 int ncf_prepare_epoch(const uint64_t *rows, const int64_t *perm, int64_t n, int64_t batch_global,
                       int item_num, uint64_t *rows_out, void *workspace, int64_t workspace_bytes,
                       void *stream);
+
+/*
+ * User order of an epoch stream (since ABI 12): each global batch b of rows[0 .. n)
+ * is cut into the `world` rank slices ncf_train_step takes (cnt = its rows, slice r =
+ * [r*ceil(cnt/world), ...)), and order[slice start + k], k over the slice, lists the
+ * slice's rows by ascending user id, padding rows (user -1) last, as entries
+ * (int64_t)user << 32 | offset (offset 0-based within the slice, user -1 for
+ * padding): the step reads the user with the offset.  The order among rows of one
+ * user is unspecified.  One counting sort per slice in LDS: user_num <= 32767.
+ * Computed once per epoch; the step reads it where ncf_uses_user_order(lay) (the
+ * layered factored layer 0).
+ */
+int ncf_user_order(const uint64_t *rows, int64_t n, int64_t batch_global, int world, int user_num,
+                   int64_t *order, void *stream);
+int ncf_uses_user_order(const ncf_layout *lay);
 
 /*
  * Device epoch pipeline: the DataLoader(shuffle=True) permutation and the epoch's

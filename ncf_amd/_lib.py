@@ -29,7 +29,7 @@ NCF_E_ARG = -2
 NCF_E_LAUNCH = -3
 MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
 DZ_BCE, DZ_DLOGIT, DZ_KD = 0, 1, 2
-ABI_VERSION = 11  # include/ncf_hip.h NCF_ABI_VERSION
+ABI_VERSION = 12  # include/ncf_hip.h NCF_ABI_VERSION
 PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 LAYOUT_PER_ROW_L0, LAYOUT_WG_SHIFT, LAYOUT_WG_MASK = 0x1, 8, 0xFFF  # ncf_layout.flags (ncf_layout_tune)
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
@@ -63,9 +63,9 @@ _HIP_PROTOS = {
     "ncf_layout_init": (ctypes.c_int, [ctypes.c_int] * 5 + [ctypes.POINTER(NcfLayout)]),
     "ncf_slab_rows": (ctypes.c_int, []),
     "ncf_layout_tune": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_i64]),
-    "ncf_train_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp,
+    "ncf_train_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_vp, c_i64, c_vp, c_vp]),
-    "ncf_train_step_kd": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp,
+    "ncf_train_step_kd": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                          c_i64, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float,
                                          ctypes.c_float, c_vp, c_i64, c_vp, c_vp]),
     "ncf_kd_feature_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, ctypes.POINTER(NcfLayout), c_vp,
@@ -101,6 +101,8 @@ _HIP_PROTOS = {
     "ncf_randperm_workspace": (c_i64, [c_i64]),
     "ncf_randperm": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "ncf_build_rows": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, ctypes.c_int, c_vp, c_vp]),
+    "ncf_user_order": (ctypes.c_int, [c_vp, c_i64, c_i64, ctypes.c_int, ctypes.c_int, c_vp, c_vp]),
+    "ncf_uses_user_order": (ctypes.c_int, [c_vp]),
 }
 
 _SAMPLER_PROTOS = {

@@ -27,6 +27,7 @@ struct LyrArgs {
     const float* params;
     float* grads;            // train: dense gradient buffer (embedding scatter targets)
     const uint64_t* rows;    // packed rows (NCF_ROW_PACK)
+    const int64_t* uorder;   // train, factored layer 0: ncf_user_order of rows (nullptr: per-row user atomics)
     const float* dlogit;     // NCF_DZ_DLOGIT: dL/dlogit per row
     ncf_step_ctl* ctl;       // train: batch selection; nullptr = forward over fwd_n rows
     int64_t batch_global, fwd_n;

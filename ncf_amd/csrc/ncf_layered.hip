@@ -581,71 +581,101 @@ __global__ __launch_bounds__(GNT) void lyr_fwd0_fact_kernel(LyrArgs a, const flo
 }
 
 // dY_0 rows -> grads[um][u] and grads[im][i] (width DM), db_0 -> slab.  A walker of
-// 32 lanes takes SC_ROWS consecutive rows (lane = feature, + 32 per column group):
-// its rows' values are loaded first, then the walk sums runs of equal items (each
-// batch is grouped by item, ncf_prepare_epoch) before their atomics; users add per
-// row.  db_0: walker sums -> LDS -> one atomic per feature per block.
-constexpr int SC_LANES = 32, SC_ROWS = 16, SC_COLS = 4;  // DM <= 128
-__global__ __launch_bounds__(GNT) void lyr_scatter0_kernel(LyrArgs a, const float* __restrict__ D0) {
-    __shared__ float sdb[GNT / SC_LANES][SC_LANES * SC_COLS];
+// DM lanes (one feature each; 256 / DM walkers per block, a walker may span two
+// waves: nothing crosses lanes) takes SC_ROWS consecutive rows: its rows' values are
+// loaded first, then the walk sums runs of equal items (each batch is grouped by
+// item, ncf_prepare_epoch) before their atomics.  Users: with the epoch's user
+// order (UORD, ncf_user_order) the walker takes the same number of consecutive
+// positions of that order and sums runs of equal users likewise (a second, gathered
+// pass over D0: ~10 rows per user in a 65,536-row batch of ML-1M, so ~5x fewer user
+// atomics); without it, one atomic per row and feature.  One feature per lane keeps
+// the grid at 4 x 65,536 / SC_ROWS waves for a dm-128 batch of 65,536: the dependent
+// loads (order entry -> D0 row) are latency-bound and need the waves.
+// db_0: walker sums -> LDS -> one atomic per feature per block; 1,024-thread blocks
+// (8 walkers at dm 128) keep those slab atomics 4x fewer than 256-thread ones.
+constexpr int SC_ROWS = 16, SC_NT = 1024;
+template <int DM, bool UORD>
+__global__ __launch_bounds__(SC_NT) void lyr_scatter0_kernel(LyrArgs a, const float* __restrict__ D0) {
+    constexpr int NW = SC_NT / DM;  // walkers per block
+    __shared__ float sdb[NW][DM];
     const Sel s = select_rows(a);
     const ncf_layout& lay = a.lay;
-    const int DM = lay.factor_num << (lay.num_layers - 1);
-    const int lane = threadIdx.x % SC_LANES, wk = threadIdx.x / SC_LANES;
-    const int64_t r0 = ((int64_t)blockIdx.x * (GNT / SC_LANES) + wk) * SC_ROWS;
-    float db[SC_COLS];
-#pragma unroll
-    for (int q = 0; q < SC_COLS; ++q) db[q] = 0.f;
+    const int n = threadIdx.x % DM, wk = threadIdx.x / DM;
+    const int64_t r0 = ((int64_t)blockIdx.x * NW + wk) * SC_ROWS;
+    float db = 0.f;
     if (r0 < s.nloc) {
         const int nr = (int)(s.nloc - r0 < SC_ROWS ? s.nloc - r0 : SC_ROWS);
         int us[SC_ROWS], is[SC_ROWS];
-        float v[SC_ROWS][SC_COLS];
+        float v[SC_ROWS];
 #pragma unroll
         for (int k = 0; k < SC_ROWS; ++k) {
             const int64_t m = r0 + (k < nr ? k : 0);
             const uint64_t rw = a.rows[s.base + m];
             us[k] = (int)(uint32_t)rw;
             is[k] = us[k] < 0 ? -1 : (int)((rw >> 32) & 0x7fffffffu);  // row_ids: padding rows add nothing
-#pragma unroll
-            for (int q = 0; q < SC_COLS; ++q) {
-                const int n = lane + SC_LANES * q;
-                v[k][q] = (n < DM) ? D0[m * DM + n] : 0.f;
-            }
+            v[k] = D0[m * DM + n];
         }
-        float run[SC_COLS];
-#pragma unroll
-        for (int q = 0; q < SC_COLS; ++q) run[q] = 0.f;
+        float run = 0.f;
 #pragma unroll
         for (int k = 0; k < SC_ROWS; ++k) {
-            const bool in = k < nr;
-            const bool end = k + 1 >= nr || is[k + 1 < SC_ROWS ? k + 1 : k] != is[k];  // item run ends here
+            if (k < nr) {
+                const bool end = k + 1 >= nr || is[k + 1 < SC_ROWS ? k + 1 : k] != is[k];  // item run ends here
+                db += v[k];
+                if (!UORD && us[k] >= 0) atomicAdd(a.grads + lay.um + (int64_t)us[k] * DM + n, v[k]);
+                run += v[k];
+                if (end) {
+                    if (is[k] >= 0) atomicAdd(a.grads + lay.im + (int64_t)is[k] * DM + n, run);
+                    run = 0.f;
+                }
+            }
+        }
+        if constexpr (UORD) {
+            int64_t ms[SC_ROWS];
 #pragma unroll
-            for (int q = 0; q < SC_COLS; ++q) {
-                const int n = lane + SC_LANES * q;
-                if (in && n < DM) {
-                    db[q] += v[k][q];
-                    if (us[k] >= 0) atomicAdd(a.grads + lay.um + (int64_t)us[k] * DM + n, v[k][q]);
-                    run[q] += v[k][q];
+            for (int k = 0; k < SC_ROWS; ++k) {
+                const int64_t e = a.uorder[s.base + r0 + (k < nr ? k : 0)];  // user << 32 | offset
+                const int64_t m = (int64_t)(uint32_t)e;
+                const bool ok = m < s.nloc;
+                ms[k] = ok ? m : 0;
+                us[k] = ok ? (int)(e >> 32) : -1;
+            }
+#pragma unroll
+            for (int k = 0; k < SC_ROWS; ++k) v[k] = D0[ms[k] * DM + n];
+            run = 0.f;
+#pragma unroll
+            for (int k = 0; k < SC_ROWS; ++k) {
+                if (k < nr) {
+                    const bool end = k + 1 >= nr || us[k + 1 < SC_ROWS ? k + 1 : k] != us[k];  // user run ends here
+                    run += v[k];
                     if (end) {
-                        if (is[k] >= 0) atomicAdd(a.grads + lay.im + (int64_t)is[k] * DM + n, run[q]);
-                        run[q] = 0.f;
+                        if (us[k] >= 0) atomicAdd(a.grads + lay.um + (int64_t)us[k] * DM + n, run);
+                        run = 0.f;
                     }
                 }
             }
         }
     }
-#pragma unroll
-    for (int q = 0; q < SC_COLS; ++q) sdb[wk][lane + SC_LANES * q] = db[q];
+    sdb[wk][n] = db;
     __syncthreads();
-    for (int n = threadIdx.x; n < DM; n += GNT) {
+    if (threadIdx.x < DM) {  // DM <= 128 < SC_NT
         float t = 0.f;
 #pragma unroll
-        for (int k = 0; k < GNT / SC_LANES; ++k) t += sdb[k][n];
+        for (int k = 0; k < NW; ++k) t += sdb[k][threadIdx.x];
         if (t != 0.f)
             atomicAdd(a.slab + (int64_t)(blockIdx.x % lyr_slab_rows(&lay)) * (lay.tower_len + 64) +
-                          (lay.b[0] - lay.tower_begin) + n,
+                          (lay.b[0] - lay.tower_begin) + threadIdx.x,
                       t);
     }
+}
+
+template <int DM>
+static void launch_scatter0(const LyrArgs& a, const float* D0, int64_t R, hipStream_t st) {
+    const int64_t per_block = (int64_t)(SC_NT / DM) * SC_ROWS;
+    const dim3 grid((unsigned)((R + per_block - 1) / per_block));
+    if (a.uorder)
+        hipLaunchKernelGGL((lyr_scatter0_kernel<DM, true>), grid, dim3(SC_NT), 0, st, a, D0);
+    else
+        hipLaunchKernelGGL((lyr_scatter0_kernel<DM, false>), grid, dim3(SC_NT), 0, st, a, D0);
 }
 
 // ---------------------------------------------------------------------------
@@ -911,9 +941,14 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
     for (int k = L - 1; k >= 0; --k) {
         const int K = (2 * DM) >> k, J = K / 2;
         if (k == 0 && fact) {  // dY_0 into the table rows; dW0 / dUm / dIm by fact_expand_kernel
-            const int64_t per_block = (int64_t)(GNT / SC_LANES) * SC_ROWS;
-            hipLaunchKernelGGL(lyr_scatter0_kernel, dim3((unsigned)((R + per_block - 1) / per_block)), dim3(GNT), 0,
-                               st, a, Dcur);
+            switch (DM) {  // factored path: dm in {8, ..., 128} (fact_mode)
+                case 8: launch_scatter0<8>(a, Dcur, R, st); break;
+                case 16: launch_scatter0<16>(a, Dcur, R, st); break;
+                case 32: launch_scatter0<32>(a, Dcur, R, st); break;
+                case 64: launch_scatter0<64>(a, Dcur, R, st); break;
+                case 128: launch_scatter0<128>(a, Dcur, R, st); break;
+                default: return NCF_E_UNSUPPORTED;
+            }
             break;
         }
         // weight gradient: split the rows so the launch has ~512 blocks

@@ -532,6 +532,74 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_part_kernel(const uint64_t*
     }
 }
 
+// User order (ncf_user_order): one workgroup per rank slice of a batch, counting
+// sort by user in LDS (histogram, exclusive scan, placement by LDS atomics).  The
+// slice's rows are read twice (the second pass from L2); the entries are written
+// inside the slice's own 8-byte-per-row window.
+constexpr int UO_THREADS = 1024;
+constexpr int UO_MAX_USERS = 32767;
+__device__ __forceinline__ int uo_bin(uint64_t rw, int user_num) {
+    const int u = (int)(uint32_t)rw;
+    return (u < 0 || u >= user_num) ? user_num : u;  // padding rows (-1) last
+}
+__global__ __launch_bounds__(UO_THREADS) void user_order_kernel(const uint64_t* __restrict__ rows, int64_t n,
+                                                                int64_t B, int world, int user_num,
+                                                                int64_t* __restrict__ order) {
+    extern __shared__ int uh[];  // [user_num + 1]
+    __shared__ int wsum[UO_THREADS / 64];
+    const int tid = threadIdx.x;
+    const int64_t b = blockIdx.x / world;
+    const int r = (int)(blockIdx.x - b * world);
+    const int64_t b0 = b * B;
+    if (b0 >= n) return;  // block-uniform
+    const int64_t cnt = (n - b0) < B ? (n - b0) : B;
+    const int64_t per = (cnt + world - 1) / world;
+    const int64_t lo = (int64_t)r * per;
+    if (lo >= cnt) return;
+    const int len = (int)((cnt - lo) < per ? (cnt - lo) : per);
+    const uint64_t* rb = rows + b0 + lo;
+    int64_t* ob = order + b0 + lo;
+    const int nbin = user_num + 1;
+    for (int i = tid; i < nbin; i += UO_THREADS) uh[i] = 0;
+    __syncthreads();
+    for (int k = tid; k < len; k += UO_THREADS) atomicAdd(&uh[uo_bin(rb[k], user_num)], 1);
+    __syncthreads();
+    const int chunk = (nbin + UO_THREADS - 1) / UO_THREADS;
+    const int i0 = min(nbin, tid * chunk), i1 = min(nbin, i0 + chunk);
+    int tot = 0;
+    for (int i = i0; i < i1; ++i) tot += uh[i];
+    const int lane = tid & 63, wv = tid >> 6;
+    int incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int q = 0; q < UO_THREADS / 64; ++q) {
+            const int v = wsum[q];
+            wsum[q] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    int s = wsum[wv] + incl - tot;
+    for (int i = i0; i < i1; ++i) {
+        const int c = uh[i];
+        uh[i] = s;
+        s += c;
+    }
+    __syncthreads();
+    for (int k = tid; k < len; k += UO_THREADS) {
+        const uint64_t rw = rb[k];
+        const int bin = uo_bin(rw, user_num);
+        ob[atomicAdd(&uh[bin], 1)] = (int64_t)(((uint64_t)(uint32_t)(bin < user_num ? bin : -1) << 32) | (uint32_t)k);
+    }
+}
+
 static int prep_parts(int64_t B) {
     if (B <= PART_ROWS) return 1;
     const int64_t need = (B + PART_ROWS - 1) / PART_ROWS;
@@ -1118,7 +1186,8 @@ int64_t ncf_forward_workspace_bytes(const ncf_layout* lay, int64_t n) {
 }
 
 static int train_step_impl(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
-                           const float* dlogit, ncf_step_ctl* ctl, int64_t batch_global, int world, int rank,
+                           const int64_t* user_order, const float* dlogit, ncf_step_ctl* ctl, int64_t batch_global,
+                           int world, int rank,
                            int dz_mode, float kd_wt, float kd_wr, float kd_temp, void* workspace,
                            int64_t workspace_bytes,
                            float* logits_out, void* stream) {
@@ -1137,6 +1206,7 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
         la.params = params;
         la.grads = grads;
         la.rows = rows;
+        la.uorder = ncf_uses_user_order(lay) ? user_order : nullptr;
         la.dlogit = dlogit;
         la.ctl = ctl;
         la.batch_global = batch_global;
@@ -1187,19 +1257,22 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
 }
 
 int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
-                   const float* dlogit, ncf_step_ctl* ctl, int64_t batch_global, int world, int rank,
+                   const int64_t* user_order, const float* dlogit, ncf_step_ctl* ctl, int64_t batch_global,
+                   int world, int rank,
                    int dz_mode, void* workspace, int64_t workspace_bytes, float* logits_out, void* stream) {
     if (dz_mode == NCF_DZ_KD) return NCF_E_ARG;  // ncf_train_step_kd carries the weights
-    return train_step_impl(lay, params, grads, rows, dlogit, ctl, batch_global, world, rank, dz_mode, 0.f, 0.f, 0.f,
+    return train_step_impl(lay, params, grads, rows, user_order, dlogit, ctl, batch_global, world, rank, dz_mode, 0.f,
+                           0.f, 0.f,
                            workspace, workspace_bytes, logits_out, stream);
 }
 
 int ncf_train_step_kd(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
-                      const float* teacher_logits, ncf_step_ctl* ctl, int64_t batch_global, int world, int rank,
+                      const int64_t* user_order, const float* teacher_logits, ncf_step_ctl* ctl,
+                      int64_t batch_global, int world, int rank,
                       float w_task, float w_resp, float temperature, void* workspace, int64_t workspace_bytes,
                       float* logits_out, void* stream) {
     if (!teacher_logits) return NCF_E_ARG;
-    return train_step_impl(lay, params, grads, rows, teacher_logits, ctl, batch_global, world, rank, NCF_DZ_KD,
+    return train_step_impl(lay, params, grads, rows, user_order, teacher_logits, ctl, batch_global, world, rank, NCF_DZ_KD,
                            w_task, w_resp, temperature, workspace, workspace_bytes, logits_out, stream);
 }
 
@@ -1443,6 +1516,25 @@ int ncf_prepare_epoch(const uint64_t* rows, const int64_t* perm, int64_t n, int6
     hipLaunchKernelGGL(sort_part_kernel, dim3((unsigned)g3), dim3(SORT_THREADS), (size_t)SORT_LDS, st, shuf, hist,
                        parts, n, batch_global, item_num, P, nb, rows_out);
     return launch_status();
+}
+
+int ncf_user_order(const uint64_t* rows, int64_t n, int64_t batch_global, int world, int user_num, int64_t* order,
+                   void* stream) {
+    if (!rows || !order || n < 0 || batch_global <= 0 || world < 1 || user_num <= 0) return NCF_E_ARG;
+    if (user_num > UO_MAX_USERS) return NCF_E_UNSUPPORTED;
+    if (n == 0) return NCF_OK;
+    const int64_t nb = (n + batch_global - 1) / batch_global;
+    if (nb * world > 0x7fffffff) return NCF_E_ARG;
+    const int64_t lds = (int64_t)(user_num + 1) * 4;
+    if (ensure_lds(reinterpret_cast<const void*>(&user_order_kernel), lds) != NCF_OK) return NCF_E_LAUNCH;
+    hipLaunchKernelGGL(user_order_kernel, dim3((unsigned)(nb * world)), dim3(UO_THREADS), (size_t)lds,
+                       (hipStream_t)stream, rows, n, batch_global, world, user_num, order);
+    return launch_status();
+}
+
+int ncf_uses_user_order(const ncf_layout* lay) {
+    if (!lay) return 0;
+    return (fact_mode(lay) && !train_fused(lay) && lay->user_num <= UO_MAX_USERS) ? 1 : 0;
 }
 
 int ncf_hr_ndcg(const float* logits, const int32_t* items, int64_t n, int batch, int top_k, int32_t* hr, float* ndcg,

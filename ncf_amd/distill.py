@@ -360,7 +360,7 @@ class DeviceDistillPlan:
     def launch(self, eng, st):
         lib = L.hip()
         L.check(lib.ncf_train_step_kd(ctypes.byref(eng.lay), eng.flat.data_ptr(), eng.grads.data_ptr(),
-                                      eng.rows.data_ptr(), self.tlog.data_ptr(), eng.ctl.data_ptr(),
+                                      eng.rows.data_ptr(), eng.user_order_ptr(), self.tlog.data_ptr(), eng.ctl.data_ptr(),
                                       eng.batch_size, eng.world_size, eng.rank, self.w_task, self.w_resp,
                                       self.temperature, eng.ws.data_ptr(), eng.ws.numel() * 4, None, st),
                 "ncf_train_step_kd")  # (factored layer 0 expanded inside, before the feature terms)

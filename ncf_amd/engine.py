@@ -148,6 +148,9 @@ class TrainEngine:
         # the current one): captured together with it, so a buffer switch at an
         # epoch boundary replays graphs already built
         self.stream_buffers = []
+        # ncf_user_order output per epoch-stream buffer (key: pointer, rows)
+        self._orders = {}
+        self._uses_order = False
 
     # ------------------------------------------------------------------ data
     def set_epoch_stream(self, rows, batch_size, checked=False):
@@ -183,11 +186,31 @@ class TrainEngine:
             self._ctl_n = n
         else:
             self.ctl[0:1].zero_()
+        # layered factored layer 0: the rows of each rank slice by user, once per epoch
+        # (the step then sums user runs before its atomics, ncf_user_order)
+        self._uses_order = (os.environ.get("NCF_USER_ORDER", "1") == "1"
+                            and bool(L.hip().ncf_uses_user_order(ctypes.byref(self.lay))))
+        if self._uses_order:
+            L.check(L.hip().ncf_user_order(rows.data_ptr(), n, self.batch_size, self.world_size,
+                                           self.model.user_num, self._order_buf(rows).data_ptr(),
+                                           L.stream_ptr(self.device)), "ncf_user_order")
         self._hb = 0  # host copy of the batch index (the sparse exchange needs the batch's rows)
         if self.distill is not None:
             # the frozen teacher's logit for every row of the epoch stream (one
             # forward launch per epoch instead of one no_grad forward per step)
             self.distill.teacher_logits(rows)
+
+    def _order_buf(self, rows):
+        """The user-order buffer that goes with epoch-stream buffer `rows`."""
+        key = (rows.data_ptr(), rows.numel())
+        buf = self._orders.get(key)
+        if buf is None:
+            buf = self._orders[key] = torch.empty(rows.numel(), dtype=torch.int64, device=self.device)
+        return buf
+
+    def user_order_ptr(self):
+        """ncf_train_step's user_order argument for the current stream (None: unused)."""
+        return self._order_buf(self.rows).data_ptr() if self._uses_order else None
 
     @property
     def num_batches(self):
@@ -281,7 +304,8 @@ class TrainEngine:
             self.distill.launch(self, st)
             return
         L.check(L.hip().ncf_train_step(ctypes.byref(self.lay), self.flat.data_ptr(), self.grads.data_ptr(),
-                                       self.rows.data_ptr(), None, self.ctl.data_ptr(), self.batch_size,
+                                       self.rows.data_ptr(), self.user_order_ptr(), None, self.ctl.data_ptr(),
+                                       self.batch_size,
                                        self.world_size, self.rank, L.DZ_BCE, self.ws.data_ptr(),
                                        self.ws.numel() * 4, None, st), "ncf_train_step")
 
@@ -348,7 +372,7 @@ class TrainEngine:
 
         def launch():
             L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.rows.data_ptr(),
-                                       None, self.ctl.data_ptr(), self.batch_size, self.world_size, self.rank,
+                                       self.user_order_ptr(), None, self.ctl.data_ptr(), self.batch_size, self.world_size, self.rank,
                                        L.DZ_BCE, self.ws.data_ptr(), self.ws.numel() * 4, None, sp), "ncf_train_step")
         launch()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -418,6 +442,8 @@ class TrainEngine:
                         or key in self._graphs):
                     continue
                 self.rows = buf
+                if self._uses_order:
+                    self._order_buf(buf)  # allocated outside the capture (filled when the buffer is set)
                 self.capture()
         finally:
             self.rows, self._graph, self._graph_k = cur

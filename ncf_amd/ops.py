@@ -218,7 +218,7 @@ def fused_backward(flat, lay, rows, dlogit, gflat, ws, ctl):
     n = rows.numel()
     dev = flat.device
     st = L.stream_ptr(dev)
-    L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
+    L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(), None,
                                    dlogit.data_ptr(), ctl.data_ptr(), int(n), 1, 0, L.DZ_DLOGIT,
                                    ws.data_ptr(), ws.numel() * 4, None, st), "ncf_train_step")
     L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), ws.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st),
@@ -276,7 +276,7 @@ def _dropout_logits(model, rows, drop):
     ws = new_workspace(lay, n, dev)
     ctl = new_ctl(n, dev, adam_t=t)
     dl = torch.zeros(n, dtype=torch.float32, device=dev)
-    L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), scratch.data_ptr(), rows.data_ptr(),
+    L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), scratch.data_ptr(), rows.data_ptr(), None,
                                    dl.data_ptr(), ctl.data_ptr(), int(n), 1, 0, L.DZ_DLOGIT,
                                    ws.data_ptr(), ws.numel() * 4, logits.data_ptr(), L.stream_ptr(dev)),
             "ncf_train_step")

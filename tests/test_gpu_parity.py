@@ -135,9 +135,10 @@ def _fact_mode(lay):
     return ops.fact_mode(lay)
 
 
-def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3, flags=0):
+def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3, flags=0, order=False):
     """Logits, loss and every gradient of one fused step vs the oracle.  flags: OR-ed
-    into a copy of the layout (e.g. NCF_LAYOUT_PER_ROW_L0)."""
+    into a copy of the layout (e.g. NCF_LAYOUT_PER_ROW_L0); order: pass the batch's
+    ncf_user_order to the step."""
     import ncf_amd._lib as L
     from ncf_amd import ops
     ref, m = _models(mt, f, Lyr, U=U, I=I, seed=seed)
@@ -159,9 +160,13 @@ def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3, flags=0):
     logits = torch.empty(B, device=DEV)
     st = L.stream_ptr()
     rows = ops.pack_rows(u, it, y)
+    uord = None
+    if order:
+        uord = torch.empty(B, dtype=torch.int64, device=DEV)
+        L.check(L.hip().ncf_user_order(rows.data_ptr(), B, B, 1, U, uord.data_ptr(), st), "order")
     L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
-                                   None, ctl.data_ptr(), B, 1, 0, L.DZ_BCE,
-                                   ws.data_ptr(), ws.numel() * 4, logits.data_ptr(), st), "train")
+                                   None if uord is None else uord.data_ptr(), None, ctl.data_ptr(), B, 1, 0,
+                                   L.DZ_BCE, ws.data_ptr(), ws.numel() * 4, logits.data_ptr(), st), "train")
     L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), ws.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st), "reduce")
     torch.cuda.synchronize()
     np.testing.assert_allclose(logits.cpu().numpy(), logits_ref.numpy(), rtol=1e-5, atol=1e-7)
@@ -216,12 +221,15 @@ def test_one_step_fact_boundary(U, I, fact):
 def test_one_step_layered_factored_layer0(mt, f, Lyr, B):
     """Layered path with the factored layer 0 (ABI 10: table projections through W0,
     per-row gather, D0 row sums expanded by fact_expand_kernel; dm = 128 for
-    NCF(32,3) and NCF(16,4)) at ml-1m ids, and the same shape forced per-row
-    (NCF_LAYOUT_PER_ROW_L0): both vs the oracle."""
+    NCF(32,3) and NCF(16,4)) at ml-1m ids, with and without the user order (ABI 12:
+    user runs summed before the atomics), and the same shape forced per-row
+    (NCF_LAYOUT_PER_ROW_L0): all vs the oracle."""
     import ncf_amd._lib as L
     assert L.supported(mt, f, Lyr) == L.PATH_LAYERED
     lay = _one_step(mt, f, Lyr, B, 6041, 3707, seed=19)
     assert _fact_mode(lay)
+    assert L.hip().ncf_uses_user_order(L.ctypes.byref(lay)) == 1
+    _one_step(mt, f, Lyr, B, 6041, 3707, seed=19, order=True)
     lay = _one_step(mt, f, Lyr, min(B, 8192), 6041, 3707, seed=19, flags=L.LAYOUT_PER_ROW_L0)
     assert not _fact_mode(lay)
 
@@ -385,8 +393,11 @@ def test_rank_shards_sum_to_full_batch(world, f, Lyr):
         gflat = torch.zeros(int(lay.total), device=DEV)
         ws = ops.new_workspace(lay, (B + world - 1) // world, DEV)
         ctl = ops.new_ctl(B, DEV)
+        # the rank slices' user order (used where ncf_uses_user_order: NCF(32,3))
+        uord = torch.empty(B, dtype=torch.int64, device=DEV)
+        L.check(L.hip().ncf_user_order(rows.data_ptr(), B, B, world, U, uord.data_ptr(), st), "order")
         L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
-                                       None, ctl.data_ptr(), B, world, rank, L.DZ_BCE,
+                                       uord.data_ptr(), None, ctl.data_ptr(), B, world, rank, L.DZ_BCE,
                                        ws.data_ptr(), ws.numel() * 4, None, st), "train")
         L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), ws.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st), "reduce")
         return gflat
@@ -493,6 +504,40 @@ def test_prepare_epoch_batches_grouped_by_item(n, bs, n_items, hot):
     for b0 in range(0, n, bs):
         sl = slice(b0, min(n, b0 + bs))
         assert np.array_equal(np.sort(exp2[sl]), np.sort(out2[sl]))
+
+
+@pytest.mark.parametrize("n,bs,world,users", [(65536 * 2 + 123, 65536, 1, 6040), (70001, 65536, 3, 6040),
+                                              (10007, 1000, 2, 1), (5000, 4096, 4, 32767), (99, 7, 5, 50)])
+def test_user_order_sorts_each_rank_slice(n, bs, world, users):
+    """ncf_user_order: in every rank slice of every batch (the partial last batch
+    split by its own ceil(cnt / world), as the step selects rows), the entries'
+    offsets are a permutation of the slice's by ascending user, padding rows (-1)
+    last, and each entry's user field is its row's user."""
+    import ncf_amd._lib as L
+    rng = np.random.default_rng(n + world)
+    rows = _rand_rows(rng, n, users, 3707, hot=0.2)
+    pad = torch.as_tensor(rng.random(n) < 0.01, device=DEV)
+    rows = torch.where(pad, rows | 0xFFFFFFFF, rows)  # user -1
+    order = torch.full((n,), -7, dtype=torch.int64, device=DEV)
+    L.check(L.hip().ncf_user_order(rows.data_ptr(), n, bs, world, users, order.data_ptr(), L.stream_ptr()),
+            "ncf_user_order")
+    torch.cuda.synchronize()
+    r, e = rows.cpu().numpy(), order.cpu().numpy()
+    o, ou = e & 0xFFFFFFFF, e >> 32  # entry: user << 32 | offset (user -1: padding)
+    slices = 0
+    for b0 in range(0, n, bs):
+        cnt = min(bs, n - b0)
+        per = -(-cnt // world)
+        for lo in range(0, cnt, per):
+            s0, ln = b0 + lo, min(per, cnt - lo)
+            oo = o[s0:s0 + ln]
+            assert np.array_equal(np.sort(oo), np.arange(ln)), "not a permutation of the slice"
+            u = (r[s0:s0 + ln][oo] & 0xFFFFFFFF).astype(np.int64)
+            assert np.array_equal(ou[s0:s0 + ln], np.where(u == 0xFFFFFFFF, -1, u)), "entry user field"
+            key = np.where(u == 0xFFFFFFFF, users, u)
+            assert (np.diff(key) >= 0).all(), "slice not sorted by user"
+            slices += 1
+    assert slices >= world
 
 
 LAYERED = [("NeuMF-end", 32, 3), ("MLP", 6, 2), ("GMF", 5, 1), ("NeuMF-pre", 64, 4)]
@@ -669,7 +714,7 @@ def test_one_step_dropout_vs_masked_oracle(mt, f, Lyr, p):
     logits = torch.empty(B, device=DEV)
     st = L.stream_ptr()
     L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(), None,
-                                   ctl.data_ptr(), B, 1, 0, L.DZ_BCE, ws.data_ptr(), ws.numel() * 4,
+                                   None, ctl.data_ptr(), B, 1, 0, L.DZ_BCE, ws.data_ptr(), ws.numel() * 4,
                                    logits.data_ptr(), st), "train")
     L.check(L.hip().ncf_reduce_slab(L.ctypes.byref(lay), ws.data_ptr(), gflat.data_ptr(), ctl.data_ptr(), st),
             "reduce")
