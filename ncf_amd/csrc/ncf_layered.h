@@ -46,6 +46,10 @@ int launch_zero_f32(float* p, int64_t n, hipStream_t st);
 // projections (factored layer 0, fact_part_floats >= 0)] + activations [+ dY buffers].
 int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train, int64_t fact_part_floats);
 
+// Factored layer 0: P = [Um W0[:, :DM]^T ; Im W0[:, DM:]^T] ((U + I) x DM floats at P),
+// the per-step table projection the layered step's layer-0 forward gathers from.
+int lyr_launch_proj(const ncf_layout* lay, const float* params, float* P, hipStream_t st);
+
 // Launch the layered forward (train = false) or forward + BCE + backward (train = true)
 // over at most R rows; ws = lyr_workspace_floats(lay, R, train) floats.
 int lyr_run(const LyrArgs& a, float* ws, int64_t R, bool train, hipStream_t st);

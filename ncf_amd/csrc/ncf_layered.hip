@@ -504,51 +504,52 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
 
 // ---------------------------------------------------------------------------
 // Factored layer 0.  Projection: P[r][n] = sum_c X[r][c] W0[n][koff + c] over the
-// user rows (blocks [0, nbu), X = Um, koff = 0) then the item rows (X = Im,
-// koff = DM); grid (nbu + nbi, ceil(DM / 64)).
-__global__ __launch_bounds__(GNT) void lyr_proj_kernel(LyrArgs a, float* __restrict__ P, int nbu) {
-    const ncf_layout& lay = a.lay;
-    const int DM = lay.factor_num << (lay.num_layers - 1);
-    const bool user = (int)blockIdx.x < nbu;
+// user rows (X = Um, koff = 0) then the item rows (X = Im, koff = DM).  One wave
+// per 16 table rows, no LDS: in the orientation C[i = n][j = row] a lane (c, g)
+// loads its own row's k-fragments X[row c][16t + 4g .. +3] and the W0 fragments
+// W0[16mt + c][koff + 16t + 4g .. +3] (W0 is 16-64 KB, L2-resident) as 16-byte
+// loads, and stores P[row c][16mt + 4g .. +3].  DM / 16 x DM / 16 x 4 MFMAs per
+// wave; one load round trip (the GEMM-core version with LDS K-steps took 6 us for
+// the 9,746 rows of ml-1m).
+template <int DM>
+__global__ __launch_bounds__(64) void lyr_proj_kernel(ncf_layout lay, const float* __restrict__ prm,
+                                                      float* __restrict__ P, int nwu) {
+    constexpr int KT = (DM + 15) / 16, MT = KT;
+    const int l = threadIdx.x, c = l & 15, g = l >> 4;
+    const bool user = (int)blockIdx.x < nwu;
     const int64_t nrows = user ? lay.user_num : lay.item_num;
-    const int64_t m0 = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * GBM;
-    const int n0 = blockIdx.y * GBN;
-    const float* X = a.params + (user ? lay.um : lay.im);
-    const float* W = a.params + lay.w[0] + (user ? 0 : DM);  // row stride 2 DM
-    float* Pout = P + (user ? 0 : (int64_t)lay.user_num * DM);
-    auto ga = [&](int r, int64_t c) -> float {
-        const int64_t m = m0 + r;
-        return (m < nrows && c < DM) ? X[m * DM + c] : 0.f;
-    };
-    auto gb = [&](int64_t c, int n) -> float {
-        const int nn = n0 + n;
-        return (nn < DM && c < DM) ? W[(int64_t)nn * 2 * DM + c] : 0.f;
-    };
-    auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
+    const int64_t row = (int64_t)(user ? blockIdx.x : blockIdx.x - nwu) * 16 + c;
+    const bool rok = row < nrows;
+    const float* X = prm + (user ? lay.um : lay.im) + (rok ? row : 0) * DM;
+    const float* W = prm + lay.w[0] + (user ? 0 : DM);  // row stride 2 DM
+    float* Pout = P + (user ? 0 : (int64_t)lay.user_num * DM) + (rok ? row : 0) * DM;
+    f4 xv[KT];
 #pragma unroll
-        for (int ti = 0; ti < 2; ++ti)
+    for (int t = 0; t < KT; ++t) {
+        const int k0 = 16 * t + 4 * g;
+        xv[t] = k0 < DM ? *reinterpret_cast<const f4*>(X + k0) : f4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
-            for (int tj = 0; tj < 2; ++tj) {
-                const int n = n0 + wn + 16 * tj + (l & 15);
-                if (n >= DM) continue;
+    for (int mt = 0; mt < MT; ++mt) {
+        const int n = 16 * mt + c;
+        f4 wv[KT];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t m = m0 + wm + 16 * ti + 4 * (l >> 4) + r;
-                    if (m < nrows) Pout[m * DM + n] = lane_get(acc[ti][tj], r);
-                }
-            }
-    };
-    auto ga4 = [&](int r, int64_t c) -> f4 {
-        const int64_t m = m0 + r;
-        return (m < nrows && c < DM) ? ld4(X + m * DM + c) : zero4();
-    };
-    auto gb4 = [&](int64_t c, int n) -> f4 {
-        const int nn = n0 + n;
-        return (nn < DM && c < DM) ? ld4(W + (int64_t)nn * 2 * DM + c) : zero4();
-    };
-    (void)ga;
-    (void)gb;
-    gemm_block_v<true, true>(0, DM, ga4, gb4, ep);  // factored path: dm in {8, ..., 128}
+        for (int t = 0; t < KT; ++t) {
+            const int k0 = 16 * t + 4 * g;
+            wv[t] = (n < DM && k0 < DM) ? *reinterpret_cast<const f4*>(W + (int64_t)n * 2 * DM + k0)
+                                        : f4{0.f, 0.f, 0.f, 0.f};
+        }
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+            acc = MFMA4(wv[t].x, xv[t].x, acc);
+            acc = MFMA4(wv[t].y, xv[t].y, acc);
+            acc = MFMA4(wv[t].z, xv[t].z, acc);
+            acc = MFMA4(wv[t].w, xv[t].w, acc);
+        }
+        const int j0 = 16 * mt + 4 * g;  // acc: row c, outputs j0 .. j0 + 3
+        if (rok && j0 < DM) *reinterpret_cast<f4*>(Pout + j0) = acc;
+    }
 }
 
 // H_1[m][n] = ReLU(P[u_m][n] + P[U + i_m][n] + b_0[n]), four outputs per thread
@@ -840,6 +841,21 @@ __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float
 }  // namespace
 
 // ---------------------------------------------------------------------------
+int lyr_launch_proj(const ncf_layout* lay, const float* params, float* P, hipStream_t st) {
+    const int DM = lay->factor_num << (lay->num_layers - 1);
+    const int nwu = (int)((lay->user_num + 15) / 16), nwi = (int)((lay->item_num + 15) / 16);
+    const dim3 grid((unsigned)(nwu + nwi));
+    switch (DM) {
+        case 8: hipLaunchKernelGGL(lyr_proj_kernel<8>, grid, dim3(64), 0, st, *lay, params, P, nwu); break;
+        case 16: hipLaunchKernelGGL(lyr_proj_kernel<16>, grid, dim3(64), 0, st, *lay, params, P, nwu); break;
+        case 32: hipLaunchKernelGGL(lyr_proj_kernel<32>, grid, dim3(64), 0, st, *lay, params, P, nwu); break;
+        case 64: hipLaunchKernelGGL(lyr_proj_kernel<64>, grid, dim3(64), 0, st, *lay, params, P, nwu); break;
+        case 128: hipLaunchKernelGGL(lyr_proj_kernel<128>, grid, dim3(64), 0, st, *lay, params, P, nwu); break;
+        default: return NCF_E_UNSUPPORTED;
+    }
+    return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
+}
+
 int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train, int64_t fact_part_floats) {
     int64_t fl = rup64((int64_t)lyr_slab_rows(lay) * (lay->tower_len + 64));
     if (lay->model_type == NCF_MODEL_GMF) return fl;
@@ -892,9 +908,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             const int N = (2 * DM) >> (k + 1);
             const dim3 grid(mt, (unsigned)((N + GBN - 1) / GBN));
             if (k == 0 && fact) {
-                const int nbu = (int)((lay.user_num + GBM - 1) / GBM), nbi = (int)((lay.item_num + GBM - 1) / GBM);
-                hipLaunchKernelGGL(lyr_proj_kernel, dim3((unsigned)(nbu + nbi), (unsigned)((DM + GBN - 1) / GBN)),
-                                   dim3(GNT), 0, st, a, Pj, nbu);
+                if (lyr_launch_proj(&lay, a.params, Pj, st) != NCF_OK) return NCF_E_LAUNCH;
                 int64_t g0 = (R * (DM / 4) + GNT - 1) / GNT;
                 if (g0 > 8192) g0 = 8192;
                 hipLaunchKernelGGL(lyr_fwd0_fact_kernel, dim3((unsigned)g0), dim3(GNT), 0, st, a, Pj, H[1], R);
