@@ -37,6 +37,8 @@ struct LyrArgs {
     float* logits_out;       // optional per-row logits
     int64_t fact_part_floats;  // train: >= 0 factored layer 0 (that many floats of dW0 partials
                                // follow the slab row, filled by fact_expand_kernel); -1 per-row
+    float* zero_p;             // train: the slab, zeroed by the step's first kernel (zero_n4 16-byte units)
+    int64_t zero_n4;
 };
 
 // p[0 .. n) = 0 (n % 4 == 0, p 16-byte aligned) on stream st.
@@ -47,8 +49,10 @@ int launch_zero_f32(float* p, int64_t n, hipStream_t st);
 int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train, int64_t fact_part_floats);
 
 // Factored layer 0: P = [Um W0[:, :DM]^T ; Im W0[:, DM:]^T] ((U + I) x DM floats at P),
-// the per-step table projection the layered step's layer-0 forward gathers from.
-int lyr_launch_proj(const ncf_layout* lay, const float* params, float* P, hipStream_t st);
+// the per-step table projection the layered step's layer-0 forward gathers from; the
+// launch also zeroes zero[0 .. zero_floats) (the step's slab; 16-byte aligned, % 4 == 0).
+int lyr_launch_proj(const ncf_layout* lay, const float* params, float* P, float* zero, int64_t zero_floats,
+                    hipStream_t st);
 
 // Launch the layered forward (train = false) or forward + BCE + backward (train = true)
 // over at most R rows; ws = lyr_workspace_floats(lay, R, train) floats.

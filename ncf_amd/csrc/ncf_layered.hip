@@ -83,6 +83,14 @@ __device__ __forceinline__ float drop_mul(const Drop& d, int k, int64_t row, int
     return dropout_hash(d.seed, d.t, (uint32_t)k, row, (uint32_t)c) >= d.thr ? d.scale : 0.f;
 }
 
+// This thread's grid-stride share of zeroing n4 16-byte units at p (the step's slab,
+// cleared by its first kernel instead of a launch of its own).
+__device__ __forceinline__ void zero_share(float* p, int64_t n4) {
+    const int64_t nt = (int64_t)gridDim.x * gridDim.y * blockDim.x;
+    const int64_t id = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+    for (int64_t i = id; i < n4; i += nt) reinterpret_cast<f4*>(p)[i] = f4{0.f, 0.f, 0.f, 0.f};
+}
+
 __device__ __forceinline__ void row_ids(const LyrArgs& a, const Sel& s, int64_t m, int& u, int& it) {
     if (m < s.nloc) {
         const uint64_t r = a.rows[s.base + m];
@@ -102,11 +110,19 @@ __device__ __forceinline__ int map_mn(int t, int p) { return KC ? (t >> 4) + 16 
 template <bool KC>
 __device__ __forceinline__ int map_k(int t, int p) { return KC ? (t & 15) : (t >> 6) + 4 * p; }
 
+// Store-time hook on the A operand (sa(value) once per loaded element, when it is
+// written to LDS -- the load has landed by then, so no extra wait): the weight
+// gradient sums dY's columns through it for db_k.
+struct NoHook {
+    template <class T>
+    __device__ __forceinline__ void operator()(const T&) const {}
+};
+
 // C[mb..mb+32) x [nb..nb+32) for this wave: acc[ti][tj] reg r at
 // row 16*ti + 4*(l>>4) + r, col 16*tj + (l&15).
-template <bool AKC, bool BKC, class GA, class GB, class EP>
+template <bool AKC, bool BKC, class GA, class GB, class EP, class SA = NoHook>
 __device__ __forceinline__ void gemm_block(int64_t m0, int64_t n0, int64_t kbeg, int64_t kend, GA ga, GB gb,
-                                           EP ep) {
+                                           EP ep, SA sa = SA{}) {
     __shared__ float As[2][GBK][GBM + GPAD];
     __shared__ float Bs[2][GBK][GBN + GPAD];
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
@@ -119,6 +135,8 @@ __device__ __forceinline__ void gemm_block(int64_t m0, int64_t n0, int64_t kbeg,
         for (int p = 0; p < 4; ++p) rb[p] = gb(k0 + map_k<BKC>(t, p), map_mn<BKC>(t, p));
     };
     auto store = [&](int buf) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) sa(ra[p]);
 #pragma unroll
         for (int p = 0; p < 4; ++p) As[buf][map_k<AKC>(t, p)][map_mn<AKC>(t, p)] = ra[p];
 #pragma unroll
@@ -160,8 +178,8 @@ __device__ __forceinline__ void gemm_block(int64_t m0, int64_t n0, int64_t kbeg,
 // else M/N), which must be a multiple of 4 with 16-byte aligned rows (factor_num
 // % 4 == 0).  KC tile [64][16]: thread t loads row t / 4, k 4 (t % 4) .. + 3;
 // otherwise [16][64]: k t / 16, columns 4 (t % 16) .. + 3 (one LDS f4 store).
-template <bool AKC, bool BKC, class GA, class GB, class EP>
-__device__ __forceinline__ void gemm_block_v(int64_t kbeg, int64_t kend, GA ga4, GB gb4, EP ep) {
+template <bool AKC, bool BKC, class GA, class GB, class EP, class SA = NoHook>
+__device__ __forceinline__ void gemm_block_v(int64_t kbeg, int64_t kend, GA ga4, GB gb4, EP ep, SA sa = SA{}) {
     __shared__ __attribute__((aligned(16))) float As[2][GBK][GBM + GPAD];
     __shared__ __attribute__((aligned(16))) float Bs[2][GBK][GBN + GPAD];
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
@@ -174,6 +192,7 @@ __device__ __forceinline__ void gemm_block_v(int64_t kbeg, int64_t kend, GA ga4,
         rb = gb4(k0 + b_k, b_mn);
     };
     auto store = [&](int buf) {
+        sa(ra);
         if constexpr (AKC) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) As[buf][a_k + i][a_mn] = lane_get(ra, i);
@@ -235,6 +254,7 @@ __global__ __launch_bounds__(GNT) void lyr_fwd_kernel(LyrArgs a, int k, const fl
     const float* prm = a.params;
     const float* W = prm + lay.w[k];
     const float* bias = prm + lay.b[k];
+    if (FIRST && a.zero_p != nullptr) zero_share(a.zero_p, a.zero_n4);  // the step's first kernel
     if (FIRST && threadIdx.x < GBM) {
         int u, it;
         row_ids(a, s, m0 + threadIdx.x, u, it);
@@ -399,22 +419,35 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
     float* slab = a.slab + (int64_t)(blockIdx.z % lyr_slab_rows(&lay)) * (lay.tower_len + 64);
     const int64_t tb = lay.tower_begin;
     const Drop dr = DROP ? drop_of(a) : Drop{false, 0, 0, 0, 1.f};
+    // db_k = column sums of dY_k: summed by the blocks of column tile 0 from the dY
+    // values they stage anyway (store-time hook of the GEMM core), instead of a ones
+    // column appended to A, which costs a whole extra 64-wide tile when K % 64 == 0
+    const bool dbt = blockIdx.y == 0;  // block-uniform
+    f4 db4 = zero4();
+    float db1 = 0.f;
+    auto sa4 = [&](const f4& v) {
+        if (dbt) {
+            db4.x += v.x;
+            db4.y += v.y;
+            db4.z += v.z;
+            db4.w += v.w;
+        }
+    };
+    auto sa1 = [&](const float& v) {
+        if (dbt) db1 += v;
+    };
     auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
             for (int tj = 0; tj < 2; ++tj) {
                 const int c = c0 + wn + 16 * tj + (l & 15);
-                if (c > K) continue;
+                if (c >= K) continue;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int j = j0 + wm + 16 * ti + 4 * (l >> 4) + r;
                     if (j >= J) continue;
-                    const float v = lane_get(acc[ti][tj], r);
-                    if (c < K)
-                        atomicAdd(slab + (lay.w[k] - tb) + (int64_t)j * K + c, v);
-                    else
-                        atomicAdd(slab + (lay.b[k] - tb) + j, v);
+                    atomicAdd(slab + (lay.w[k] - tb) + (int64_t)j * K + c, lane_get(acc[ti][tj], r));
                 }
             }
     };
@@ -436,8 +469,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
             __syncthreads();
             auto gb = [&](int64_t m, int cr) -> float {
                 const int c = c0 + cr;
-                if (m >= q1 || c > K) return 0.f;
-                if (c == K) return 1.f;
+                if (m >= q1 || c >= K) return 0.f;
                 const int e = (int)(m - q0);
                 float v = c < DM ? prm[lay.um + (int64_t)su[e] * DM + c] : prm[lay.im + (int64_t)si[e] * DM + (c - DM)];
                 if constexpr (DROP) v *= drop_mul(dr, k, s.base + m, c);
@@ -454,8 +486,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
                 };
                 auto gb4 = [&](int64_t m, int cr) -> f4 {
                     const int c = c0 + cr;
-                    if (m >= q1 || c > K) return zero4();
-                    if (c == K) return f4{1.f, 0.f, 0.f, 0.f};  // the ones column of db
+                    if (m >= q1 || c >= K) return zero4();
                     const int e = (int)(m - q0);
                     f4 v = c < DM ? ld4(prm + lay.um + (int64_t)su[e] * DM + c)
                                   : ld4(prm + lay.im + (int64_t)si[e] * DM + (c - DM));
@@ -465,16 +496,15 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
                     }
                     return v;
                 };
-                gemm_block_v<false, false>(q0, q1, ga4, gb4, ep);
+                gemm_block_v<false, false>(q0, q1, ga4, gb4, ep, sa4);
             } else {
-                gemm_block<false, false>(j0, c0, q0, q1, ga2, gb, ep);
+                gemm_block<false, false>(j0, c0, q0, q1, ga2, gb, ep, sa1);
             }
         }
     } else {
         auto gb = [&](int64_t m, int cr) -> float {
             const int c = c0 + cr;
-            if (m >= r1 || c > K) return 0.f;
-            if (c == K) return 1.f;
+            if (m >= r1 || c >= K) return 0.f;
             float v = Ain[m * K + c];
             if constexpr (DROP) v *= drop_mul(dr, k, s.base + m, c);
             return v;
@@ -486,8 +516,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
             };
             auto gb4 = [&](int64_t m, int cr) -> f4 {
                 const int c = c0 + cr;
-                if (m >= r1 || c > K) return zero4();
-                if (c == K) return f4{1.f, 0.f, 0.f, 0.f};  // the ones column of db
+                if (m >= r1 || c >= K) return zero4();
                 f4 v = ld4(Ain + m * K + c);
                 if constexpr (DROP) {
 #pragma unroll
@@ -495,61 +524,75 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
                 }
                 return v;
             };
-            gemm_block_v<false, false>(r0, r1, ga4, gb4, ep);
+            gemm_block_v<false, false>(r0, r1, ga4, gb4, ep, sa4);
         } else {
-            gemm_block<false, false>(j0, c0, r0, r1, ga, gb, ep);
+            gemm_block<false, false>(j0, c0, r0, r1, ga, gb, ep, sa1);
+        }
+    }
+    if (dbt) {  // db_k: per-thread column sums -> LDS -> one atomic per column per block
+        // A operand [16 rows of m][64 j]: VEC thread t holds j 4 (t % 16) .. + 3 of
+        // rows t / 16 (16 slots); scalar thread t holds j t % 64 of rows t / 64 (4 slots)
+        __shared__ float dred[16][GBM];
+        const int t = threadIdx.x;
+        if constexpr (VEC) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dred[t >> 4][4 * (t & 15) + i] = lane_get(db4, i);
+        } else {
+            dred[t >> 6][t & 63] = db1;
+        }
+        __syncthreads();
+        if (t < GBM) {
+            float sum = 0.f;
+#pragma unroll
+            for (int q = 0; q < (VEC ? 16 : 4); ++q) sum += dred[q][t];
+            const int j = j0 + t;
+            if (j < J && sum != 0.f) atomicAdd(slab + (lay.b[k] - tb) + j, sum);
         }
     }
 }
 
 // ---------------------------------------------------------------------------
 // Factored layer 0.  Projection: P[r][n] = sum_c X[r][c] W0[n][koff + c] over the
-// user rows (X = Um, koff = 0) then the item rows (X = Im, koff = DM).  One wave
-// per 16 table rows, no LDS: in the orientation C[i = n][j = row] a lane (c, g)
-// loads its own row's k-fragments X[row c][16t + 4g .. +3] and the W0 fragments
-// W0[16mt + c][koff + 16t + 4g .. +3] (W0 is 16-64 KB, L2-resident) as 16-byte
-// loads, and stores P[row c][16mt + 4g .. +3].  DM / 16 x DM / 16 x 4 MFMAs per
-// wave; one load round trip (the GEMM-core version with LDS K-steps took 6 us for
-// the 9,746 rows of ml-1m).
-template <int DM>
-__global__ __launch_bounds__(64) void lyr_proj_kernel(ncf_layout lay, const float* __restrict__ prm,
-                                                      float* __restrict__ P, int nwu) {
-    constexpr int KT = (DM + 15) / 16, MT = KT;
-    const int l = threadIdx.x, c = l & 15, g = l >> 4;
-    const bool user = (int)blockIdx.x < nwu;
+// user rows (blocks [0, nbu), X = Um, koff = 0) then the item rows (X = Im,
+// koff = DM); grid (nbu + nbi, ceil(DM / 64)).  The GEMM core shares each W0 tile
+// through LDS over 64 rows (an LDS-free wave-per-16-rows variant re-read the 64 KB
+// W0 half per wave at dm 128: 15.5 against 9.4 us).  It is the step's first kernel
+// and also clears the slab (zp, zn4).
+__global__ __launch_bounds__(GNT) void lyr_proj_kernel(ncf_layout lay, const float* __restrict__ prm,
+                                                       float* __restrict__ P, int nbu, float* __restrict__ zp,
+                                                       int64_t zn4) {
+    if (zp != nullptr) zero_share(zp, zn4);
+    const int DM = lay.factor_num << (lay.num_layers - 1);
+    const bool user = (int)blockIdx.x < nbu;
     const int64_t nrows = user ? lay.user_num : lay.item_num;
-    const int64_t row = (int64_t)(user ? blockIdx.x : blockIdx.x - nwu) * 16 + c;
-    const bool rok = row < nrows;
-    const float* X = prm + (user ? lay.um : lay.im) + (rok ? row : 0) * DM;
+    const int64_t m0 = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * GBM;
+    const int n0 = blockIdx.y * GBN;
+    const float* X = prm + (user ? lay.um : lay.im);
     const float* W = prm + lay.w[0] + (user ? 0 : DM);  // row stride 2 DM
-    float* Pout = P + (user ? 0 : (int64_t)lay.user_num * DM) + (rok ? row : 0) * DM;
-    f4 xv[KT];
+    float* Pout = P + (user ? 0 : (int64_t)lay.user_num * DM);
+    auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
 #pragma unroll
-    for (int t = 0; t < KT; ++t) {
-        const int k0 = 16 * t + 4 * g;
-        xv[t] = k0 < DM ? *reinterpret_cast<const f4*>(X + k0) : f4{0.f, 0.f, 0.f, 0.f};
-    }
+        for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int n = 16 * mt + c;
-        f4 wv[KT];
+            for (int tj = 0; tj < 2; ++tj) {
+                const int n = n0 + wn + 16 * tj + (l & 15);
+                if (n >= DM) continue;
 #pragma unroll
-        for (int t = 0; t < KT; ++t) {
-            const int k0 = 16 * t + 4 * g;
-            wv[t] = (n < DM && k0 < DM) ? *reinterpret_cast<const f4*>(W + (int64_t)n * 2 * DM + k0)
-                                        : f4{0.f, 0.f, 0.f, 0.f};
-        }
-        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < KT; ++t) {
-            acc = MFMA4(wv[t].x, xv[t].x, acc);
-            acc = MFMA4(wv[t].y, xv[t].y, acc);
-            acc = MFMA4(wv[t].z, xv[t].z, acc);
-            acc = MFMA4(wv[t].w, xv[t].w, acc);
-        }
-        const int j0 = 16 * mt + 4 * g;  // acc: row c, outputs j0 .. j0 + 3
-        if (rok && j0 < DM) *reinterpret_cast<f4*>(Pout + j0) = acc;
-    }
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t m = m0 + wm + 16 * ti + 4 * (l >> 4) + r;
+                    if (m < nrows) Pout[m * DM + n] = lane_get(acc[ti][tj], r);
+                }
+            }
+    };
+    auto ga4 = [&](int r, int64_t c) -> f4 {
+        const int64_t m = m0 + r;
+        return (m < nrows && c < DM) ? ld4(X + m * DM + c) : zero4();
+    };
+    auto gb4 = [&](int64_t c, int n) -> f4 {
+        const int nn = n0 + n;
+        return (nn < DM && c < DM) ? ld4(W + (int64_t)nn * 2 * DM + c) : zero4();
+    };
+    gemm_block_v<true, true>(0, DM, ga4, gb4, ep);  // factored path: dm in {8, ..., 128}
 }
 
 // H_1[m][n] = ReLU(P[u_m][n] + P[U + i_m][n] + b_0[n]), four outputs per thread
@@ -841,18 +884,12 @@ __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float
 }  // namespace
 
 // ---------------------------------------------------------------------------
-int lyr_launch_proj(const ncf_layout* lay, const float* params, float* P, hipStream_t st) {
+int lyr_launch_proj(const ncf_layout* lay, const float* params, float* P, float* zero, int64_t zero_floats,
+                    hipStream_t st) {
     const int DM = lay->factor_num << (lay->num_layers - 1);
-    const int nwu = (int)((lay->user_num + 15) / 16), nwi = (int)((lay->item_num + 15) / 16);
-    const dim3 grid((unsigned)(nwu + nwi));
-    switch (DM) {
-        case 8: hipLaunchKernelGGL(lyr_proj_kernel<8>, grid, dim3(64), 0, st, *lay, params, P, nwu); break;
-        case 16: hipLaunchKernelGGL(lyr_proj_kernel<16>, grid, dim3(64), 0, st, *lay, params, P, nwu); break;
-        case 32: hipLaunchKernelGGL(lyr_proj_kernel<32>, grid, dim3(64), 0, st, *lay, params, P, nwu); break;
-        case 64: hipLaunchKernelGGL(lyr_proj_kernel<64>, grid, dim3(64), 0, st, *lay, params, P, nwu); break;
-        case 128: hipLaunchKernelGGL(lyr_proj_kernel<128>, grid, dim3(64), 0, st, *lay, params, P, nwu); break;
-        default: return NCF_E_UNSUPPORTED;
-    }
+    const int nbu = (int)((lay->user_num + GBM - 1) / GBM), nbi = (int)((lay->item_num + GBM - 1) / GBM);
+    hipLaunchKernelGGL(lyr_proj_kernel, dim3((unsigned)(nbu + nbi), (unsigned)((DM + GBN - 1) / GBN)), dim3(GNT), 0,
+                       st, *lay, params, P, nbu, zero, zero_floats / 4);
     return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
 }
 
@@ -901,14 +938,21 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             Db = ws + off;
         }
     }
-    if (train && launch_zero_f32(slab, slab_floats, st) != NCF_OK) return NCF_E_LAUNCH;
+    // the slab is cleared by the step's first kernel (the projection or the first
+    // forward layer) -- every slab add comes later in the stream; GMF-only: a launch
+    if (train && mlp) {
+        a.zero_p = slab;
+        a.zero_n4 = slab_floats / 4;
+    } else if (train && launch_zero_f32(slab, slab_floats, st) != NCF_OK) {
+        return NCF_E_LAUNCH;
+    }
     const unsigned mt = (unsigned)((R + GBM - 1) / GBM);
     if (mlp) {
         for (int k = 0; k < L; ++k) {
             const int N = (2 * DM) >> (k + 1);
             const dim3 grid(mt, (unsigned)((N + GBN - 1) / GBN));
             if (k == 0 && fact) {
-                if (lyr_launch_proj(&lay, a.params, Pj, st) != NCF_OK) return NCF_E_LAUNCH;
+                if (lyr_launch_proj(&lay, a.params, Pj, a.zero_p, 4 * a.zero_n4, st) != NCF_OK) return NCF_E_LAUNCH;
                 int64_t g0 = (R * (DM / 4) + GNT - 1) / GNT;
                 if (g0 > 8192) g0 = 8192;
                 hipLaunchKernelGGL(lyr_fwd0_fact_kernel, dim3((unsigned)g0), dim3(GNT), 0, st, a, Pj, H[1], R);
@@ -966,7 +1010,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             break;
         }
         // weight gradient: split the rows so the launch has ~512 blocks
-        const int64_t tiles = (int64_t)((J + GBM - 1) / GBM) * ((K + 1 + GBN - 1) / GBN);
+        const int64_t tiles = (int64_t)((J + GBM - 1) / GBM) * ((K + GBN - 1) / GBN);
         int64_t splits = 1024 / tiles;
         const int64_t max_splits = (R + 255) / 256;
         if (splits > max_splits) splits = max_splits;
@@ -974,7 +1018,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
         int64_t chunk = (R + splits - 1) / splits;
         chunk = (chunk + GBK - 1) / GBK * GBK;
         splits = (R + chunk - 1) / chunk;
-        const dim3 gw((unsigned)((J + GBM - 1) / GBM), (unsigned)((K + 1 + GBN - 1) / GBN), (unsigned)splits);
+        const dim3 gw((unsigned)((J + GBM - 1) / GBM), (unsigned)((K + GBN - 1) / GBN), (unsigned)splits);
         if (k == 0)
             {
                 if (drop) hipLaunchKernelGGL((lyr_bwd_w_kernel<true, true, false>), gw, dim3(GNT), 0, st, a, k, Dcur, nullptr, R, chunk);

@@ -852,10 +852,13 @@ constexpr int FX_WAVES = 16;  // 16 waves: dW0 / dX output tiles dealt round-rob
 // Chunk rows per LDS pass: 64 up to DM = 64, 32 at DM = 128 (W0 half + 3 chunk
 // images = 118 KB).  A block walks `cpb` consecutive chunks of one table with the
 // W0 half staged once and its dW0 partial held in registers across them.
+#ifndef NCF_FX_CPB128
+#define NCF_FX_CPB128 2
+#endif
 template <int DM>
 struct FxShape {
     static constexpr int CH = DM <= 64 ? 64 : 32;
-    static constexpr int CPB = DM <= 64 ? 1 : 4;  // chunks per block
+    static constexpr int CPB = DM <= 64 ? 1 : NCF_FX_CPB128;  // chunks per block
     static constexpr int ST = DM + 4, NT = (DM + 15) / 16, Q4 = DM / 4;
     static constexpr int TPW = (NT * NT + FX_WAVES - 1) / FX_WAVES;  // dW0 tiles per wave
     static constexpr int64_t LDS = ((int64_t)DM * ST + 3LL * CH * ST) * 4;
@@ -1034,7 +1037,7 @@ static int slab_lo(const ncf_layout* lay) {
 }
 
 static int fact_ch(const ncf_layout* lay) { return fact_dm(lay) <= 64 ? 64 : 32; }  // FxShape<DM>::CH
-static int fact_cpb(const ncf_layout* lay) { return fact_dm(lay) <= 64 ? 1 : 4; }   // FxShape<DM>::CPB
+static int fact_cpb(const ncf_layout* lay) { return fact_dm(lay) <= 64 ? 1 : NCF_FX_CPB128; }  // FxShape<DM>::CPB
 
 static int fact_blocks(const ncf_layout* lay, int* nbu) {
     const int64_t per = (int64_t)fact_ch(lay) * fact_cpb(lay);
