@@ -536,7 +536,7 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_part_kernel(const uint64_t*
 // sort by user in LDS (histogram, exclusive scan, placement by LDS atomics).  The
 // slice's rows are read twice (the second pass from L2); the entries are written
 // inside the slice's own 8-byte-per-row window.
-constexpr int UO_THREADS = 1024;
+constexpr int UO_THREADS = 1024, UO_UNROLL = 16;
 constexpr int UO_MAX_USERS = 32767;
 __device__ __forceinline__ int uo_bin(uint64_t rw, int user_num) {
     const int u = (int)(uint32_t)rw;
@@ -562,7 +562,19 @@ __global__ __launch_bounds__(UO_THREADS) void user_order_kernel(const uint64_t* 
     const int nbin = user_num + 1;
     for (int i = tid; i < nbin; i += UO_THREADS) uh[i] = 0;
     __syncthreads();
-    for (int k = tid; k < len; k += UO_THREADS) atomicAdd(&uh[uo_bin(rb[k], user_num)], 1);
+    // rows in batches of UO_UNROLL per thread, loads issued together ahead of the LDS
+    // atomics (one dependent load -> atomic per row was latency-bound: 160 us/epoch)
+    for (int k0 = 0; k0 < len; k0 += UO_THREADS * UO_UNROLL) {
+        int bins[UO_UNROLL];
+#pragma unroll
+        for (int q = 0; q < UO_UNROLL; ++q) {
+            const int k = k0 + q * UO_THREADS + tid;
+            bins[q] = k < len ? uo_bin(rb[k], user_num) : -1;
+        }
+#pragma unroll
+        for (int q = 0; q < UO_UNROLL; ++q)
+            if (bins[q] >= 0) atomicAdd(&uh[bins[q]], 1);
+    }
     __syncthreads();
     const int chunk = (nbin + UO_THREADS - 1) / UO_THREADS;
     const int i0 = min(nbin, tid * chunk), i1 = min(nbin, i0 + chunk);
@@ -593,10 +605,20 @@ __global__ __launch_bounds__(UO_THREADS) void user_order_kernel(const uint64_t* 
         s += c;
     }
     __syncthreads();
-    for (int k = tid; k < len; k += UO_THREADS) {
-        const uint64_t rw = rb[k];
-        const int bin = uo_bin(rw, user_num);
-        ob[atomicAdd(&uh[bin], 1)] = (int64_t)(((uint64_t)(uint32_t)(bin < user_num ? bin : -1) << 32) | (uint32_t)k);
+    for (int k0 = 0; k0 < len; k0 += UO_THREADS * UO_UNROLL) {
+        int bins[UO_UNROLL];
+#pragma unroll
+        for (int q = 0; q < UO_UNROLL; ++q) {
+            const int k = k0 + q * UO_THREADS + tid;
+            bins[q] = k < len ? uo_bin(rb[k], user_num) : -1;
+        }
+#pragma unroll
+        for (int q = 0; q < UO_UNROLL; ++q) {
+            const int k = k0 + q * UO_THREADS + tid;
+            if (bins[q] >= 0)
+                ob[atomicAdd(&uh[bins[q]], 1)] =
+                    (int64_t)(((uint64_t)(uint32_t)(bins[q] < user_num ? bins[q] : -1) << 32) | (uint32_t)k);
+        }
     }
 }
 

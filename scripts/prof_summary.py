@@ -16,7 +16,9 @@ from collections import defaultdict
 
 
 def short(name):
-    n = name.split("(")[0]
+    # kernels in an anonymous namespace print as "ncf::(anonymous namespace)::k<...>(args)":
+    # drop that qualifier before cutting the argument list
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     return n.replace("void ", "").strip()
 
 
