@@ -624,6 +624,169 @@ __global__ __launch_bounds__(GNT) void lyr_fwd0_fact_kernel(LyrArgs a, const flo
     }
 }
 
+// Factored forward chain (training, every tower width a multiple of 4): for 64-row
+// tiles (4 waves x 16 rows) one launch forms H_1 = ReLU(P[u] + P[U + i] + b_0) from
+// the projections and runs tower layers 1 .. L-1 with their weights in LDS, in the
+// fused kernel's register orientation (lane (c, g): row c, features 16t + 4g .. +3;
+// a layer's output is directly the next layer's MFMA B operand).  Each H_k is still
+// written for the backward, but none is read back, and the launches of
+// lyr_fwd0_fact_kernel and the L - 1 lyr_fwd_kernel GEMMs are one.
+template <int DM, int L>
+struct ChainShape {
+    __host__ __device__ static constexpr int S(int k) { return (2 * DM) >> k; }  // S(1) = DM
+    __host__ __device__ static constexpr int T16(int n) { return (n + 15) / 16; }
+    __host__ __device__ static constexpr int SW(int k) { return 16 * T16(S(k)) + 4; }   // LDS row stride of W_k
+    __host__ __device__ static constexpr int WR(int k) { return 16 * T16(S(k + 1)); }   // W_k rows, padded
+    __host__ __device__ static constexpr int woff(int k) { return k <= 1 ? 0 : woff(k - 1) + WR(k - 1) * SW(k - 1); }
+    __host__ __device__ static constexpr int boff(int k) { return k == 0 ? 0 : boff(k - 1) + 16 * T16(S(k)); }
+    static constexpr int W_TOTAL = woff(L);  // layers 1 .. L-1
+    static constexpr int B_TOTAL = boff(L);  // b_0 .. b_{L-1}, each padded to 16
+    static constexpr int KT1 = T16(DM), MT1 = T16(DM / 2);
+};
+struct ChainOut {
+    float* H[5];  // H[1 .. L]
+};
+#ifndef NCF_CHAIN_NT
+#define NCF_CHAIN_NT 256
+#endif
+constexpr int CNT = NCF_CHAIN_NT, CROWS = CNT / 4;  // threads per block, rows per tile (16 per wave)
+template <int DM, int L>
+__global__ __launch_bounds__(CNT, 2) void lyr_fwd_chain_kernel(LyrArgs a, const float* __restrict__ P, ChainOut o,
+                                                            int64_t R) {
+    using C_ = ChainShape<DM, L>;
+    __shared__ __attribute__((aligned(16))) float sW[C_::W_TOTAL > 0 ? C_::W_TOTAL : 4];
+    __shared__ __attribute__((aligned(16))) float sB[C_::B_TOTAL];
+    const Sel s = select_rows(a);
+    const ncf_layout& lay = a.lay;
+    const float* prm = a.params;
+    const int t = threadIdx.x, l = t & 63, w = t >> 6, c = l & 15, g = l >> 4;
+    // weights: every thread's 16-byte loads issued together, then the LDS stores (a
+    // load -> store per element serialises on the load latency)
+#pragma unroll
+    for (int k = 1; k < L; ++k) {
+        constexpr int PERMAX = (C_::WR(1) * (C_::SW(1) / 4) + CNT - 1) / CNT;
+        const int sw4 = C_::SW(k) / 4, in4 = C_::S(k) / 4, out = C_::S(k + 1), n4 = C_::WR(k) * sw4;
+        const f4* Wg = reinterpret_cast<const f4*>(prm + lay.w[k]);  // [out][in], in % 4 == 0
+        f4* Ws = reinterpret_cast<f4*>(sW + C_::woff(k));
+        f4 v[PERMAX];
+#pragma unroll
+        for (int q = 0; q < PERMAX; ++q) {
+            const int e = t + q * CNT, r = e / sw4, i4 = e - r * sw4;
+            v[q] = (e < n4 && r < out && i4 < in4) ? Wg[(int64_t)r * in4 + i4] : zero4();
+        }
+#pragma unroll
+        for (int q = 0; q < PERMAX; ++q) {
+            const int e = t + q * CNT;
+            if (e < n4) Ws[e] = v[q];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+        const int out = C_::S(k + 1);
+        for (int e = t; e < 16 * C_::T16(out); e += CNT) sB[C_::boff(k) + e] = e < out ? prm[lay.b[k] + e] : 0.f;
+    }
+    __syncthreads();
+    const int64_t ntile = (R + CROWS - 1) / CROWS;
+    // the next tile's packed row is requested while this tile computes
+    auto fetch = [&](int64_t tile) -> uint64_t {
+        const int64_t m = tile * CROWS + 16 * w + c;
+        return (tile < ntile && m < s.nloc) ? a.rows[s.base + m] : ~0ull;  // ~0: padding (user -1)
+    };
+    uint64_t nrow = fetch(blockIdx.x);
+    for (int64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+        const int64_t m = tile * CROWS + 16 * w + c;  // this lane's row
+        const uint64_t rw = nrow;
+        nrow = fetch(tile + gridDim.x);
+        // row_ids: padding rows (and rows past the shard) gather id 0, as lyr_fwd0_fact_kernel
+        int u = (int)(uint32_t)rw, it = (int)((rw >> 32) & 0x7fffffffu);
+        if (u < 0) u = it = 0;
+        const float* pu = P + (int64_t)u * DM;
+        const float* pi = P + ((int64_t)lay.user_num + it) * DM;
+        f4 x[C_::KT1];
+#pragma unroll
+        for (int q = 0; q < C_::KT1; ++q) {
+            const int j0 = 16 * q + 4 * g;
+            x[q] = zero4();
+            if (j0 < DM) {
+                const f4 vu = ld4(pu + j0), vi = ld4(pi + j0), bb = ld4(sB + j0);
+                x[q].x = fmaxf(vu.x + vi.x + bb.x, 0.f);
+                x[q].y = fmaxf(vu.y + vi.y + bb.y, 0.f);
+                x[q].z = fmaxf(vu.z + vi.z + bb.z, 0.f);
+                x[q].w = fmaxf(vu.w + vi.w + bb.w, 0.f);
+                if (m < R) *reinterpret_cast<f4*>(o.H[1] + m * DM + j0) = x[q];
+            }
+        }
+#pragma unroll
+        for (int k = 1; k < L; ++k) {
+            const int KT = C_::T16(C_::S(k)), MT = C_::T16(C_::S(k + 1)), out = C_::S(k + 1), sw = C_::SW(k);
+            const float* Ws = sW + C_::woff(k);
+            f4 acc[C_::MT1 > 0 ? C_::MT1 : 1];
+#pragma unroll
+            for (int mt = 0; mt < C_::MT1; ++mt)
+                if (mt < MT) acc[mt] = ld4(sB + C_::boff(k) + 16 * mt + 4 * g);
+            // one output tile at a time: its KT weight fragments, then its MFMAs (the
+            // barrier keeps the compiler from hoisting every tile's LDS reads, which
+            // took ~300 VGPRs and left one wave per SIMD)
+#pragma unroll
+            for (int mt = 0; mt < C_::MT1; ++mt) {
+                if (mt >= MT) continue;
+                f4 wv[C_::KT1];
+#pragma unroll
+                for (int q = 0; q < C_::KT1; ++q)
+                    if (q < KT) wv[q] = ld4(Ws + (16 * mt + c) * sw + 16 * q + 4 * g);
+#pragma unroll
+                for (int q = 0; q < C_::KT1; ++q) {
+                    if (q >= KT) continue;
+                    acc[mt] = MFMA4(wv[q].x, x[q].x, acc[mt]);
+                    acc[mt] = MFMA4(wv[q].y, x[q].y, acc[mt]);
+                    acc[mt] = MFMA4(wv[q].z, x[q].z, acc[mt]);
+                    acc[mt] = MFMA4(wv[q].w, x[q].w, acc[mt]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int mt = 0; mt < C_::MT1; ++mt) {
+                if (mt >= MT) continue;
+                f4 h;
+                h.x = fmaxf(acc[mt].x, 0.f);
+                h.y = fmaxf(acc[mt].y, 0.f);
+                h.z = fmaxf(acc[mt].z, 0.f);
+                h.w = fmaxf(acc[mt].w, 0.f);
+                const int j0 = 16 * mt + 4 * g;
+                if (m < R && j0 < out) *reinterpret_cast<f4*>(o.H[k + 1] + m * out + j0) = h;
+                x[mt] = h;  // padded outputs are 0: zero weight rows and bias
+            }
+        }
+    }
+}
+
+// Launch the chain for (DM, L) with factor_num = DM >> (L - 1) a multiple of 4; false
+// if there is no instantiation (the caller runs lyr_fwd0_fact_kernel + lyr_fwd_kernel).
+#ifndef NCF_CHAIN_GRID
+#define NCF_CHAIN_GRID 512
+#endif
+static bool launch_fwd_chain(const LyrArgs& a, const float* P, float* const* H, int64_t R, hipStream_t st) {
+    const ncf_layout& lay = a.lay;
+    const int L = lay.num_layers, DM = lay.factor_num << (L - 1);
+    ChainOut o;
+    for (int k = 0; k < 5; ++k) o.H[k] = (k >= 1 && k <= L) ? H[k] : nullptr;
+    int64_t grid = (R + CROWS - 1) / CROWS;
+    if (grid > NCF_CHAIN_GRID) grid = NCF_CHAIN_GRID;  // weights staged once per block
+    if (grid < 1) grid = 1;
+#define NCF_CHAIN(D, LL)                                                                                    \
+    if (DM == D && L == LL) {                                                                               \
+        hipLaunchKernelGGL((lyr_fwd_chain_kernel<D, LL>), dim3((unsigned)grid), dim3(CNT), 0, st, a, P, o, R); \
+        return true;                                                                                        \
+    }
+    NCF_CHAIN(8, 1) NCF_CHAIN(8, 2)
+    NCF_CHAIN(16, 1) NCF_CHAIN(16, 2) NCF_CHAIN(16, 3)
+    NCF_CHAIN(32, 1) NCF_CHAIN(32, 2) NCF_CHAIN(32, 3) NCF_CHAIN(32, 4)
+    NCF_CHAIN(64, 1) NCF_CHAIN(64, 2) NCF_CHAIN(64, 3) NCF_CHAIN(64, 4)
+    NCF_CHAIN(128, 1) NCF_CHAIN(128, 2) NCF_CHAIN(128, 3) NCF_CHAIN(128, 4)
+#undef NCF_CHAIN
+    return false;
+}
+
 // dY_0 rows -> grads[um][u] and grads[im][i] (width DM), db_0 -> slab.  A walker of
 // DM lanes (one feature each; 256 / DM walkers per block, a walker may span two
 // waves: nothing crosses lanes) takes SC_ROWS consecutive rows: its rows' values are
@@ -953,6 +1116,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             const dim3 grid(mt, (unsigned)((N + GBN - 1) / GBN));
             if (k == 0 && fact) {
                 if (lyr_launch_proj(&lay, a.params, Pj, a.zero_p, 4 * a.zero_n4, st) != NCF_OK) return NCF_E_LAUNCH;
+                if (vec && !drop && launch_fwd_chain(a, Pj, H, R, st)) break;  // layers 1 .. L-1 ran in it too
                 int64_t g0 = (R * (DM / 4) + GNT - 1) / GNT;
                 if (g0 > 8192) g0 = 8192;
                 hipLaunchKernelGGL(lyr_fwd0_fact_kernel, dim3((unsigned)g0), dim3(GNT), 0, st, a, Pj, H[1], R);
