@@ -624,44 +624,62 @@ __global__ __launch_bounds__(GNT) void lyr_fwd0_fact_kernel(LyrArgs a, const flo
     }
 }
 
-// Factored forward chain (training, every tower width a multiple of 4): for 64-row
-// tiles (4 waves x 16 rows) one launch forms H_1 = ReLU(P[u] + P[U + i] + b_0) from
-// the projections and runs tower layers 1 .. L-1 with their weights in LDS, in the
-// fused kernel's register orientation (lane (c, g): row c, features 16t + 4g .. +3;
-// a layer's output is directly the next layer's MFMA B operand).  Each H_k is still
-// written for the backward, but none is read back, and the launches of
-// lyr_fwd0_fact_kernel and the L - 1 lyr_fwd_kernel GEMMs are one.
+// Factored step chain (training, every tower width a multiple of 4): a tile's rows
+// are independent through the whole forward and data-gradient chain, so one launch
+// does, for 64-row tiles (4 waves x 16 rows), everything but the weight gradients:
+//   H_1 = ReLU(P[u] + P[U + i] + b_0), H_{k+1} = ReLU(W_k H_k + b_k)   (k = 1 .. L-1)
+//   logit, BCE / KD / given dL/dlogit, the GMF backward (user rows per row, item runs
+//   summed first: batches are grouped by item), dwp / dbp / loss
+//   D_{L-1} = dz wp_mlp [H_L > 0],  D_{k-1} = (D_k W_k) [H_k > 0]   (k = L-1 .. 1)
+// with the tower weights in LDS and activations in the fused kernel's register
+// orientation (lane (c, g): row c, features 16t + 4g .. +3; a layer's output is the
+// next MFMA's B operand, the forward values stay in registers as the dgrad masks).
+// H_k and D_k are written for lyr_bwd_w_kernel / lyr_scatter0_kernel, none is read
+// back.  Replaces lyr_fwd0_fact_kernel, L - 1 lyr_fwd_kernel, lyr_predict_kernel and
+// L - 1 lyr_bwd_data_kernel launches.
 template <int DM, int L>
 struct ChainShape {
-    __host__ __device__ static constexpr int S(int k) { return (2 * DM) >> k; }  // S(1) = DM
+    __host__ __device__ static constexpr int S(int k) { return (2 * DM) >> k; }  // S(1) = DM, S(L) = F
     __host__ __device__ static constexpr int T16(int n) { return (n + 15) / 16; }
     __host__ __device__ static constexpr int SW(int k) { return 16 * T16(S(k)) + 4; }   // LDS row stride of W_k
     __host__ __device__ static constexpr int WR(int k) { return 16 * T16(S(k + 1)); }   // W_k rows, padded
     __host__ __device__ static constexpr int woff(int k) { return k <= 1 ? 0 : woff(k - 1) + WR(k - 1) * SW(k - 1); }
     __host__ __device__ static constexpr int boff(int k) { return k == 0 ? 0 : boff(k - 1) + 16 * T16(S(k)); }
+    static constexpr int F = DM >> (L - 1);
     static constexpr int W_TOTAL = woff(L);  // layers 1 .. L-1
     static constexpr int B_TOTAL = boff(L);  // b_0 .. b_{L-1}, each padded to 16
-    static constexpr int KT1 = T16(DM), MT1 = T16(DM / 2);
+    static constexpr int KT1 = T16(DM), MT1 = T16(DM / 2), TF = T16(F);
 };
-struct ChainOut {
+struct ChainBufs {
     float* H[5];  // H[1 .. L]
+    float* D[4];  // D[0 .. L-1]: dL/d pre-activation of layer k, row stride S(k + 1)
 };
 #ifndef NCF_CHAIN_NT
 #define NCF_CHAIN_NT 256
 #endif
 constexpr int CNT = NCF_CHAIN_NT, CROWS = CNT / 4;  // threads per block, rows per tile (16 per wave)
 template <int DM, int L>
-__global__ __launch_bounds__(CNT, 2) void lyr_fwd_chain_kernel(LyrArgs a, const float* __restrict__ P, ChainOut o,
-                                                            int64_t R) {
+__global__ __launch_bounds__(CNT, 2) void lyr_step_chain_kernel(LyrArgs a, const float* __restrict__ P, ChainBufs o,
+                                                                int64_t R) {
     using C_ = ChainShape<DM, L>;
+    constexpr int F = C_::F, TF = C_::TF, NW = CNT / 64;
     __shared__ __attribute__((aligned(16))) float sW[C_::W_TOTAL > 0 ? C_::W_TOTAL : 4];
     __shared__ __attribute__((aligned(16))) float sB[C_::B_TOTAL];
+    __shared__ __attribute__((aligned(16))) float sWP[2][16 * TF];  // wp: [0] GMF part, [1] tower part (zero-padded)
+    __shared__ float sIg[NW][16][16 * TF + 1];                    // per wave: GMF item-gradient rows
+    __shared__ int sIt[NW][16];                                    // per wave: item id per row (-1: none)
+    __shared__ float sred[2 * 16 * TF + 2];                        // block sums: dwp GMF | dwp tower | dbp | loss
     const Sel s = select_rows(a);
     const ncf_layout& lay = a.lay;
     const float* prm = a.params;
+    const bool gmf = lay.model_type != NCF_MODEL_MLP;
+    const int Pg = gmf ? F : 0;
     const int t = threadIdx.x, l = t & 63, w = t >> 6, c = l & 15, g = l >> 4;
-    // weights: every thread's 16-byte loads issued together, then the LDS stores (a
-    // load -> store per element serialises on the load latency)
+    if (blockIdx.x == 0 && t == 0) {  // step snapshot for ncf_reduce_adam_step
+        a.ctl->snap_batch = a.ctl->batch;
+        a.ctl->snap_t = a.ctl->adam_t + 1;
+    }
+    // weights: every thread's 16-byte loads issued together, then the LDS stores
 #pragma unroll
     for (int k = 1; k < L; ++k) {
         constexpr int PERMAX = (C_::WR(1) * (C_::SW(1) / 4) + CNT - 1) / CNT;
@@ -685,10 +703,20 @@ __global__ __launch_bounds__(CNT, 2) void lyr_fwd_chain_kernel(LyrArgs a, const 
         const int out = C_::S(k + 1);
         for (int e = t; e < 16 * C_::T16(out); e += CNT) sB[C_::boff(k) + e] = e < out ? prm[lay.b[k] + e] : 0.f;
     }
+    for (int e = t; e < 16 * TF; e += CNT) {
+        sWP[0][e] = (gmf && e < F) ? prm[lay.wp + e] : 0.f;
+        sWP[1][e] = e < F ? prm[lay.wp + Pg + e] : 0.f;
+    }
+    for (int e = t; e < 2 * 16 * TF + 2; e += CNT) sred[e] = 0.f;
     __syncthreads();
+    const float bp = prm[lay.bp];
+    // per-lane partials over the block's rows: dwp (features 16q + 4g .. +3), dbp, loss
+    f4 aWg[TF], aWm[TF];
+#pragma unroll
+    for (int q = 0; q < TF; ++q) aWg[q] = aWm[q] = zero4();
+    float aB = 0.f, aL = 0.f;
     const int64_t ntile = (R + CROWS - 1) / CROWS;
-    // the next tile's packed row is requested while this tile computes
-    auto fetch = [&](int64_t tile) -> uint64_t {
+    auto fetch = [&](int64_t tile) -> uint64_t {  // the next tile's packed row, requested early
         const int64_t m = tile * CROWS + 16 * w + c;
         return (tile < ntile && m < s.nloc) ? a.rows[s.base + m] : ~0ull;  // ~0: padding (user -1)
     };
@@ -697,39 +725,45 @@ __global__ __launch_bounds__(CNT, 2) void lyr_fwd_chain_kernel(LyrArgs a, const 
         const int64_t m = tile * CROWS + 16 * w + c;  // this lane's row
         const uint64_t rw = nrow;
         nrow = fetch(tile + gridDim.x);
-        // row_ids: padding rows (and rows past the shard) gather id 0, as lyr_fwd0_fact_kernel
         int u = (int)(uint32_t)rw, it = (int)((rw >> 32) & 0x7fffffffu);
+        const bool valid = u >= 0 && m < R;  // padding rows gather id 0 and get dz = 0
         if (u < 0) u = it = 0;
-        const float* pu = P + (int64_t)u * DM;
-        const float* pi = P + ((int64_t)lay.user_num + it) * DM;
-        f4 x[C_::KT1];
+        // ---- forward
+        f4 h[L + 1][C_::KT1];  // h[k]: H_k, orientation A
+        {
+            const float* pu = P + (int64_t)u * DM;
+            const float* pi = P + ((int64_t)lay.user_num + it) * DM;
 #pragma unroll
-        for (int q = 0; q < C_::KT1; ++q) {
-            const int j0 = 16 * q + 4 * g;
-            x[q] = zero4();
-            if (j0 < DM) {
-                const f4 vu = ld4(pu + j0), vi = ld4(pi + j0), bb = ld4(sB + j0);
-                x[q].x = fmaxf(vu.x + vi.x + bb.x, 0.f);
-                x[q].y = fmaxf(vu.y + vi.y + bb.y, 0.f);
-                x[q].z = fmaxf(vu.z + vi.z + bb.z, 0.f);
-                x[q].w = fmaxf(vu.w + vi.w + bb.w, 0.f);
-                if (m < R) *reinterpret_cast<f4*>(o.H[1] + m * DM + j0) = x[q];
+            for (int q = 0; q < C_::KT1; ++q) {
+                const int j0 = 16 * q + 4 * g;
+                h[1][q] = zero4();
+                if (j0 < DM) {
+                    const f4 vu = ld4(pu + j0), vi = ld4(pi + j0), bb = ld4(sB + j0);
+                    h[1][q].x = fmaxf(vu.x + vi.x + bb.x, 0.f);
+                    h[1][q].y = fmaxf(vu.y + vi.y + bb.y, 0.f);
+                    h[1][q].z = fmaxf(vu.z + vi.z + bb.z, 0.f);
+                    h[1][q].w = fmaxf(vu.w + vi.w + bb.w, 0.f);
+                    if (m < R) *reinterpret_cast<f4*>(o.H[1] + m * DM + j0) = h[1][q];
+                }
+            }
+        }
+        f4 ug[TF], ig[TF];
+        if (gmf) {  // GMF rows, same orientation (requested before the tower MFMAs)
+#pragma unroll
+            for (int q = 0; q < TF; ++q) {
+                const int j0 = 16 * q + 4 * g;
+                ug[q] = j0 < F ? ld4(prm + lay.ug + (int64_t)u * F + j0) : zero4();
+                ig[q] = j0 < F ? ld4(prm + lay.ig + (int64_t)it * F + j0) : zero4();
             }
         }
 #pragma unroll
         for (int k = 1; k < L; ++k) {
             const int KT = C_::T16(C_::S(k)), MT = C_::T16(C_::S(k + 1)), out = C_::S(k + 1), sw = C_::SW(k);
             const float* Ws = sW + C_::woff(k);
-            f4 acc[C_::MT1 > 0 ? C_::MT1 : 1];
-#pragma unroll
-            for (int mt = 0; mt < C_::MT1; ++mt)
-                if (mt < MT) acc[mt] = ld4(sB + C_::boff(k) + 16 * mt + 4 * g);
-            // one output tile at a time: its KT weight fragments, then its MFMAs (the
-            // barrier keeps the compiler from hoisting every tile's LDS reads, which
-            // took ~300 VGPRs and left one wave per SIMD)
 #pragma unroll
             for (int mt = 0; mt < C_::MT1; ++mt) {
                 if (mt >= MT) continue;
+                f4 acc = ld4(sB + C_::boff(k) + 16 * mt + 4 * g);
                 f4 wv[C_::KT1];
 #pragma unroll
                 for (int q = 0; q < C_::KT1; ++q)
@@ -737,46 +771,214 @@ __global__ __launch_bounds__(CNT, 2) void lyr_fwd_chain_kernel(LyrArgs a, const 
 #pragma unroll
                 for (int q = 0; q < C_::KT1; ++q) {
                     if (q >= KT) continue;
-                    acc[mt] = MFMA4(wv[q].x, x[q].x, acc[mt]);
-                    acc[mt] = MFMA4(wv[q].y, x[q].y, acc[mt]);
-                    acc[mt] = MFMA4(wv[q].z, x[q].z, acc[mt]);
-                    acc[mt] = MFMA4(wv[q].w, x[q].w, acc[mt]);
+                    acc = MFMA4(wv[q].x, h[k][q].x, acc);
+                    acc = MFMA4(wv[q].y, h[k][q].y, acc);
+                    acc = MFMA4(wv[q].z, h[k][q].z, acc);
+                    acc = MFMA4(wv[q].w, h[k][q].w, acc);
+                }
+                f4 hh;
+                hh.x = fmaxf(acc.x, 0.f);
+                hh.y = fmaxf(acc.y, 0.f);
+                hh.z = fmaxf(acc.z, 0.f);
+                hh.w = fmaxf(acc.w, 0.f);
+                const int j0 = 16 * mt + 4 * g;
+                if (m < R && j0 < out) *reinterpret_cast<f4*>(o.H[k + 1] + m * out + j0) = hh;
+                h[k + 1][mt] = hh;  // padded outputs are 0: zero weight rows and bias
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // ---- predict, loss, dz
+        float zp = 0.f;
+#pragma unroll
+        for (int q = 0; q < TF; ++q) {
+            const f4 wm = ld4(&sWP[1][16 * q + 4 * g]);
+            zp += wm.x * h[L][q].x + wm.y * h[L][q].y + wm.z * h[L][q].z + wm.w * h[L][q].w;
+            if (gmf) {
+                const f4 wg = ld4(&sWP[0][16 * q + 4 * g]);
+                zp += wg.x * (ug[q].x * ig[q].x) + wg.y * (ug[q].y * ig[q].y) + wg.z * (ug[q].z * ig[q].z) +
+                      wg.w * (ug[q].w * ig[q].w);
+            }
+        }
+        zp += __shfl_xor(zp, 16, 64);
+        zp += __shfl_xor(zp, 32, 64);
+        const float z = zp + bp;
+        if (valid && g == 0 && a.logits_out != nullptr) a.logits_out[m] = z;
+        float dz = 0.f;
+        if (valid) {
+            if (a.dz_mode == NCF_DZ_BCE) {
+                const float y = (float)(uint32_t)(rw >> 63);
+                dz = (sigmoidf_(z) - y) / s.gb;
+                if (g == 0) aL += bce_loss(z, y) / s.gb;
+            } else if (a.dz_mode == NCF_DZ_KD) {
+                const float y = (float)(uint32_t)(rw >> 63);
+                float rl;
+                const float rg = kd_response(z, a.dlogit[s.base + m], a.kd_temp, &rl);
+                dz = (a.kd_wt * (sigmoidf_(z) - y) + a.kd_wr * rg) / s.gb;
+                if (g == 0) aL += (a.kd_wt * bce_loss(z, y) + a.kd_wr * rl) / s.gb;
+            } else {
+                dz = a.dlogit[s.base + m];
+            }
+        }
+        if (g == 0) aB += dz;
+        // ---- GMF backward: user rows per row, item rows staged for the run walk
+        if (gmf) {
+            if (g == 0) sIt[w][c] = valid ? it : -1;
+#pragma unroll
+            for (int q = 0; q < TF; ++q) {
+                const int j0 = 16 * q + 4 * g;
+                const f4 wg = ld4(&sWP[0][16 * q + 4 * g]);
+                aWg[q].x += dz * (ug[q].x * ig[q].x);
+                aWg[q].y += dz * (ug[q].y * ig[q].y);
+                aWg[q].z += dz * (ug[q].z * ig[q].z);
+                aWg[q].w += dz * (ug[q].w * ig[q].w);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float dg = dz * lane_get(wg, r);
+                    if (valid && j0 + r < F) atomicAdd(a.grads + lay.ug + (int64_t)u * F + j0 + r, dg * lane_get(ig[q], r));
+                    if (j0 + r < 16 * TF) sIg[w][c][j0 + r] = dg * lane_get(ug[q], r);
+                }
+            }
+        }
+        // ---- tower backward: D_{L-1} = dz wp [H_L > 0], then D_{k-1} = (D_k W_k) [H_k > 0]
+        f4 d[C_::KT1];
+#pragma unroll
+        for (int q = 0; q < TF; ++q) {
+            const f4 wm = ld4(&sWP[1][16 * q + 4 * g]);
+            aWm[q].x += dz * h[L][q].x;
+            aWm[q].y += dz * h[L][q].y;
+            aWm[q].z += dz * h[L][q].z;
+            aWm[q].w += dz * h[L][q].w;
+            d[q].x = h[L][q].x > 0.f ? dz * wm.x : 0.f;
+            d[q].y = h[L][q].y > 0.f ? dz * wm.y : 0.f;
+            d[q].z = h[L][q].z > 0.f ? dz * wm.z : 0.f;
+            d[q].w = h[L][q].w > 0.f ? dz * wm.w : 0.f;
+            const int j0 = 16 * q + 4 * g;
+            if (m < R && j0 < F) *reinterpret_cast<f4*>(o.D[L - 1] + m * F + j0) = d[q];
+        }
+#pragma unroll
+        for (int k = L - 1; k >= 1; --k) {
+            const int MT = C_::T16(C_::S(k + 1)), KT = C_::T16(C_::S(k)), in = C_::S(k), sw = C_::SW(k);
+            const float* Ws = sW + C_::woff(k);
+            f4 acc[C_::KT1];
+#pragma unroll
+            for (int m2 = 0; m2 < C_::KT1; ++m2) acc[m2] = zero4();
+#pragma unroll
+            for (int q = 0; q < C_::MT1; ++q) {
+                if (q >= MT) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float bv = lane_get(d[q], r);
+#pragma unroll
+                    for (int m2 = 0; m2 < C_::KT1; ++m2) {
+                        if (m2 >= KT) continue;
+                        acc[m2] = MFMA4(Ws[(16 * q + 4 * g + r) * sw + 16 * m2 + c], bv, acc[m2]);
+                    }
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
-            for (int mt = 0; mt < C_::MT1; ++mt) {
-                if (mt >= MT) continue;
-                f4 h;
-                h.x = fmaxf(acc[mt].x, 0.f);
-                h.y = fmaxf(acc[mt].y, 0.f);
-                h.z = fmaxf(acc[mt].z, 0.f);
-                h.w = fmaxf(acc[mt].w, 0.f);
-                const int j0 = 16 * mt + 4 * g;
-                if (m < R && j0 < out) *reinterpret_cast<f4*>(o.H[k + 1] + m * out + j0) = h;
-                x[mt] = h;  // padded outputs are 0: zero weight rows and bias
+            for (int m2 = 0; m2 < C_::KT1; ++m2) {
+                if (m2 >= KT) continue;
+                const f4 hv = h[k][m2];
+                f4 dd;
+                dd.x = hv.x > 0.f ? acc[m2].x : 0.f;
+                dd.y = hv.y > 0.f ? acc[m2].y : 0.f;
+                dd.z = hv.z > 0.f ? acc[m2].z : 0.f;
+                dd.w = hv.w > 0.f ? acc[m2].w : 0.f;
+                const int j0 = 16 * m2 + 4 * g;
+                if (m < R && j0 < in) *reinterpret_cast<f4*>(o.D[k - 1] + m * in + j0) = dd;
+                d[m2] = dd;
+            }
+        }
+        // ---- GMF item rows: runs of equal items summed (lane = feature) before the atomics
+        if (gmf) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // same-wave LDS hand-off
+            int ids[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) ids[r] = __builtin_amdgcn_readfirstlane(sIt[w][r]);
+            for (int f0 = 0; f0 < F; f0 += 64) {
+                const int f = f0 + l;
+                const int fc = f < F ? f : F - 1;
+                float v[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[r] = sIg[w][r][fc];
+                float run = 0.f;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    run += v[r];
+                    if (r == 15 || ids[r + 1] != ids[r]) {
+                        if (ids[r] >= 0 && f < F) atomicAdd(a.grads + lay.ig + (int64_t)ids[r] * F + f, run);
+                        run = 0.f;
+                    }
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next tile's writes
+        }
+    }
+    // ---- block tail: dwp (sum over the 16 rows of a lane group), dbp, loss -> LDS -> slab
+#pragma unroll
+    for (int q = 0; q < TF; ++q) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float vg = lane_get(aWg[q], r), vm = lane_get(aWm[q], r);
+#pragma unroll
+            for (int o2 = 1; o2 < 16; o2 <<= 1) {
+                vg += __shfl_xor(vg, o2, 64);
+                vm += __shfl_xor(vm, o2, 64);
+            }
+            const int f = 16 * q + 4 * g + r;
+            if (c == 0 && f < F) {
+                if (gmf) atomicAdd(&sred[f], vg);
+                atomicAdd(&sred[16 * TF + f], vm);
             }
         }
     }
+#pragma unroll
+    for (int o2 = 1; o2 < 64; o2 <<= 1) {
+        aB += __shfl_xor(aB, o2, 64);
+        aL += __shfl_xor(aL, o2, 64);
+    }
+    if (l == 0) {
+        atomicAdd(&sred[2 * 16 * TF], aB);
+        atomicAdd(&sred[2 * 16 * TF + 1], aL);
+    }
+    __syncthreads();
+    const int64_t tb = lay.tower_begin;
+    float* slab = a.slab + (int64_t)(blockIdx.x % lyr_slab_rows(&lay)) * (lay.tower_len + 64);
+    for (int e = t; e < 2 * F + 2; e += CNT) {
+        int src;
+        int64_t off;
+        if (e < F) {
+            if (!gmf) continue;
+            src = e;
+            off = (lay.wp - tb) + e;
+        } else if (e < 2 * F) {
+            src = 16 * TF + (e - F);
+            off = (lay.wp - tb) + Pg + (e - F);
+        } else {
+            src = 2 * 16 * TF + (e - 2 * F);
+            off = e == 2 * F ? (lay.bp - tb) : lay.tower_len;
+        }
+        const float v = sred[src];
+        if (v != 0.f) atomicAdd(slab + off, v);
+    }
 }
 
-// Launch the chain for (DM, L) with factor_num = DM >> (L - 1) a multiple of 4; false
-// if there is no instantiation (the caller runs lyr_fwd0_fact_kernel + lyr_fwd_kernel).
 #ifndef NCF_CHAIN_GRID
 #define NCF_CHAIN_GRID 512
 #endif
-static bool launch_fwd_chain(const LyrArgs& a, const float* P, float* const* H, int64_t R, hipStream_t st) {
+// Launch the step chain for (DM, L) with factor_num = DM >> (L - 1) a multiple of 4;
+// false if there is no instantiation (the caller runs the per-layer kernels).
+static bool launch_step_chain(const LyrArgs& a, const float* P, const ChainBufs& o, int64_t R, hipStream_t st) {
     const ncf_layout& lay = a.lay;
     const int L = lay.num_layers, DM = lay.factor_num << (L - 1);
-    ChainOut o;
-    for (int k = 0; k < 5; ++k) o.H[k] = (k >= 1 && k <= L) ? H[k] : nullptr;
     int64_t grid = (R + CROWS - 1) / CROWS;
-    if (grid > NCF_CHAIN_GRID) grid = NCF_CHAIN_GRID;  // weights staged once per block
+    if (grid > NCF_CHAIN_GRID) grid = NCF_CHAIN_GRID;  // weights staged once per block, several tiles each
     if (grid < 1) grid = 1;
-#define NCF_CHAIN(D, LL)                                                                                    \
-    if (DM == D && L == LL) {                                                                               \
-        hipLaunchKernelGGL((lyr_fwd_chain_kernel<D, LL>), dim3((unsigned)grid), dim3(CNT), 0, st, a, P, o, R); \
-        return true;                                                                                        \
+#define NCF_CHAIN(D, LL)                                                                                      \
+    if (DM == D && L == LL) {                                                                                 \
+        hipLaunchKernelGGL((lyr_step_chain_kernel<D, LL>), dim3((unsigned)grid), dim3(CNT), 0, st, a, P, o, R); \
+        return true;                                                                                          \
     }
     NCF_CHAIN(8, 1) NCF_CHAIN(8, 2)
     NCF_CHAIN(16, 1) NCF_CHAIN(16, 2) NCF_CHAIN(16, 3)
@@ -1110,13 +1312,28 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
         return NCF_E_LAUNCH;
     }
     const unsigned mt = (unsigned)((R + GBM - 1) / GBM);
+    // factored training with f % 4 == 0: the step chain (forward, predict, data
+    // gradients in one launch); D_0 in Da, D_1 .. D_{L-1} packed into Db
+    ChainBufs cb;
+    bool chained = false;
+    if (fact && vec && !drop) {
+        for (int k = 0; k < 5; ++k) cb.H[k] = (k >= 1 && k <= L) ? H[k] : nullptr;
+        float* q = Db;
+        for (int k = 0; k < 4; ++k) {
+            cb.D[k] = k == 0 ? Da : (k < L ? q : nullptr);
+            if (k >= 1 && k < L) q += R * (DM >> k);  // row stride S(k + 1) = DM >> k, a multiple of 4
+        }
+    }
     if (mlp) {
         for (int k = 0; k < L; ++k) {
             const int N = (2 * DM) >> (k + 1);
             const dim3 grid(mt, (unsigned)((N + GBN - 1) / GBN));
             if (k == 0 && fact) {
                 if (lyr_launch_proj(&lay, a.params, Pj, a.zero_p, 4 * a.zero_n4, st) != NCF_OK) return NCF_E_LAUNCH;
-                if (vec && !drop && launch_fwd_chain(a, Pj, H, R, st)) break;  // layers 1 .. L-1 ran in it too
+                if (vec && !drop && launch_step_chain(a, Pj, cb, R, st)) {
+                    chained = true;
+                    break;
+                }
                 int64_t g0 = (R * (DM / 4) + GNT - 1) / GNT;
                 if (g0 > 8192) g0 = 8192;
                 hipLaunchKernelGGL(lyr_fwd0_fact_kernel, dim3((unsigned)g0), dim3(GNT), 0, st, a, Pj, H[1], R);
@@ -1133,6 +1350,31 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
                 else hipLaunchKernelGGL((lyr_fwd_kernel<false, false, false>), grid, dim3(GNT), 0, st, a, k, H[k], H[k + 1], R);
             }
         }
+    }
+    if (chained) {  // weight gradients of layers L-1 .. 1, then the layer-0 scatter
+        for (int k = L - 1; k >= 1; --k) {
+            const int K = (2 * DM) >> k, J = K / 2;
+            const int64_t tiles = (int64_t)((J + GBM - 1) / GBM) * ((K + GBN - 1) / GBN);
+            int64_t splits = 1024 / tiles;
+            const int64_t max_splits = (R + 255) / 256;
+            if (splits > max_splits) splits = max_splits;
+            if (splits < 1) splits = 1;
+            int64_t chunk = (R + splits - 1) / splits;
+            chunk = (chunk + GBK - 1) / GBK * GBK;
+            splits = (R + chunk - 1) / chunk;
+            const dim3 gw((unsigned)((J + GBM - 1) / GBM), (unsigned)((K + GBN - 1) / GBN), (unsigned)splits);
+            hipLaunchKernelGGL((lyr_bwd_w_kernel<false, false, true>), gw, dim3(GNT), 0, st, a, k, cb.D[k], H[k], R,
+                               chunk);
+        }
+        switch (DM) {
+            case 8: launch_scatter0<8>(a, cb.D[0], R, st); break;
+            case 16: launch_scatter0<16>(a, cb.D[0], R, st); break;
+            case 32: launch_scatter0<32>(a, cb.D[0], R, st); break;
+            case 64: launch_scatter0<64>(a, cb.D[0], R, st); break;
+            case 128: launch_scatter0<128>(a, cb.D[0], R, st); break;
+            default: return NCF_E_UNSUPPORTED;
+        }
+        return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
     }
     int G = 1;
     while (G < F && G < 64) G <<= 1;
