@@ -321,7 +321,10 @@ int ncf_prepare_epoch(const uint64_t *rows, const int64_t *perm, int64_t n, int6
  * slice's rows by ascending user id, padding rows (user -1) last, as entries
  * (int64_t)user << 32 | offset (offset 0-based within the slice, user -1 for
  * padding): the step reads the user with the offset.  The order among rows of one
- * user is unspecified.  One counting sort per slice in LDS: user_num <= 32767.
+ * user is unspecified.  The buffer holds n such entries followed by n int32 inverse
+ * positions: ((int32_t *)(order + n))[slice start + k] = the position of the slice's
+ * row k in its order (12 bytes per row in all).  One counting sort per slice in LDS:
+ * user_num <= 32767.
  * Computed once per epoch; the step reads it where ncf_uses_user_order(lay) (the
  * layered factored layer 0).
  */

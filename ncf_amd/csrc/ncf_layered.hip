@@ -658,15 +658,21 @@ struct ChainBufs {
 #define NCF_CHAIN_NT 256
 #endif
 constexpr int CNT = NCF_CHAIN_NT, CROWS = CNT / 4;  // threads per block, rows per tile (16 per wave)
-template <int DM, int L>
+// UORD (the step was given the epoch's user order): the chain also sums item runs of
+// D_0 (rows are item-grouped) and db_0 from an LDS image of the tile, and writes each
+// D_0 row at its position in the user order, so the user-side walk
+// (lyr_user_walk_kernel) reads D_0 sequentially.  Without it, D_0 in row order and
+// lyr_scatter0_kernel does all three.
+template <int DM, int L, bool UORD>
 __global__ __launch_bounds__(CNT, 2) void lyr_step_chain_kernel(LyrArgs a, const float* __restrict__ P, ChainBufs o,
                                                                 int64_t R) {
     using C_ = ChainShape<DM, L>;
     constexpr int F = C_::F, TF = C_::TF, NW = CNT / 64;
+    constexpr int SROW = (UORD && DM > 16 * TF ? DM : 16 * TF) + 1;  // staging row: GMF item grads, then D_0
     __shared__ __attribute__((aligned(16))) float sW[C_::W_TOTAL > 0 ? C_::W_TOTAL : 4];
     __shared__ __attribute__((aligned(16))) float sB[C_::B_TOTAL];
     __shared__ __attribute__((aligned(16))) float sWP[2][16 * TF];  // wp: [0] GMF part, [1] tower part (zero-padded)
-    __shared__ float sIg[NW][16][16 * TF + 1];                    // per wave: GMF item-gradient rows
+    __shared__ float sIg[NW][16][SROW];                           // per wave: GMF item-gradient rows, then D_0 rows
     __shared__ int sIt[NW][16];                                    // per wave: item id per row (-1: none)
     __shared__ float sred[2 * 16 * TF + 2];                        // block sums: dwp GMF | dwp tower | dbp | loss
     const Sel s = select_rows(a);
@@ -708,6 +714,14 @@ __global__ __launch_bounds__(CNT, 2) void lyr_step_chain_kernel(LyrArgs a, const
         sWP[1][e] = e < F ? prm[lay.wp + Pg + e] : 0.f;
     }
     for (int e = t; e < 2 * 16 * TF + 2; e += CNT) sred[e] = 0.f;
+    __shared__ float sdb0[UORD ? DM : 1];  // UORD: db_0 block sums
+    if (UORD)
+        for (int e = t; e < DM; e += CNT) sdb0[e] = 0.f;
+    const int32_t* inv = nullptr;  // UORD: row offset -> position in the user order (ncf_user_order)
+    if constexpr (UORD) inv = reinterpret_cast<const int32_t*>(a.uorder + a.ctl->n_total) + s.base;
+    float db0[(DM + 63) / 64];
+#pragma unroll
+    for (int i = 0; i < (DM + 63) / 64; ++i) db0[i] = 0.f;
     __syncthreads();
     const float bp = prm[lay.bp];
     // per-lane partials over the block's rows: dwp (features 16q + 4g .. +3), dbp, loss
@@ -821,8 +835,8 @@ __global__ __launch_bounds__(CNT, 2) void lyr_step_chain_kernel(LyrArgs a, const
         }
         if (g == 0) aB += dz;
         // ---- GMF backward: user rows per row, item rows staged for the run walk
+        if (g == 0) sIt[w][c] = valid ? it : -1;
         if (gmf) {
-            if (g == 0) sIt[w][c] = valid ? it : -1;
 #pragma unroll
             for (int q = 0; q < TF; ++q) {
                 const int j0 = 16 * q + 4 * g;
@@ -839,6 +853,30 @@ __global__ __launch_bounds__(CNT, 2) void lyr_step_chain_kernel(LyrArgs a, const
                 }
             }
         }
+        // ---- GMF item rows: runs of equal items summed (lane = feature) before the atomics
+        if (gmf) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // same-wave LDS hand-off
+            int ids[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) ids[r] = __builtin_amdgcn_readfirstlane(sIt[w][r]);
+            for (int f0 = 0; f0 < F; f0 += 64) {
+                const int f = f0 + l;
+                const int fc = f < F ? f : F - 1;
+                float v[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[r] = sIg[w][r][fc];
+                float run = 0.f;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    run += v[r];
+                    if (r == 15 || ids[r + 1] != ids[r]) {
+                        if (ids[r] >= 0 && f < F) atomicAdd(a.grads + lay.ig + (int64_t)ids[r] * F + f, run);
+                        run = 0.f;
+                    }
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next tile's writes
+        }
         // ---- tower backward: D_{L-1} = dz wp [H_L > 0], then D_{k-1} = (D_k W_k) [H_k > 0]
         f4 d[C_::KT1];
 #pragma unroll
@@ -853,7 +891,11 @@ __global__ __launch_bounds__(CNT, 2) void lyr_step_chain_kernel(LyrArgs a, const
             d[q].z = h[L][q].z > 0.f ? dz * wm.z : 0.f;
             d[q].w = h[L][q].w > 0.f ? dz * wm.w : 0.f;
             const int j0 = 16 * q + 4 * g;
-            if (m < R && j0 < F) *reinterpret_cast<f4*>(o.D[L - 1] + m * F + j0) = d[q];
+            if (UORD && L == 1) {  // D_0 at the row's position in the user order
+                if (m < s.nloc && j0 < F) *reinterpret_cast<f4*>(o.D[0] + (int64_t)inv[m] * F + j0) = d[q];
+            } else if (m < R && j0 < F) {
+                *reinterpret_cast<f4*>(o.D[L - 1] + m * F + j0) = d[q];
+            }
         }
 #pragma unroll
         for (int k = L - 1; k >= 1; --k) {
@@ -886,28 +928,45 @@ __global__ __launch_bounds__(CNT, 2) void lyr_step_chain_kernel(LyrArgs a, const
                 dd.z = hv.z > 0.f ? acc[m2].z : 0.f;
                 dd.w = hv.w > 0.f ? acc[m2].w : 0.f;
                 const int j0 = 16 * m2 + 4 * g;
-                if (m < R && j0 < in) *reinterpret_cast<f4*>(o.D[k - 1] + m * in + j0) = dd;
+                if (UORD && k == 1) {  // D_0 at the row's position in the user order
+                    if (m < s.nloc && j0 < in) *reinterpret_cast<f4*>(o.D[0] + (int64_t)inv[m] * in + j0) = dd;
+                } else if (m < R && j0 < in) {
+                    *reinterpret_cast<f4*>(o.D[k - 1] + m * in + j0) = dd;
+                }
                 d[m2] = dd;
             }
         }
-        // ---- GMF item rows: runs of equal items summed (lane = feature) before the atomics
-        if (gmf) {
+        // ---- D_0 (UORD): item runs and db_0 from the tile's LDS image, rows to user-order positions
+        if constexpr (UORD) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the GMF walk's reads are done
+#pragma unroll
+            for (int m2 = 0; m2 < C_::KT1; ++m2) {
+                const int j0 = 16 * m2 + 4 * g;
+                if (j0 < DM) {
+                    sIg[w][c][j0] = d[m2].x;
+                    sIg[w][c][j0 + 1] = d[m2].y;
+                    sIg[w][c][j0 + 2] = d[m2].z;
+                    sIg[w][c][j0 + 3] = d[m2].w;
+                }
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // same-wave LDS hand-off
             int ids[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) ids[r] = __builtin_amdgcn_readfirstlane(sIt[w][r]);
-            for (int f0 = 0; f0 < F; f0 += 64) {
-                const int f = f0 + l;
-                const int fc = f < F ? f : F - 1;
+#pragma unroll
+            for (int i = 0; i < (DM + 63) / 64; ++i) {
+                const int f = 64 * i + l;
+                const int fc = f < DM ? f : DM - 1;
                 float v[16];
 #pragma unroll
                 for (int r = 0; r < 16; ++r) v[r] = sIg[w][r][fc];
                 float run = 0.f;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
+                    db0[i] += v[r];  // padding rows carry 0
                     run += v[r];
                     if (r == 15 || ids[r + 1] != ids[r]) {
-                        if (ids[r] >= 0 && f < F) atomicAdd(a.grads + lay.ig + (int64_t)ids[r] * F + f, run);
+                        if (ids[r] >= 0 && f < DM) atomicAdd(a.grads + lay.im + (int64_t)ids[r] * DM + f, run);
                         run = 0.f;
                     }
                 }
@@ -942,9 +1001,18 @@ __global__ __launch_bounds__(CNT, 2) void lyr_step_chain_kernel(LyrArgs a, const
         atomicAdd(&sred[2 * 16 * TF], aB);
         atomicAdd(&sred[2 * 16 * TF + 1], aL);
     }
+    if constexpr (UORD) {
+#pragma unroll
+        for (int i = 0; i < (DM + 63) / 64; ++i)
+            if (64 * i + l < DM) atomicAdd(&sdb0[64 * i + l], db0[i]);
+    }
     __syncthreads();
     const int64_t tb = lay.tower_begin;
     float* slab = a.slab + (int64_t)(blockIdx.x % lyr_slab_rows(&lay)) * (lay.tower_len + 64);
+    if constexpr (UORD) {
+        for (int e = t; e < DM; e += CNT)
+            if (sdb0[e] != 0.f) atomicAdd(slab + (lay.b[0] - tb) + e, sdb0[e]);
+    }
     for (int e = t; e < 2 * F + 2; e += CNT) {
         int src;
         int64_t off;
@@ -975,10 +1043,15 @@ static bool launch_step_chain(const LyrArgs& a, const float* P, const ChainBufs&
     int64_t grid = (R + CROWS - 1) / CROWS;
     if (grid > NCF_CHAIN_GRID) grid = NCF_CHAIN_GRID;  // weights staged once per block, several tiles each
     if (grid < 1) grid = 1;
-#define NCF_CHAIN(D, LL)                                                                                      \
-    if (DM == D && L == LL) {                                                                                 \
-        hipLaunchKernelGGL((lyr_step_chain_kernel<D, LL>), dim3((unsigned)grid), dim3(CNT), 0, st, a, P, o, R); \
-        return true;                                                                                          \
+#define NCF_CHAIN(D, LL)                                                                                   \
+    if (DM == D && L == LL) {                                                                              \
+        if (a.uorder)                                                                                      \
+            hipLaunchKernelGGL((lyr_step_chain_kernel<D, LL, true>), dim3((unsigned)grid), dim3(CNT), 0, st, a, \
+                               P, o, R);                                                                   \
+        else                                                                                               \
+            hipLaunchKernelGGL((lyr_step_chain_kernel<D, LL, false>), dim3((unsigned)grid), dim3(CNT), 0, st, a, \
+                               P, o, R);                                                                   \
+        return true;                                                                                       \
     }
     NCF_CHAIN(8, 1) NCF_CHAIN(8, 2)
     NCF_CHAIN(16, 1) NCF_CHAIN(16, 2) NCF_CHAIN(16, 3)
@@ -1085,6 +1158,49 @@ static void launch_scatter0(const LyrArgs& a, const float* D0, int64_t R, hipStr
         hipLaunchKernelGGL((lyr_scatter0_kernel<DM, true>), grid, dim3(SC_NT), 0, st, a, D0);
     else
         hipLaunchKernelGGL((lyr_scatter0_kernel<DM, false>), grid, dim3(SC_NT), 0, st, a, D0);
+}
+
+// User side of the factored layer 0 after the step chain (UORD): D_0 rows already
+// sit in user order (position p of the rank slice at D0u + p * DM), so a walker of
+// DM lanes reads SC_ROWS consecutive positions sequentially, takes each position's
+// user from its order entry (user << 32 | offset) and sums runs of equal users
+// before the atomics into grads[um].  Items and db_0 were done in the chain.
+template <int DM>
+__global__ __launch_bounds__(SC_NT) void lyr_user_walk_kernel(LyrArgs a, const float* __restrict__ D0u) {
+    constexpr int NW = SC_NT / DM;
+    const Sel s = select_rows(a);
+    const ncf_layout& lay = a.lay;
+    const int n = threadIdx.x % DM, wk = threadIdx.x / DM;
+    const int64_t r0 = ((int64_t)blockIdx.x * NW + wk) * SC_ROWS;
+    if (r0 >= s.nloc) return;
+    const int nr = (int)(s.nloc - r0 < SC_ROWS ? s.nloc - r0 : SC_ROWS);
+    int us[SC_ROWS];
+    float v[SC_ROWS];
+#pragma unroll
+    for (int k = 0; k < SC_ROWS; ++k) {
+        const int64_t p = r0 + (k < nr ? k : 0);
+        us[k] = (int)(a.uorder[s.base + p] >> 32);
+        v[k] = D0u[p * DM + n];
+    }
+    float run = 0.f;
+#pragma unroll
+    for (int k = 0; k < SC_ROWS; ++k) {
+        if (k < nr) {
+            const bool end = k + 1 >= nr || us[k + 1 < SC_ROWS ? k + 1 : k] != us[k];
+            run += v[k];
+            if (end) {
+                if (us[k] >= 0) atomicAdd(a.grads + lay.um + (int64_t)us[k] * DM + n, run);
+                run = 0.f;
+            }
+        }
+    }
+}
+
+template <int DM>
+static void launch_user_walk(const LyrArgs& a, const float* D0u, int64_t R, hipStream_t st) {
+    const int64_t per_block = (int64_t)(SC_NT / DM) * SC_ROWS;
+    hipLaunchKernelGGL((lyr_user_walk_kernel<DM>), dim3((unsigned)((R + per_block - 1) / per_block)), dim3(SC_NT), 0,
+                       st, a, D0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -1366,14 +1482,20 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             hipLaunchKernelGGL((lyr_bwd_w_kernel<false, false, true>), gw, dim3(GNT), 0, st, a, k, cb.D[k], H[k], R,
                                chunk);
         }
+        // with the user order the chain did the item runs and db_0 and left D_0 in user
+        // order (the user walk reads it sequentially); without, the full scatter
+#define NCF_L0(DD)                           \
+    case DD:                                 \
+        if (a.uorder)                        \
+            launch_user_walk<DD>(a, cb.D[0], R, st); \
+        else                                 \
+            launch_scatter0<DD>(a, cb.D[0], R, st);  \
+        break;
         switch (DM) {
-            case 8: launch_scatter0<8>(a, cb.D[0], R, st); break;
-            case 16: launch_scatter0<16>(a, cb.D[0], R, st); break;
-            case 32: launch_scatter0<32>(a, cb.D[0], R, st); break;
-            case 64: launch_scatter0<64>(a, cb.D[0], R, st); break;
-            case 128: launch_scatter0<128>(a, cb.D[0], R, st); break;
+            NCF_L0(8) NCF_L0(16) NCF_L0(32) NCF_L0(64) NCF_L0(128)
             default: return NCF_E_UNSUPPORTED;
         }
+#undef NCF_L0
         return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
     }
     int G = 1;

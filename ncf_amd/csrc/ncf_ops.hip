@@ -559,6 +559,7 @@ __global__ __launch_bounds__(UO_THREADS) void user_order_kernel(const uint64_t* 
     const int len = (int)((cnt - lo) < per ? (cnt - lo) : per);
     const uint64_t* rb = rows + b0 + lo;
     int64_t* ob = order + b0 + lo;
+    int32_t* ib = reinterpret_cast<int32_t*>(order + n) + b0 + lo;  // inverse: row offset -> position
     const int nbin = user_num + 1;
     for (int i = tid; i < nbin; i += UO_THREADS) uh[i] = 0;
     __syncthreads();
@@ -615,9 +616,11 @@ __global__ __launch_bounds__(UO_THREADS) void user_order_kernel(const uint64_t* 
 #pragma unroll
         for (int q = 0; q < UO_UNROLL; ++q) {
             const int k = k0 + q * UO_THREADS + tid;
-            if (bins[q] >= 0)
-                ob[atomicAdd(&uh[bins[q]], 1)] =
-                    (int64_t)(((uint64_t)(uint32_t)(bins[q] < user_num ? bins[q] : -1) << 32) | (uint32_t)k);
+            if (bins[q] >= 0) {
+                const int pos = atomicAdd(&uh[bins[q]], 1);
+                ob[pos] = (int64_t)(((uint64_t)(uint32_t)(bins[q] < user_num ? bins[q] : -1) << 32) | (uint32_t)k);
+                ib[k] = pos;
+            }
         }
     }
 }

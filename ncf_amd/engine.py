@@ -205,7 +205,8 @@ class TrainEngine:
         key = (rows.data_ptr(), rows.numel())
         buf = self._orders.get(key)
         if buf is None:
-            buf = self._orders[key] = torch.empty(rows.numel(), dtype=torch.int64, device=self.device)
+            n = rows.numel()  # n int64 entries + n int32 inverse positions (ncf_user_order)
+            buf = self._orders[key] = torch.empty(n + (n + 1) // 2, dtype=torch.int64, device=self.device)
         return buf
 
     def user_order_ptr(self):

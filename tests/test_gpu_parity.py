@@ -162,7 +162,7 @@ def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3, flags=0, order=False):
     rows = ops.pack_rows(u, it, y)
     uord = None
     if order:
-        uord = torch.empty(B, dtype=torch.int64, device=DEV)
+        uord = torch.empty(B + (B + 1) // 2, dtype=torch.int64, device=DEV)  # entries + int32 inverse
         L.check(L.hip().ncf_user_order(rows.data_ptr(), B, B, 1, U, uord.data_ptr(), st), "order")
     L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
                                    None if uord is None else uord.data_ptr(), None, ctl.data_ptr(), B, 1, 0,
@@ -397,7 +397,7 @@ def test_rank_shards_sum_to_full_batch(world, f, Lyr):
         ws = ops.new_workspace(lay, (B + world - 1) // world, DEV)
         ctl = ops.new_ctl(B, DEV)
         # the rank slices' user order (used where ncf_uses_user_order: NCF(32,3))
-        uord = torch.empty(B, dtype=torch.int64, device=DEV)
+        uord = torch.empty(B + (B + 1) // 2, dtype=torch.int64, device=DEV)  # entries + int32 inverse
         L.check(L.hip().ncf_user_order(rows.data_ptr(), B, B, world, U, uord.data_ptr(), st), "order")
         L.check(L.hip().ncf_train_step(L.ctypes.byref(lay), flat.data_ptr(), gflat.data_ptr(), rows.data_ptr(),
                                        uord.data_ptr(), None, ctl.data_ptr(), B, world, rank, L.DZ_BCE,
@@ -521,11 +521,12 @@ def test_user_order_sorts_each_rank_slice(n, bs, world, users):
     rows = _rand_rows(rng, n, users, 3707, hot=0.2)
     pad = torch.as_tensor(rng.random(n) < 0.01, device=DEV)
     rows = torch.where(pad, rows | 0xFFFFFFFF, rows)  # user -1
-    order = torch.full((n,), -7, dtype=torch.int64, device=DEV)
+    order = torch.full((n + (n + 1) // 2,), -7, dtype=torch.int64, device=DEV)  # entries + int32 inverse
     L.check(L.hip().ncf_user_order(rows.data_ptr(), n, bs, world, users, order.data_ptr(), L.stream_ptr()),
             "ncf_user_order")
     torch.cuda.synchronize()
-    r, e = rows.cpu().numpy(), order.cpu().numpy()
+    r, e = rows.cpu().numpy(), order[:n].cpu().numpy()
+    inv = order.cpu().numpy().view(np.int32)[2 * n:3 * n]
     o, ou = e & 0xFFFFFFFF, e >> 32  # entry: user << 32 | offset (user -1: padding)
     slices = 0
     for b0 in range(0, n, bs):
@@ -535,6 +536,7 @@ def test_user_order_sorts_each_rank_slice(n, bs, world, users):
             s0, ln = b0 + lo, min(per, cnt - lo)
             oo = o[s0:s0 + ln]
             assert np.array_equal(np.sort(oo), np.arange(ln)), "not a permutation of the slice"
+            assert np.array_equal(inv[s0:s0 + ln][oo], np.arange(ln)), "inverse positions"
             u = (r[s0:s0 + ln][oo] & 0xFFFFFFFF).astype(np.int64)
             assert np.array_equal(ou[s0:s0 + ln], np.where(u == 0xFFFFFFFF, -1, u)), "entry user field"
             key = np.where(u == 0xFFFFFFFF, users, u)
