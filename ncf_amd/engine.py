@@ -62,6 +62,18 @@ def _active_ranges(model, lay, extra=None):
 
 
 class TrainEngine:
+    # world > 1 default exchange: one all-reduce + replicated Adam up to this many flat
+    # floats, zero1 (reduce-scatter, shard Adam, all-gather: the same wire bytes) above.
+    # Sharding saves 7/8 of a 32 B/param Adam pass at W = 8 (~5 ps/param at ~6 TB/s)
+    # but costs two more launches and a collective (~16 us per step measured with a
+    # one-rank RCCL group, scripts/dp_overhead.py): break-even near 3-4M floats
+    # (C3 0.79M: allreduce; C4 13.2M: zero1).
+    ALLREDUCE_MAX_FLOATS = 4 << 20
+
+    @classmethod
+    def default_dp_mode(cls, total_floats):
+        return "allreduce" if total_floats <= cls.ALLREDUCE_MAX_FLOATS else "zero1"
+
     def __init__(self, model, lr=1e-3, optimizer="adam", betas=(0.9, 0.999), eps=1e-8,
                  world_size=1, rank=0, process_group=None, max_batches=1 << 16, dp_mode=None, distill=None):
         """distill: an ``ncf_amd.distill.DeviceDistillPlan`` -- the student step then
@@ -70,14 +82,15 @@ class TrainEngine:
         self.model = model
         self.distill = distill
         self.world_size, self.rank, self.group = int(world_size), int(rank), process_group
+        lay = L.layout(model.user_num, model.item_num, model.factor_num, model.num_layers, model.model_type)
         if dp_mode is None:
-            dp_mode = os.environ.get("NCF_DP_MODE", "zero1") if self.world_size > 1 else "single"
+            dp_mode = os.environ.get("NCF_DP_MODE", self.default_dp_mode(int(lay.total))) \
+                if self.world_size > 1 else "single"
         # an explicit exchange mode stands at world 1 (a one-rank group still runs the
         # real collectives: how the captured-collective graph is tested on one GPU)
         if dp_mode not in ("single", "zero1", "allreduce", "sparse"):
             raise ValueError(f"dp_mode {dp_mode!r}")
         self.dp_mode = dp_mode
-        lay = L.layout(model.user_num, model.item_num, model.factor_num, model.num_layers, model.model_type)
         if dp_mode in ("zero1", "sparse"):
             # flat buffers padded to world x shard floats; rank r owns [r*S, (r+1)*S)
             self.shard = D.shard_floats(int(lay.total), self.world_size)
@@ -428,6 +441,13 @@ class TrainEngine:
                 self._graph_k = self._graph_of(body)
         else:
             self._graph = (self._graph_of(self._compute), self._graph_of(self._optimize))
+            if self.dp_mode == "allreduce":
+                # step t's optimizer and step t + 1's compute in one graph: one replay and
+                # one collective per step from the host (run())
+                def opt_compute():
+                    self._optimize()
+                    self._compute()
+                self._graph = self._graph + (self._graph_of(opt_compute),)
             self._graph_k = None
         self._graphs[(self.batch_size, self.n_total, self.rows.data_ptr())] = (self._graph, self._graph_k)
         return self._graph
@@ -456,7 +476,7 @@ class TrainEngine:
     def _replay(self):
         if len(self._graph) == 1:
             self._graph[0].replay()
-        else:
+        else:  # (compute, optimize[, optimize + compute])
             self._graph[0].replay()
             self._allreduce()
             self._graph[1].replay()
@@ -485,6 +505,17 @@ class TrainEngine:
             for _ in range(left // k):
                 self._graph_k.replay()
             left %= k
+        if len(self._graph) == 3 and left >= 2:
+            # eager all-reduce between graphs: compute(t0), then [optimize(t), compute(t+1)]
+            # per step, the last optimize after the loop -- the launch order of
+            # left x _replay() with one host replay per step fewer
+            self._graph[0].replay()
+            self._allreduce()
+            for _ in range(left - 1):
+                self._graph[2].replay()
+                self._allreduce()
+            self._graph[1].replay()
+            return
         for _ in range(left):
             self._replay()
 

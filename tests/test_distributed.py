@@ -95,7 +95,8 @@ def test_gloo_two_ranks_equal_single_process_gradient():
 
 # ---------------------------------------------------------------------------
 # zero1: reduce-scatter -> Adam on the own shard -> in-place all-gather
-# (ncf_amd.engine.TrainEngine(dp_mode="zero1"), the default for world > 1)
+# (ncf_amd.engine.TrainEngine(dp_mode="zero1"), the default for world > 1 above
+# TrainEngine.ALLREDUCE_MAX_FLOATS)
 
 def test_shard_floats_and_ranges_cover_active_params():
     from ncf_amd.distributed import shard_floats, shard_ranges

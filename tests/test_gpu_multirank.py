@@ -71,6 +71,8 @@ def _free_port():
 @pytest.mark.parametrize("mt,f,nl,use_graph,dp_mode", [("NeuMF-end", 16, 3, True, "zero1"),
                                                        ("NeuMF-end", 16, 3, False, "zero1"),
                                                        ("NeuMF-end", 16, 3, True, "allreduce"),
+                                                       ("NeuMF-end", 16, 3, True, None),  # default: allreduce
+                                                       ("NeuMF-end", 16, 3, False, "allreduce"),
                                                        ("NeuMF-end", 16, 3, True, "sparse"),
                                                        ("NeuMF-end", 16, 3, False, "sparse"),
                                                        ("GMF", 16, 3, True, "sparse"),
