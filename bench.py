@@ -265,7 +265,10 @@ def e2e_fit(cfg, ds, dev, epochs):
             "note": "wall clock of Trainer.fit(epochs) (per epoch: fresh negatives and permutation, the "
                     "steps, metrics() over the leave-one-out test set, the printed-line readback), after "
                     "one warm-up fit(1)",
-            "prefetch_hits": tr._pipe.stats["prefetch_hits"] if tr._pipe is not None else None}
+            "prefetch_hits": tr._pipe.stats["prefetch_hits"] if tr._pipe is not None else None,
+            "pipeline_depth": tr._pipe.depth if tr._pipe is not None else None,
+            "boundary_join_ms": [round(x[0], 2) for x in tr._pipe.stats.get("boundary_ms", [])[1:]]
+            if tr._pipe is not None else None}
 
 
 def main():
@@ -279,7 +282,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--skip-cpu-baseline", action="store_true")
     ap.add_argument("--skip-eval", action="store_true")
-    ap.add_argument("--e2e-epochs", type=int, default=8, help="Trainer.fit epochs for the e2e figure (0: skip)")
+    ap.add_argument("--e2e-epochs", type=int, default=16, help="Trainer.fit epochs for the e2e figure (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -31,6 +31,7 @@ prefetch, and the epoch is built synchronously.
 from __future__ import annotations
 
 import collections
+import os
 import threading
 import time
 
@@ -82,7 +83,7 @@ class EpochPipeline:
     """depth: epochs staged ahead (host draws, uploads and device build); slots =
     depth + 1 sets of buffers, one being trained from."""
 
-    def __init__(self, dataset, device, batch_size, item_num, user_num=None, prefetch=True, depth=2):
+    def __init__(self, dataset, device, batch_size, item_num, user_num=None, prefetch=True, depth=None):
         self.ds = dataset
         self.device = torch.device(device)
         self.batch_size = int(batch_size)
@@ -102,6 +103,8 @@ class EpochPipeline:
         self.pi = torch.as_tensor(pi, dtype=torch.int32).to(dev)
         self.S = self.P * self.ng
         self.n = self.P + self.S
+        if depth is None:
+            depth = int(os.environ.get("NCF_PIPE_DEPTH", "2"))
         self.depth = max(1, int(depth)) if prefetch else 0
         self.prefetch = prefetch
         K = self.depth + 1
