@@ -73,6 +73,7 @@ typedef struct ncf_layout {
 /* ncf_layout.flags (set by ncf_layout_tune; every entry point reads them from the
  * layout it is given, so one tuned layout must be used for a whole step) */
 #define NCF_LAYOUT_PER_ROW_L0 0x1   /* per-row layer-0 gradients even where the factored path applies */
+#define NCF_LAYOUT_LAYERED 0x2      /* training steps on the layered path even where a fused kernel exists */
 #define NCF_LAYOUT_WG_SHIFT 8       /* bits 8..19: workgroups of the fused step (0 = ncf_slab_rows()) */
 #define NCF_LAYOUT_WG_MASK 0xfff
 

@@ -1034,6 +1034,7 @@ static const KernelEntry* fused_entry(const ncf_layout* lay) {
 }
 // Fused kernel of a training step: none with dropout (the layered path applies it).
 static const KernelEntry* train_fused(const ncf_layout* lay) {
+    if (lay->flags & NCF_LAYOUT_LAYERED) return nullptr;
     return lay->dropout > 0.f ? nullptr : fused_entry(lay);
 }
 static int fact_dm(const ncf_layout* lay) { return lay->factor_num << (lay->num_layers - 1); }

@@ -184,6 +184,8 @@ class TrainEngine:
             # launch shape for this batch size: workgroups = its 128-row tiles (up to
             # one per CU), per-row layer 0 for batches small against the tables
             L.check(L.hip().ncf_layout_tune(ctypes.byref(self.lay), per), "ncf_layout_tune")
+            if os.environ.get("NCF_FORCE_LAYERED", "0") == "1":  # A/B: the layered path for any shape
+                self.lay.flags |= L.LAYOUT_LAYERED
             self.ws = ops.new_workspace(self.lay, per, self.device)
         self.batch_size = int(batch_size)
         if self.num_batches > self.loss_hist.numel():
