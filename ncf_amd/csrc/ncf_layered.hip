@@ -29,6 +29,8 @@
 // loaders map lanes along the operand's contiguous memory dimension.  Rows at
 // or past the batch's end are padding: they gather id 0 and their dz is 0, so
 // every gradient contribution from them is zero.
+#include <cstring>
+
 #include "ncf_common.h"
 #include "ncf_layered.h"
 
@@ -401,28 +403,29 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, con
 // into the slab (tower partials, reduced by ncf_reduce_slab).
 // grid (ceil(J/64), ceil((s_k+1)/64), splits).
 template <bool FIRST, bool DROP, bool VEC>
-__global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const float* __restrict__ D,
-                                                        const float* __restrict__ Ain, int64_t R, int64_t chunk) {
+__device__ __forceinline__ void bwd_w_body(const LyrArgs& a, int k, const float* __restrict__ D,
+                                           const float* __restrict__ Ain, int64_t R, int64_t chunk, int bx, int by,
+                                           int bz) {
     __shared__ int su[GBK * 64], si[GBK * 64];  // ids of up to 1024 rows of the chunk (FIRST)
     const Sel s = select_rows(a);
     const ncf_layout& lay = a.lay;
     const int DM = lay.factor_num << (lay.num_layers - 1);
     const int K = (2 * DM) >> k, J = K / 2;
-    const int j0 = blockIdx.x * GBM;
-    const int c0 = blockIdx.y * GBN;
-    const int64_t r0 = (int64_t)blockIdx.z * chunk;
+    const int j0 = bx * GBM;
+    const int c0 = by * GBN;
+    const int64_t r0 = (int64_t)bz * chunk;
     int64_t r1 = r0 + chunk;
     if (r1 > R) r1 = R;
     if (r1 > s.nloc) r1 = s.nloc;  // padding rows carry dY = 0
     if (r0 >= r1) return;          // block-uniform
     const float* prm = a.params;
-    float* slab = a.slab + (int64_t)(blockIdx.z % lyr_slab_rows(&lay)) * (lay.tower_len + 64);
+    float* slab = a.slab + (int64_t)(bz % lyr_slab_rows(&lay)) * (lay.tower_len + 64);
     const int64_t tb = lay.tower_begin;
     const Drop dr = DROP ? drop_of(a) : Drop{false, 0, 0, 0, 1.f};
     // db_k = column sums of dY_k: summed by the blocks of column tile 0 from the dY
     // values they stage anyway (store-time hook of the GEMM core), instead of a ones
     // column appended to A, which costs a whole extra 64-wide tile when K % 64 == 0
-    const bool dbt = blockIdx.y == 0;  // block-uniform
+    const bool dbt = by == 0;  // block-uniform
     f4 db4 = zero4();
     float db1 = 0.f;
     auto sa4 = [&](const f4& v) {
@@ -549,6 +552,37 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
             if (j < J && sum != 0.f) atomicAdd(slab + (lay.b[k] - tb) + j, sum);
         }
     }
+}
+
+template <bool FIRST, bool DROP, bool VEC>
+__global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const float* __restrict__ D,
+                                                        const float* __restrict__ Ain, int64_t R, int64_t chunk) {
+    bwd_w_body<FIRST, DROP, VEC>(a, k, D, Ain, R, chunk, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// The weight gradients of several layers k >= 1 in one launch (the step chain leaves
+// every D_k and H_k in the workspace at once): a 1-D grid, layer i owning blocks
+// [start[i], start[i + 1]), each decoded to the (j tile, column tile, row chunk) of
+// lyr_bwd_w_kernel's 3-D grid.  The layers' GEMMs are small (NCF(32,3): 64 x 128 and
+// 32 x 64 outputs over 65,536 rows): two launches paid the launch ramp and the drain
+// of the split atomics twice.
+struct BwMulti {
+    int n;
+    int k[3], gx[3], gy[3];
+    const float* D[3];
+    const float* A[3];
+    int64_t chunk[3];
+    int start[4];
+};
+__global__ __launch_bounds__(GNT) void lyr_bwd_w_multi_kernel(LyrArgs a, BwMulti m, int64_t R) {
+    const int b = blockIdx.x;
+    int i = 0;
+#pragma unroll
+    for (int q = 1; q < 3; ++q)
+        if (q < m.n && b >= m.start[q]) i = q;
+    const int loc = b - m.start[i], per = m.gx[i] * m.gy[i];
+    const int bz = loc / per, rem = loc - bz * per;
+    bwd_w_body<false, false, true>(a, m.k[i], m.D[i], m.A[i], R, m.chunk[i], rem % m.gx[i], rem / m.gx[i], bz);
 }
 
 // ---------------------------------------------------------------------------
@@ -1467,7 +1501,9 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             }
         }
     }
-    if (chained) {  // weight gradients of layers L-1 .. 1, then the layer-0 scatter
+    if (chained) {  // weight gradients of layers L-1 .. 1 (one launch), then the layer-0 scatter
+        BwMulti bm;
+        memset(&bm, 0, sizeof(bm));
         for (int k = L - 1; k >= 1; --k) {
             const int K = (2 * DM) >> k, J = K / 2;
             const int64_t tiles = (int64_t)((J + GBM - 1) / GBM) * ((K + GBN - 1) / GBN);
@@ -1478,10 +1514,17 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             int64_t chunk = (R + splits - 1) / splits;
             chunk = (chunk + GBK - 1) / GBK * GBK;
             splits = (R + chunk - 1) / chunk;
-            const dim3 gw((unsigned)((J + GBM - 1) / GBM), (unsigned)((K + GBN - 1) / GBN), (unsigned)splits);
-            hipLaunchKernelGGL((lyr_bwd_w_kernel<false, false, true>), gw, dim3(GNT), 0, st, a, k, cb.D[k], H[k], R,
-                               chunk);
+            const int i = bm.n++;
+            bm.k[i] = k;
+            bm.gx[i] = (J + GBM - 1) / GBM;
+            bm.gy[i] = (K + GBN - 1) / GBN;
+            bm.D[i] = cb.D[k];
+            bm.A[i] = H[k];
+            bm.chunk[i] = chunk;
+            bm.start[i + 1] = bm.start[i] + (int)(bm.gx[i] * bm.gy[i] * splits);
         }
+        if (bm.n > 0)
+            hipLaunchKernelGGL(lyr_bwd_w_multi_kernel, dim3((unsigned)bm.start[bm.n]), dim3(GNT), 0, st, a, bm, R);
         // with the user order the chain did the item runs and db_0 and left D_0 in user
         // order (the user walk reads it sequentially); without, the full scatter
 #define NCF_L0(DD)                           \
