@@ -566,6 +566,8 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const 
 // lyr_bwd_w_kernel's 3-D grid.  The layers' GEMMs are small (NCF(32,3): 64 x 128 and
 // 32 x 64 outputs over 65,536 rows): two launches paid the launch ramp and the drain
 // of the split atomics twice.
+// With the user order, blocks past the layers' run the user-order walk of D_0
+// (user_walk_body with 256-thread blocks), which is independent of them.
 struct BwMulti {
     int n;
     int k[3], gx[3], gy[3];
@@ -573,9 +575,17 @@ struct BwMulti {
     const float* A[3];
     int64_t chunk[3];
     int start[4];
+    const float* D0u;  // user-order D_0 (nullptr: no walk blocks)
+    int walk_dm;
 };
+__device__ __forceinline__ void user_walk_body(const LyrArgs& a, const float* __restrict__ D0u, int64_t blk,
+                                               int nt, int dm);
 __global__ __launch_bounds__(GNT) void lyr_bwd_w_multi_kernel(LyrArgs a, BwMulti m, int64_t R) {
     const int b = blockIdx.x;
+    if (b >= m.start[m.n]) {  // block-uniform
+        user_walk_body(a, m.D0u, b - m.start[m.n], GNT, m.walk_dm);
+        return;
+    }
     int i = 0;
 #pragma unroll
     for (int q = 1; q < 3; ++q)
@@ -695,8 +705,8 @@ constexpr int CNT = NCF_CHAIN_NT, CROWS = CNT / 4;  // threads per block, rows p
 // UORD (the step was given the epoch's user order): the chain also sums item runs of
 // D_0 (rows are item-grouped) and db_0 from an LDS image of the tile, and writes each
 // D_0 row at its position in the user order, so the user-side walk
-// (lyr_user_walk_kernel) reads D_0 sequentially.  Without it, D_0 in row order and
-// lyr_scatter0_kernel does all three.
+// (the walk blocks of lyr_bwd_w_multi_kernel) reads D_0 sequentially.  Without it,
+// D_0 in row order and lyr_scatter0_kernel does all three.
 template <int DM, int L, bool UORD>
 __global__ __launch_bounds__(CNT, 2) void lyr_step_chain_kernel(LyrArgs a, const float* __restrict__ P, ChainBufs o,
                                                                 int64_t R) {
@@ -1199,13 +1209,14 @@ static void launch_scatter0(const LyrArgs& a, const float* D0, int64_t R, hipStr
 // DM lanes reads SC_ROWS consecutive positions sequentially, takes each position's
 // user from its order entry (user << 32 | offset) and sums runs of equal users
 // before the atomics into grads[um].  Items and db_0 were done in the chain.
-template <int DM>
-__global__ __launch_bounds__(SC_NT) void lyr_user_walk_kernel(LyrArgs a, const float* __restrict__ D0u) {
-    constexpr int NW = SC_NT / DM;
+// Walker share of the user-order walk: block `blk` of `nt` threads, feature n = t % dm,
+// walker t / dm over SC_ROWS consecutive positions of the user order.
+__device__ __forceinline__ void user_walk_body(const LyrArgs& a, const float* __restrict__ D0u, int64_t blk,
+                                               int nt, int dm) {
     const Sel s = select_rows(a);
     const ncf_layout& lay = a.lay;
-    const int n = threadIdx.x % DM, wk = threadIdx.x / DM;
-    const int64_t r0 = ((int64_t)blockIdx.x * NW + wk) * SC_ROWS;
+    const int n = threadIdx.x % dm, wk = threadIdx.x / dm;
+    const int64_t r0 = (blk * (nt / dm) + wk) * SC_ROWS;
     if (r0 >= s.nloc) return;
     const int nr = (int)(s.nloc - r0 < SC_ROWS ? s.nloc - r0 : SC_ROWS);
     int us[SC_ROWS];
@@ -1214,7 +1225,7 @@ __global__ __launch_bounds__(SC_NT) void lyr_user_walk_kernel(LyrArgs a, const f
     for (int k = 0; k < SC_ROWS; ++k) {
         const int64_t p = r0 + (k < nr ? k : 0);
         us[k] = (int)(a.uorder[s.base + p] >> 32);
-        v[k] = D0u[p * DM + n];
+        v[k] = D0u[p * dm + n];
     }
     float run = 0.f;
 #pragma unroll
@@ -1223,19 +1234,14 @@ __global__ __launch_bounds__(SC_NT) void lyr_user_walk_kernel(LyrArgs a, const f
             const bool end = k + 1 >= nr || us[k + 1 < SC_ROWS ? k + 1 : k] != us[k];
             run += v[k];
             if (end) {
-                if (us[k] >= 0) atomicAdd(a.grads + lay.um + (int64_t)us[k] * DM + n, run);
+                if (us[k] >= 0) atomicAdd(a.grads + lay.um + (int64_t)us[k] * dm + n, run);
                 run = 0.f;
             }
         }
     }
 }
 
-template <int DM>
-static void launch_user_walk(const LyrArgs& a, const float* D0u, int64_t R, hipStream_t st) {
-    const int64_t per_block = (int64_t)(SC_NT / DM) * SC_ROWS;
-    hipLaunchKernelGGL((lyr_user_walk_kernel<DM>), dim3((unsigned)((R + per_block - 1) / per_block)), dim3(SC_NT), 0,
-                       st, a, D0u);
-}
+
 
 // ---------------------------------------------------------------------------
 // Predict + loss + GMF backward.  A walker of G lanes (G = min(64, pow2 >= F);
@@ -1523,15 +1529,22 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             bm.chunk[i] = chunk;
             bm.start[i + 1] = bm.start[i] + (int)(bm.gx[i] * bm.gy[i] * splits);
         }
-        if (bm.n > 0)
-            hipLaunchKernelGGL(lyr_bwd_w_multi_kernel, dim3((unsigned)bm.start[bm.n]), dim3(GNT), 0, st, a, bm, R);
+        int walk = 0;
+        if (a.uorder) {  // the user-order walk of D_0 rides in the same launch
+            const int64_t per_block = (int64_t)(GNT / DM) * SC_ROWS;
+            walk = (int)((R + per_block - 1) / per_block);
+            bm.D0u = cb.D[0];
+            bm.walk_dm = DM;
+        }
+        if (bm.start[bm.n] + walk > 0)
+            hipLaunchKernelGGL(lyr_bwd_w_multi_kernel, dim3((unsigned)(bm.start[bm.n] + walk)), dim3(GNT), 0, st, a, bm,
+                               R);
         // with the user order the chain did the item runs and db_0 and left D_0 in user
-        // order (the user walk reads it sequentially); without, the full scatter
+        // order (the walk blocks of the launch above read it sequentially); without,
+        // the full scatter
 #define NCF_L0(DD)                           \
     case DD:                                 \
-        if (a.uorder)                        \
-            launch_user_walk<DD>(a, cb.D[0], R, st); \
-        else                                 \
+        if (!a.uorder)                       \
             launch_scatter0<DD>(a, cb.D[0], R, st);  \
         break;
         switch (DM) {
