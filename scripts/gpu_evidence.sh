@@ -29,5 +29,12 @@ for cfg in ${CONFIGS:-c2 c4 cli stress}; do
     run "bench_$cfg" 300 python bench.py --config "$cfg" --steps 200 --warmup 20 --skip-cpu-baseline --e2e-epochs 0
     tail -1 "gpurun_out/bench_$cfg.log" >> gpurun_out/configs.jsonl
 done
-[ "${PROFILE:-1}" = "1" ] && run profile 900 bash scripts/profile.sh
+if [ "${PROFILE:-1}" = "1" ]; then
+    for cfg in ${PROFILE_CONFIGS:-c3}; do  # scripts/profile.sh writes fixed names: keep a copy per config
+        export CONFIG=$cfg
+        run "profile_$cfg" 900 bash scripts/profile.sh
+        mkdir -p "gpurun_out/prof_$cfg"
+        cp gpurun_out/prof_summary.md gpurun_out/prof_summary.json gpurun_out/prof/run_kernel_stats.csv "gpurun_out/prof_$cfg/"
+    done
+fi
 echo ALL-DONE
