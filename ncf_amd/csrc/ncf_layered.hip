@@ -801,7 +801,7 @@ __global__ __launch_bounds__(CNT, 2) void lyr_step_chain_kernel(LyrArgs a, const
                     h[1][q].y = fmaxf(vu.y + vi.y + bb.y, 0.f);
                     h[1][q].z = fmaxf(vu.z + vi.z + bb.z, 0.f);
                     h[1][q].w = fmaxf(vu.w + vi.w + bb.w, 0.f);
-                    if (m < R) *reinterpret_cast<f4*>(o.H[1] + m * DM + j0) = h[1][q];
+                    if (L > 1 && m < R) *reinterpret_cast<f4*>(o.H[1] + m * DM + j0) = h[1][q];  // H_L: not stored
                 }
             }
         }
@@ -840,7 +840,7 @@ __global__ __launch_bounds__(CNT, 2) void lyr_step_chain_kernel(LyrArgs a, const
                 hh.z = fmaxf(acc.z, 0.f);
                 hh.w = fmaxf(acc.w, 0.f);
                 const int j0 = 16 * mt + 4 * g;
-                if (m < R && j0 < out) *reinterpret_cast<f4*>(o.H[k + 1] + m * out + j0) = hh;
+                if (k + 1 < L && m < R && j0 < out) *reinterpret_cast<f4*>(o.H[k + 1] + m * out + j0) = hh;
                 h[k + 1][mt] = hh;  // padded outputs are 0: zero weight rows and bias
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -1473,7 +1473,8 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
     ChainBufs cb;
     bool chained = false;
     if (fact && vec && !drop) {
-        for (int k = 0; k < 5; ++k) cb.H[k] = (k >= 1 && k <= L) ? H[k] : nullptr;
+        // H_L feeds nothing after the chain (the predict layer is in it): not stored
+        for (int k = 0; k < 5; ++k) cb.H[k] = (k >= 1 && k < L) ? H[k] : nullptr;
         float* q = Db;
         for (int k = 0; k < 4; ++k) {
             cb.D[k] = k == 0 ? Da : (k < L ? q : nullptr);
