@@ -880,9 +880,12 @@ constexpr int FX_WAVES = 16;  // 16 waves: dW0 / dX output tiles dealt round-rob
 #ifndef NCF_FX_CPB128
 #define NCF_FX_CPB128 2
 #endif
+#ifndef NCF_FX_CH64  // chunk rows up to DM = 64 (experiment switch)
+#define NCF_FX_CH64 64
+#endif
 template <int DM>
 struct FxShape {
-    static constexpr int CH = DM <= 64 ? 64 : 32;
+    static constexpr int CH = DM <= 64 ? NCF_FX_CH64 : 32;
     static constexpr int CPB = DM <= 64 ? 1 : NCF_FX_CPB128;  // chunks per block
     static constexpr int ST = DM + 4, NT = (DM + 15) / 16, Q4 = DM / 4;
     static constexpr int TPW = (NT * NT + FX_WAVES - 1) / FX_WAVES;  // dW0 tiles per wave
@@ -1062,7 +1065,7 @@ static int slab_lo(const ncf_layout* lay) {
     return 0;
 }
 
-static int fact_ch(const ncf_layout* lay) { return fact_dm(lay) <= 64 ? 64 : 32; }  // FxShape<DM>::CH
+static int fact_ch(const ncf_layout* lay) { return fact_dm(lay) <= 64 ? NCF_FX_CH64 : 32; }  // FxShape<DM>::CH
 static int fact_cpb(const ncf_layout* lay) { return fact_dm(lay) <= 64 ? 1 : NCF_FX_CPB128; }  // FxShape<DM>::CPB
 
 static int fact_blocks(const ncf_layout* lay, int* nbu) {
