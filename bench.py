@@ -47,7 +47,29 @@ CONFIGS = {
     "c4": ("ml-20m", 16, 3, 65536),    # ml-20m shape
     "cli": ("ml-1m", 32, 3, 65536),    # train_neumf.py --num_layers 3 with the config's factor_num 32 (layered path)
     "stress": ("ml-1m", 64, 4, 65536), # NCF(64,4): MLP [1024,512,256,128,64] (layered path)
+    "c5": ("ml-1m", 8, 2, 256),        # distillation: student NCF(8,2,'MLP') of teacher NCF(16,3,'NeuMF-end')
 }
+# model type of the trained model per config (NeuMF-end unless listed); C5 trains the
+# student of scripts/train_student.py's default response distillation
+MODEL = {"c5": "MLP"}
+C5_TEACHER = (16, 3, "NeuMF-end")
+
+
+def build_model(cfg, U, I, dev):
+    """(trained model, distillation module or None) of config `cfg`, random init from
+    the current torch seed (teacher first for C5, as train_student.py builds them)."""
+    from ncf_amd.models import NCF
+    _, f, nl, _ = CONFIGS[cfg]
+    if cfg != "c5":
+        return NCF(U, I, f, nl, 0.0, MODEL.get(cfg, "NeuMF-end")).to(dev), None
+    from ncf_amd.distill import ResponseDistillation
+    tf, tl, tm = C5_TEACHER
+    teacher = NCF(U, I, tf, tl, 0.0, tm).to(dev)
+    teacher.eval()
+    student = NCF(U, I, f, nl, 0.0, MODEL["c5"]).to(dev)
+    dist = ResponseDistillation(teacher, student)  # train_student.py default: response, T 2.0, alpha 0.5
+    dist.to(dev)
+    return student, dist
 
 
 def tower_flops_per_row(f, L, model="NeuMF-end"):
@@ -201,15 +223,14 @@ def setup_engine(cfg, ds, train, world, rank, dev, group, global_batch, seed=0):
     """Bit-exact epoch pipeline over the resident data set -> NCF + TrainEngine.
     Identical on every rank (seeded)."""
     from ncf_amd.engine import TrainEngine
-    from ncf_amd.models import NCF
     from ncf_amd.pipeline import EpochPipeline
-    shape, f, nl, _ = CONFIGS[cfg]
     U, I = ds["user_num"], ds["item_num"]
     np.random.seed(seed)
     torch.manual_seed(seed)
-    model = NCF(U, I, f, nl, 0.0, "NeuMF-end").to(dev)
+    model, dist = build_model(cfg, U, I, dev)
     pipe = EpochPipeline(train, dev, global_batch, I, user_num=U, prefetch=True)
-    eng = TrainEngine(model, lr=1e-3, world_size=world, rank=rank, process_group=group)
+    eng = TrainEngine(model, lr=1e-3, world_size=world, rank=rank, process_group=group,
+                      distill=None if dist is None else dist.device_plan())
     eng.stream_buffers = pipe.buffers  # the pipeline alternates two: graphs captured for both up front
     eng.set_epoch_stream(pipe.next_epoch(peek_eval_draw=False), global_batch, checked=True)
 
@@ -239,19 +260,18 @@ def e2e_fit(cfg, ds, dev, epochs):
     at this config on a fresh model; epoch wall times as the scripts print them."""
     from torch.utils.data import DataLoader
     from ncf_amd.data import NCFData
-    from ncf_amd.models import NCF
     from ncf_amd.trainer import Trainer
     shape, f, nl, per_gpu = CONFIGS[cfg]
     U, I = ds["user_num"], ds["item_num"]
     np.random.seed(1)
     torch.manual_seed(1)
-    model = NCF(U, I, f, nl, 0.0, "NeuMF-end").to(dev)
+    model, dist = build_model(cfg, U, I, dev)
     train = NCFData(np.stack([ds["train_users"], ds["train_items"]], 1), I, None, 4, True)
     tu = np.repeat(ds["test_users"], 100)
     ti = np.concatenate([ds["test_items"][:, None], ds["test_negatives"]], 1).reshape(-1)
     test = NCFData(np.stack([tu, ti], 1), I, None, 0, False)
     tr = Trainer(model, train, DataLoader(test, batch_size=100, shuffle=False), batch_size=per_gpu, lr=1e-3,
-                 top_k=10, device=dev, verbose=False)
+                 top_k=10, device=dev, verbose=False, distill=dist)
     tr.fit(1)  # graph capture, prefetch start-up
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -354,20 +374,22 @@ def main():
     kt["ncf_train_step_per_launch_b2b"] = eng.time_train_kernel(50)
     from ncf_amd import ops
     import ncf_amd._lib as L
+    mtype = MODEL.get(args.config, "NeuMF-end")
     fact = ops.fact_mode(eng.lay)
-    path = L.supported("NeuMF-end", f, nl)
+    path = L.supported(mtype, f, nl)
     dm = f * 2 ** (nl - 1)
     rows_per_launch = per_gpu
-    flops = tower_flops_per_row(f, nl) * rows_per_launch
+    flops = tower_flops_per_row(f, nl, mtype) * rows_per_launch
     ms = kt["ncf_train_step_per_launch_b2b"]
     achieved_tf = flops / (ms * 1e-3) / 1e12
     bytes_launch = gather_scatter_bytes_per_row(f, nl) * rows_per_launch
     achieved_gbs = bytes_launch / (ms * 1e-3) / 1e9
     if path == L.PATH_FUSED:
-        names = [f"ncf::ncf_step_kernel<{f}, {nl}, 2, false, {'true' if fact else 'false'}>"]
+        mode = {"GMF": 0, "MLP": 1}.get(mtype, 2)
+        names = [f"ncf::ncf_step_kernel<{f}, {nl}, {mode}, false, {'true' if fact else 'false'}>"]
         if fact:
             names.append(f"ncf::fact_expand_kernel<{dm}>")
-        kname = (f"ncf_step_kernel<{f},{nl},NeuMF,FACT={str(fact).lower()}>"
+        kname = (f"ncf_step_kernel<{f},{nl},{mtype.split('-')[0]},FACT={str(fact).lower()}>"
                  + (f" + fact_expand_kernel<{dm}> (factored layer 0)" if fact else " (per-row layer 0)")
                  + "; launch group timed back to back")
         traffic, traffic_src = pmc_traffic(args.config, names)
@@ -409,7 +431,11 @@ def main():
                      f"train positives, 4 bit-exact sampled negatives each, fresh negatives and permutation "
                      f"every epoch: {epochs_in_timed} epoch boundaries in the timed region; seed 0)"),
             "config": {"workload": f"{args.config.upper()}: NCF(user_num={U}, item_num={I}, factor_num={f}, "
-                                   f"num_layers={nl}, NeuMF-end), Adam lr 1e-3",
+                                   f"num_layers={nl}, {mtype}), Adam lr 1e-3"
+                                   + (f"; response distillation (T 2.0, alpha 0.5) from a random-init teacher "
+                                      f"NCF({C5_TEACHER[0]}, {C5_TEACHER[1]}, {C5_TEACHER[2]}) whose logits of "
+                                      f"each epoch stream are one forward launch at the epoch boundary"
+                                      if args.config == "c5" else ""),
                        "global_batch": global_batch, "per_gpu_batch": per_gpu, "parallelism": f"dp{world}",
                        "mlp_layers": [int(2 * f * 2 ** (nl - 1)) >> k for k in range(nl + 1)],
                        "dp_exchange": eng.dp_mode, "hip_graph": use_graph},

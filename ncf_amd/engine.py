@@ -387,6 +387,9 @@ class TrainEngine:
         sp = L.stream_ptr(self.device)
 
         def launch():
+            if self.distill is not None:  # the student's step: ncf_train_step_kd [+ feature terms]
+                self.distill.launch(self, sp)
+                return
             L.check(lib.ncf_train_step(lay, self.flat.data_ptr(), self.grads.data_ptr(), self.rows.data_ptr(),
                                        self.user_order_ptr(), None, self.ctl.data_ptr(), self.batch_size, self.world_size, self.rank,
                                        L.DZ_BCE, self.ws.data_ptr(), self.ws.numel() * 4, None, sp), "ncf_train_step")

@@ -25,7 +25,7 @@ run() {  # name, seconds, cmd...
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider
 run bench 600 python bench.py
-for cfg in ${CONFIGS:-c2 c4 cli stress}; do
+for cfg in ${CONFIGS:-c2 c4 cli stress c5}; do
     run "bench_$cfg" 300 python bench.py --config "$cfg" --steps 200 --warmup 20 --skip-cpu-baseline --e2e-epochs 0
     tail -1 "gpurun_out/bench_$cfg.log" >> gpurun_out/configs.jsonl
 done
