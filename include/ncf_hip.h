@@ -203,8 +203,9 @@ int ncf_pack_rows(const int32_t *users, const int32_t *items, const float *label
 
 /*
  * Factored layer 0 (MLP shapes with user_num + item_num <= 32768 and dm in
- * {8, 16, 32, 64, 128}, unless NCF_LAYOUT_PER_ROW_L0; ncf_fact_mode says whether it
- * runs): the step scatter-adds, per row, the layer-0 pre-activation gradient D0
+ * {8, 16, 32, 64, 128}, on the layered path also 256 and 512, unless
+ * NCF_LAYOUT_PER_ROW_L0; ncf_fact_mode says whether it runs): the step scatter-adds,
+ * per row, the layer-0 pre-activation gradient D0
  * (width dm) into the user and item rows of grads[um] / grads[im] instead of
  * forming the layer-0 weight and data gradients per row, and a second launch turns
  * those row sums into the true gradients (from the same params the step used):
@@ -212,7 +213,9 @@ int ncf_pack_rows(const int32_t *users, const int32_t *items, const float *label
  *   dW0 = [G^T Um | H^T Im]                   (per-block partials in the tail of the
  *                                              train workspace; ncf_reduce_slab /
  *                                              ncf_reduce_adam_step sum them in a fixed
- *                                              order with the other tower columns).
+ *                                              order with the other tower columns;
+ *                                              dm > 128: added into the slab's W0
+ *                                              columns by GEMM blocks, no partials).
  * Since ABI 8 ncf_train_step / ncf_train_step_kd issue that second launch
  * themselves, so a step is always: ncf_train_step[_kd] -> [ncf_kd_feature_step] ->
  * ncf_reduce_slab or ncf_reduce_adam_step.  ncf_expand_grads is kept as a no-op

@@ -641,6 +641,90 @@ __global__ __launch_bounds__(GNT) void lyr_proj_kernel(ncf_layout lay, const flo
 
 // H_1[m][n] = ReLU(P[u_m][n] + P[U + i_m][n] + b_0[n]), four outputs per thread
 // (padding rows gather id 0, as lyr_fwd_kernel<true>).
+// Factored layer 0 with dm > 128 (NCF(64,4): dm 512), too wide for
+// fact_expand_kernel's LDS-staged W0 half (1 MB): the expansion as GEMMs on the core.
+// G = the D_0 row sums the scatter left in a table's gradient rows.
+//   lyr_fact_dx_kernel   dX = G W0[:, koff : koff + DM] per table into the projection
+//                        buffer (dead after the forward; copied over G afterwards);
+//                        grid (nbu + nbi, ceil(DM / 64)) like lyr_proj_kernel
+//   lyr_fact_dw0_kernel  dW0[:, koff + c] += G^T X over row chunks of each table
+//                        (z < zu: users), into the slab's W0 columns (no partials at
+//                        dm > 128: the reductions read W0 from the slab)
+__global__ __launch_bounds__(GNT) void lyr_fact_dx_kernel(ncf_layout lay, const float* __restrict__ prm,
+                                                          const float* __restrict__ grads, float* __restrict__ out,
+                                                          int nbu) {
+    const int DM = lay.factor_num << (lay.num_layers - 1);
+    const bool user = (int)blockIdx.x < nbu;
+    const int64_t nrows = user ? lay.user_num : lay.item_num;
+    const int64_t m0 = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * GBM;
+    const int n0 = blockIdx.y * GBN;
+    const float* G = grads + (user ? lay.um : lay.im);
+    const float* W = prm + lay.w[0] + (user ? 0 : DM);  // W0[o][koff + i], row stride 2 DM
+    float* O = out + (user ? 0 : (int64_t)lay.user_num * DM);
+    auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) {
+                const int n = n0 + wn + 16 * tj + (l & 15);
+                if (n >= DM) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t m = m0 + wm + 16 * ti + 4 * (l >> 4) + r;
+                    if (m < nrows) O[m * DM + n] = lane_get(acc[ti][tj], r);
+                }
+            }
+    };
+    auto ga4 = [&](int r, int64_t k) -> f4 {  // G[m][o..o+3]
+        const int64_t m = m0 + r;
+        return (m < nrows && k < DM) ? ld4(G + m * DM + k) : zero4();
+    };
+    auto gb4 = [&](int64_t k, int n) -> f4 {  // W0[o][koff + i .. + 3]
+        const int nn = n0 + n;
+        return (k < DM && nn < DM) ? ld4(W + k * 2 * DM + nn) : zero4();
+    };
+    gemm_block_v<true, false>(0, DM, ga4, gb4, ep);
+}
+
+__global__ __launch_bounds__(GNT) void lyr_fact_dw0_kernel(LyrArgs a, int zu, int64_t chunk) {
+    const ncf_layout& lay = a.lay;
+    const int DM = lay.factor_num << (lay.num_layers - 1);
+    const bool user = (int)blockIdx.z < zu;
+    const int64_t nrows = user ? lay.user_num : lay.item_num;
+    const int64_t r0 = (int64_t)(user ? blockIdx.z : blockIdx.z - zu) * chunk;
+    const int64_t r1 = r0 + chunk < nrows ? r0 + chunk : nrows;
+    if (r0 >= r1) return;  // block-uniform
+    const int o0 = blockIdx.x * GBM, c0 = blockIdx.y * GBN;
+    const float* G = a.grads + (user ? lay.um : lay.im);
+    const float* X = a.params + (user ? lay.um : lay.im);
+    const int koff = user ? 0 : DM;
+    float* slab = a.slab + (int64_t)(blockIdx.z % lyr_slab_rows(&lay)) * (lay.tower_len + 64) +
+                  (lay.w[0] - lay.tower_begin);
+    auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) {
+                const int c = c0 + wn + 16 * tj + (l & 15);
+                if (c >= DM) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int o = o0 + wm + 16 * ti + 4 * (l >> 4) + r;
+                    if (o < DM) atomicAdd(slab + (int64_t)o * 2 * DM + koff + c, lane_get(acc[ti][tj], r));
+                }
+            }
+    };
+    auto ga4 = [&](int jr, int64_t m) -> f4 {  // G[m][o .. o + 3]
+        const int o = o0 + jr;
+        return (m < r1 && o < DM) ? ld4(G + m * DM + o) : zero4();
+    };
+    auto gb4 = [&](int64_t m, int cr) -> f4 {  // X[m][c .. c + 3]
+        const int c = c0 + cr;
+        return (m < r1 && c < DM) ? ld4(X + m * DM + c) : zero4();
+    };
+    gemm_block_v<false, false>(r0, r1, ga4, gb4, ep);
+}
+
 __global__ __launch_bounds__(GNT) void lyr_fwd0_fact_kernel(LyrArgs a, const float* __restrict__ P,
                                                             float* __restrict__ H1, int64_t R) {
     const Sel s = select_rows(a);
@@ -1584,13 +1668,32 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
     for (int k = L - 1; k >= 0; --k) {
         const int K = (2 * DM) >> k, J = K / 2;
         if (k == 0 && fact) {  // dY_0 into the table rows; dW0 / dUm / dIm by fact_expand_kernel
-            switch (DM) {  // factored path: dm in {8, ..., 128} (fact_mode)
+            switch (DM) {  // factored path: dm in {8, ..., 512} (fact_mode)
                 case 8: launch_scatter0<8>(a, Dcur, R, st); break;
                 case 16: launch_scatter0<16>(a, Dcur, R, st); break;
                 case 32: launch_scatter0<32>(a, Dcur, R, st); break;
                 case 64: launch_scatter0<64>(a, Dcur, R, st); break;
                 case 128: launch_scatter0<128>(a, Dcur, R, st); break;
+                case 256: launch_scatter0<256>(a, Dcur, R, st); break;
+                case 512: launch_scatter0<512>(a, Dcur, R, st); break;
                 default: return NCF_E_UNSUPPORTED;
+            }
+            if (DM > FACT_LDS_DM) {  // the expansion here, as GEMMs (fact_expand_kernel: dm <= 128)
+                const int U = lay.user_num, I = lay.item_num;
+                const int nbu = (U + GBM - 1) / GBM, nbi = (I + GBM - 1) / GBM;
+                hipLaunchKernelGGL(lyr_fact_dx_kernel, dim3((unsigned)(nbu + nbi), (unsigned)((DM + GBN - 1) / GBN)),
+                                   dim3(GNT), 0, st, lay, a.params, a.grads, Pj, nbu);
+                const int64_t chunk = 256;
+                const int zu = (int)((U + chunk - 1) / chunk), zi = (int)((I + chunk - 1) / chunk);
+                hipLaunchKernelGGL(lyr_fact_dw0_kernel,
+                                   dim3((unsigned)((DM + GBM - 1) / GBM), (unsigned)((DM + GBN - 1) / GBN),
+                                        (unsigned)(zu + zi)),
+                                   dim3(GNT), 0, st, a, zu, chunk);
+                if (hipMemcpyAsync(a.grads + lay.um, Pj, (size_t)U * DM * 4, hipMemcpyDeviceToDevice, st) !=
+                        hipSuccess ||
+                    hipMemcpyAsync(a.grads + lay.im, Pj + (int64_t)U * DM, (size_t)I * DM * 4,
+                                   hipMemcpyDeviceToDevice, st) != hipSuccess)
+                    return NCF_E_LAUNCH;
             }
             break;
         }

@@ -1046,10 +1046,11 @@ static bool fact_mode(const ncf_layout* lay) {
     if (lay->dropout > 0.f) return false;  // masks per row: layer 0 does not factor per entity
     if ((int64_t)lay->user_num + lay->item_num > FACT_MAX_ROWS) return false;
     const int dm = fact_dm(lay);
-    if (dm != 8 && dm != 16 && dm != 32 && dm != 64 && dm != 128) return false;  // fact_expand_kernel<DM>
+    const bool lds_dm = dm == 8 || dm == 16 || dm == 32 || dm == 64 || dm == 128;  // fact_expand_kernel<DM>
     const KernelEntry* e = train_fused(lay);
-    if (e) return e->train_fact != nullptr;
-    return lay->factor_num <= LYR_MAX_FACTOR;
+    if (e) return lds_dm && e->train_fact != nullptr;
+    // layered path: wider dm (256, 512) expanded with GEMMs (ncf_layered.hip lyr_fact_dx / dw0)
+    return (lds_dm || dm == 256 || dm == FACT_MAX_DM) && lay->factor_num <= LYR_MAX_FACTOR;
 }
 
 // Workgroups of the fused step = rows of the slab the reductions read.
@@ -1076,6 +1077,7 @@ static int fact_blocks(const ncf_layout* lay, int* nbu) {
 }
 
 static int64_t fact_partials_floats(const ncf_layout* lay) {
+    if (fact_dm(lay) > FACT_LDS_DM) return 0;  // W0 into the slab (the layered GEMM expansion)
     int nbu;
     const int64_t DM = (int64_t)lay->factor_num << (lay->num_layers - 1);
     return (int64_t)fact_blocks(lay, &nbu) * DM * DM;
@@ -1096,7 +1098,7 @@ static int reduce_rows(const ncf_layout* lay) { return train_fused(lay) ? slab_r
 static W0Part w0_part(const ncf_layout* lay, const void* workspace) {
     W0Part wp;
     memset(&wp, 0, sizeof(wp));
-    if (!fact_mode(lay)) return wp;
+    if (!fact_mode(lay) || fact_dm(lay) > FACT_LDS_DM) return wp;  // W0 from the slab
     wp.p = fact_partials(lay, const_cast<void*>(workspace));
     wp.nblk = fact_blocks(lay, &wp.nbu);
     wp.dm = lay->factor_num << (lay->num_layers - 1);
@@ -1107,6 +1109,7 @@ static W0Part w0_part(const ncf_layout* lay, const void* workspace) {
 static int launch_fact_expand(const ncf_layout* lay, const float* params, float* grads, float* partials,
                               hipStream_t st) {
     const int DM = lay->factor_num << (lay->num_layers - 1);
+    if (DM > FACT_LDS_DM) return NCF_OK;  // expanded by the layered path itself (lyr_run)
     const void* fe;
     int64_t lds;
     switch (DM) {

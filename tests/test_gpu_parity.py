@@ -220,7 +220,9 @@ def test_one_step_fact_boundary(U, I, fact):
                                         ("MLP", 32, 3, 8192), ("NeuMF-end", 16, 4, 8192),
                                         # forward-chain instantiations dm 16 / L 3, dm 8 / L 2, dm 128 / L 1
                                         ("NeuMF-end", 4, 3, 8192), ("MLP", 4, 2, 8192),
-                                        ("NeuMF-end", 128, 1, 8192)])
+                                        ("NeuMF-end", 128, 1, 8192),
+                                        # dm 512 / 256: expansion by GEMMs (lyr_fact_dx / dw0), W0 via the slab
+                                        ("NeuMF-end", 64, 4, 8192), ("MLP", 32, 4, 8192)])
 def test_one_step_layered_factored_layer0(mt, f, Lyr, B):
     """Layered path with the factored layer 0 (ABI 10: table projections through W0,
     per-row gather, D0 row sums expanded by fact_expand_kernel; dm = 128 for
