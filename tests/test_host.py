@@ -56,8 +56,12 @@ def test_abi_version_and_layout():
     dm = 64 * 8
     acts = 65536 * (dm + dm // 2 + dm // 4 + dm // 8) + 2 * 65536 * dm
     rows = L.hip().ncf_reduce_rows(ctypes.byref(lay))  # layered: slab rows the atomics spread over
-    assert 1 <= rows <= 16 and L.hip().ncf_fact_partials_bytes(ctypes.byref(lay)) == 0  # dm 512: per-row layer 0
-    assert acts * 4 <= ws <= (acts + rows * (lay.tower_len + 64) + 64 * 8) * 4
+    # dm 512: factored layer 0 expanded by GEMMs (W0 into the slab: no partials), the
+    # workspace adds the two tables' projections
+    assert L.hip().ncf_fact_mode(ctypes.byref(lay)) == 1
+    assert 1 <= rows <= 16 and L.hip().ncf_fact_partials_bytes(ctypes.byref(lay)) == 0
+    proj = (6041 + 3707) * dm
+    assert (acts + proj) * 4 <= ws <= (acts + proj + rows * (lay.tower_len + 64) + 64 * 10) * 4
     # NCF(32,3) at ml-1m: factored layer 0 on the layered path (ABI 10): the
     # workspace adds the dW0 partials and the two tables' projections
     lay = L.layout(6041, 3707, 32, 3, "NeuMF-end")
