@@ -10,7 +10,10 @@ namespace ncf {
 constexpr int LYR_MAX_FACTOR = 256;  // predict kernel: <= 4 features per lane
 // Factored layer 0: fact_expand_kernel (LDS-staged W0 half) up to this dm; wider
 // (256, 512) the layered path expands with GEMMs (lyr_fact_dx / lyr_fact_dw0).
-constexpr int FACT_LDS_DM = 128;
+#ifndef NCF_FACT_LDS_DM  // experiment switch: a smaller value takes the GEMM expansion from there up
+#define NCF_FACT_LDS_DM 128
+#endif
+constexpr int FACT_LDS_DM = NCF_FACT_LDS_DM;
 constexpr int FACT_MAX_DM = 512;
 
 static inline int64_t rup64(int64_t x) { return (x + 63) / 64 * 64; }

@@ -1509,6 +1509,28 @@ int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train, in
     return fl;
 }
 
+// The factored expansion as GEMMs (dm > FACT_LDS_DM, after the layer-0 scatter): dX
+// into the dead projection buffer, dW0 into the slab's W0 columns (both read G), then
+// dX copied over G.
+static int launch_gemm_expand(const LyrArgs& a, float* Pj, hipStream_t st) {
+    const ncf_layout& lay = a.lay;
+    const int DM = lay.factor_num << (lay.num_layers - 1);
+    const int U = lay.user_num, I = lay.item_num;
+    const int nbu = (U + GBM - 1) / GBM, nbi = (I + GBM - 1) / GBM;
+    hipLaunchKernelGGL(lyr_fact_dx_kernel, dim3((unsigned)(nbu + nbi), (unsigned)((DM + GBN - 1) / GBN)), dim3(GNT),
+                       0, st, lay, a.params, a.grads, Pj, nbu);
+    const int64_t chunk = 256;
+    const int zu = (int)((U + chunk - 1) / chunk), zi = (int)((I + chunk - 1) / chunk);
+    hipLaunchKernelGGL(lyr_fact_dw0_kernel,
+                       dim3((unsigned)((DM + GBM - 1) / GBM), (unsigned)((DM + GBN - 1) / GBN), (unsigned)(zu + zi)),
+                       dim3(GNT), 0, st, a, zu, chunk);
+    if (hipMemcpyAsync(a.grads + lay.um, Pj, (size_t)U * DM * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(a.grads + lay.im, Pj + (int64_t)U * DM, (size_t)I * DM * 4, hipMemcpyDeviceToDevice, st) !=
+            hipSuccess)
+        return NCF_E_LAUNCH;
+    return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
+}
+
 int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st) {
     LyrArgs a = a0;
     const ncf_layout& lay = a.lay;
@@ -1637,6 +1659,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             default: return NCF_E_UNSUPPORTED;
         }
 #undef NCF_L0
+        if (DM > FACT_LDS_DM && launch_gemm_expand(a, Pj, st) != NCF_OK) return NCF_E_LAUNCH;
         return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
     }
     int G = 1;
@@ -1678,23 +1701,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
                 case 512: launch_scatter0<512>(a, Dcur, R, st); break;
                 default: return NCF_E_UNSUPPORTED;
             }
-            if (DM > FACT_LDS_DM) {  // the expansion here, as GEMMs (fact_expand_kernel: dm <= 128)
-                const int U = lay.user_num, I = lay.item_num;
-                const int nbu = (U + GBM - 1) / GBM, nbi = (I + GBM - 1) / GBM;
-                hipLaunchKernelGGL(lyr_fact_dx_kernel, dim3((unsigned)(nbu + nbi), (unsigned)((DM + GBN - 1) / GBN)),
-                                   dim3(GNT), 0, st, lay, a.params, a.grads, Pj, nbu);
-                const int64_t chunk = 256;
-                const int zu = (int)((U + chunk - 1) / chunk), zi = (int)((I + chunk - 1) / chunk);
-                hipLaunchKernelGGL(lyr_fact_dw0_kernel,
-                                   dim3((unsigned)((DM + GBM - 1) / GBM), (unsigned)((DM + GBN - 1) / GBN),
-                                        (unsigned)(zu + zi)),
-                                   dim3(GNT), 0, st, a, zu, chunk);
-                if (hipMemcpyAsync(a.grads + lay.um, Pj, (size_t)U * DM * 4, hipMemcpyDeviceToDevice, st) !=
-                        hipSuccess ||
-                    hipMemcpyAsync(a.grads + lay.im, Pj + (int64_t)U * DM, (size_t)I * DM * 4,
-                                   hipMemcpyDeviceToDevice, st) != hipSuccess)
-                    return NCF_E_LAUNCH;
-            }
+            if (DM > FACT_LDS_DM && launch_gemm_expand(a, Pj, st) != NCF_OK) return NCF_E_LAUNCH;
             break;
         }
         // weight gradient: split the rows so the launch has ~512 blocks
