@@ -239,12 +239,15 @@ def test_one_step_layered_factored_layer0(mt, f, Lyr, B):
     assert not _fact_mode(lay)
 
 
-def test_engine_layered_factored_trajectory_vs_oracle():
-    """NCF(32,3) (the CLI default shape) on the factored layered path at ml-1m ids:
-    6 engine Adam steps of 8,192 rows (hipGraph) free-running
-    (_assert_trajectory_close), then every step teacher-forced."""
-    T, B = 6, 8192
-    ref, m, eng = _engine_for("NeuMF-end", 32, 3, 6041, 3707, 23)
+@pytest.mark.parametrize("f,Lyr,T", [(32, 3, 6), (64, 4, 4)])
+def test_engine_layered_factored_trajectory_vs_oracle(f, Lyr, T):
+    """NCF(32,3) (the CLI default shape: step chain, LDS expansion) and NCF(64,4) (the
+    stress shape: dm 512, GEMM expansion, W0 reduced from the slab by
+    ncf_reduce_adam_step) on the factored layered path at ml-1m ids: T engine Adam
+    steps of 8,192 rows (hipGraph) free-running (_assert_trajectory_close), then every
+    step teacher-forced."""
+    B = 8192
+    ref, m, eng = _engine_for("NeuMF-end", f, Lyr, 6041, 3707, 23)
     rng = np.random.default_rng(47)
     users = rng.integers(0, 6041, (T, B))
     items = np.minimum(rng.zipf(1.3, (T, B)) - 1, 3706)
