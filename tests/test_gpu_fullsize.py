@@ -8,15 +8,17 @@ seeds and the same init:
   * negatives bit-exact (datasets.py:53-69), batch membership by construction
     (the same permutation, train_neumf.py:55,106);
   * per-step loss of the first 100 steps (all 76 at bs 65,536) to rtol 1e-5,
-    free-running (train_neumf.py:112-115);
+    free-running (train_neumf.py:112-115; NCF(64,4): 1e-5 for the first 10, 1e-4
+    after, see late_rtol);
   * the first steps teacher-forced from the oracle's state (every parameter after
     the step, test_gpu_parity._teacher_forced_steps);
   * the epoch's mean loss to 1e-3 relative, and HR@10 / NDCG@10 of metrics()
     (metrics.py:4-25) on the leave-one-out test set within 0.01 of the oracle's.
 
 Configs: C2 (NCF(8,3), bs 1,024: tuned launch shape, per-row layer 0), C3
-(NCF(16,3), bs 65,536: fused kernel, factored layer 0) and the reference's CLI
-default NCF(32,3) at bs 65,536 (layered path, step chain, user order)."""
+(NCF(16,3), bs 65,536: fused kernel, factored layer 0), the reference's CLI
+default NCF(32,3) at bs 65,536 (layered path, step chain, user order) and the stress
+NCF(64,4) (layered path, dm-512 factored layer 0 with the GEMM expansion)."""
 import numpy as np
 import pytest
 import torch
@@ -39,9 +41,13 @@ def _data():
     return ds, train, test, tu, ti
 
 
-@pytest.mark.parametrize("name,f,L,B,forced", [("c2", 8, 3, 1024, 20), ("c3", 16, 3, 65536, 6),
-                                                ("cli", 32, 3, 65536, 4)])
-def test_full_epoch_vs_oracle(name, f, L, B, forced):
+# late_rtol: free-running loss tolerance past the first 10 steps.  NCF(64,4) (6.4M
+# parameters) turns at step 10 (loss 0.457 -> 0.475) and the two fp32 trajectories part
+# there to ~4e-5 relative; every step is held to 1e-5 teacher-forced.
+@pytest.mark.parametrize("name,f,L,B,forced,late_rtol", [("c2", 8, 3, 1024, 20, 1e-5), ("c3", 16, 3, 65536, 6, 1e-5),
+                                                          ("cli", 32, 3, 65536, 4, 1e-5),
+                                                          ("stress", 64, 4, 65536, 3, 1e-4)])
+def test_full_epoch_vs_oracle(name, f, L, B, forced, late_rtol):
     from torch.utils.data import DataLoader
     from ncf_amd.models import NCF
     from ncf_amd.trainer import Trainer
@@ -90,7 +96,8 @@ def test_full_epoch_vs_oracle(name, f, L, B, forced):
     hr, ndcg = float(np.mean(HR)), float(np.mean(NDCG))
 
     k = min(100, nb)
-    np.testing.assert_allclose(got_losses[:k], losses[:k], rtol=1e-5, err_msg=f"{name}: first {k} step losses")
+    np.testing.assert_allclose(got_losses[:10], losses[:10], rtol=1e-5, err_msg=f"{name}: first 10 step losses")
+    np.testing.assert_allclose(got_losses[:k], losses[:k], rtol=late_rtol, err_msg=f"{name}: first {k} step losses")
     assert abs(got_losses.mean() - losses.mean()) <= 1e-3 * losses.mean(), (got_losses.mean(), losses.mean())
     assert abs(h["loss"] - losses.mean()) <= 1e-3 * losses.mean()
     assert abs(h["hr"] - hr) <= 0.01 and abs(h["ndcg"] - ndcg) <= 0.01, (name, h, hr, ndcg)
