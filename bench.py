@@ -372,6 +372,28 @@ def main():
     losses = eng.epoch_losses()
     final_loss = float(losses[(eng.state_step() - 1) % eng.num_batches])
 
+    # ---- the same number of steps on the current epoch stream, reused (no fresh
+    # negatives / permutation: the step kernel wraps to the epoch's first batch): the
+    # device + exchange rate beside `value`, which the sequential host sampler bounds
+    # once an epoch is only a few steps long (N >= 4 at 65,536 rows per GPU)
+    if world > 1:
+        torch.distributed.barrier(group=group, device_ids=[local])
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    eng.run(args.steps, use_graph=use_graph)
+    torch.cuda.synchronize(dev)
+    dt_frozen = time.perf_counter() - t0
+    if world > 1:
+        torch.distributed.barrier(group=group, device_ids=[local])
+        t = torch.tensor([dt_frozen], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=group)
+        dt_frozen = float(t.item())
+    frozen = {"value": rows / dt_frozen, "ms_per_step": dt_frozen / args.steps * 1e3,
+              "note": "the same steps with the last epoch stream reused (no new negatives or permutation): "
+                      "device + exchange rate; `value` times fresh epochs, whose host sampler (sequential in "
+                      "the reference's NumPy stream, ~3 ms per ml-1m epoch) bounds it once an epoch is only a "
+                      "few global steps long"}
+
     # ---- per-kernel live timing (HIP events on the launch stream) -------------
     kt = eng.time_kernels(args.kernel_steps)
     pipe_ms = []
@@ -478,6 +500,7 @@ def main():
             "quality": {"HR@10": hr10, "NDCG@10": ndcg10, "epochs_trained": round(eng.state_step() / eng.num_batches, 2),
                         "last_batch_loss": final_loss},
             "e2e": e2e,
+            "frozen_epoch": frozen,
             "cpu_baseline": cpu,
             "setup_s": {"data+first_epoch": round(t_data, 2)},
         }
