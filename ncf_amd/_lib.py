@@ -113,6 +113,13 @@ _SAMPLER_PROTOS = {
     "ncf_mt_seed": (None, [ctypes.c_uint32, c_vp, c_vp]),
     "ncf_sampler_sample": (c_i64, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "ncf_mt_words": (None, [c_vp, c_vp, c_i64, c_vp]),
+    "ncf_sampler_create2": (c_vp, [c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_i32]),
+    "ncf_sampler_set_threads": (ctypes.c_int, [c_vp, c_i32]),
+    "ncf_sampler_stats": (ctypes.c_int, [c_vp, c_vp, c_i32]),
+    "ncf_mt_jump": (ctypes.c_int, [c_vp, c_i64]),
+    "ncf_words_create": (c_vp, [c_i32]),
+    "ncf_words_destroy": (None, [c_vp]),
+    "ncf_words_fill": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_vp]),
 }
 
 _lock = threading.Lock()

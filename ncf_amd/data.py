@@ -31,17 +31,43 @@ def _state_arrays():
 
 
 class HostSampler:
-    """Membership index over the training positives + bit-exact legacy-MT19937
-    negative draws (C++, libncf_sampler.so)."""
+    """Membership index + bit-exact legacy-MT19937 negative draws (C++,
+    libncf_sampler.so).  The runs come from the positives in file order
+    (datasets.py:57: ``for x in self.features_ps``), membership from
+    ``mem_users / mem_items`` (the keys of ``train_mat``, datasets.py:61), which
+    default to the positives.  ``threads``: the parallel pass's pool (default
+    NCF_SAMPLER_THREADS or min(16, 3/4 of the CPUs); 1 = the sequential pass)."""
 
-    def __init__(self, pos_users, pos_items, num_users, num_items):
+    def __init__(self, pos_users, pos_items, num_users, num_items, mem_users=None, mem_items=None, threads=None):
         self.pos_users = np.ascontiguousarray(pos_users, dtype=np.int32)
         self.pos_items = np.ascontiguousarray(pos_items, dtype=np.int32)
-        self._h = L.sampler_lib().ncf_sampler_create(self.pos_users.ctypes.data, self.pos_items.ctypes.data,
-                                                     len(self.pos_users), int(num_users), int(num_items))
+        if mem_users is None:
+            mem_users, mem_items = self.pos_users, self.pos_items
+        self.mem_users = np.ascontiguousarray(mem_users, dtype=np.int32)
+        self.mem_items = np.ascontiguousarray(mem_items, dtype=np.int32)
+        self._h = L.sampler_lib().ncf_sampler_create2(self.pos_users.ctypes.data, len(self.pos_users),
+                                                      self.mem_users.ctypes.data, self.mem_items.ctypes.data,
+                                                      len(self.mem_users), int(num_users), int(num_items))
         if not self._h:
-            raise RuntimeError("ncf_sampler_create failed")
+            raise RuntimeError("ncf_sampler_create2 failed")
         self.num_users, self.num_items = int(num_users), int(num_items)
+        self.set_threads(sampler_threads() if threads is None else threads)
+
+    def set_threads(self, threads):
+        if L.sampler_lib().ncf_sampler_set_threads(self._h, int(threads)) != 0:
+            raise ValueError(f"sampler threads {threads}")
+        self.threads = int(threads)
+
+    def stats(self):
+        """(parallel passes, sequential passes, runs walked directly, parallel passes
+        redone sequentially, threads, blocks, ns: words / walk / end state / chain,
+        window bits) of this sampler."""
+        import ctypes
+        out = (ctypes.c_int64 * 11)()
+        L.sampler_lib().ncf_sampler_stats(self._h, out, 11)
+        keys = ("parallel", "sequential", "run_fallbacks", "epoch_fallbacks", "threads", "blocks",
+                "words_ns", "walk_ns", "end_ns", "chain_ns", "window_bits")
+        return dict(zip(keys, list(out)))
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -69,11 +95,29 @@ class HostSampler:
             raise ValueError("out: contiguous int32 of at least n_pos * num_ng")
         words = L.sampler_lib().ncf_sampler_sample(self._h, int(num_item), int(num_ng), key.ctypes.data,
                                                    pos.ctypes.data, out.ctypes.data)
+        if words == -2:
+            # the reference's `while (u, j) in train_mat` never ends for a user who owns
+            # every item in [0, num_item): refuse instead of hanging
+            raise RuntimeError("ng_sample: a user has every item as a positive (the reference loops forever)")
         if words < 0:
             raise RuntimeError("ncf_sampler_sample: bad arguments")
         if use_global:
-            np.random.set_state((st[0], key, int(pos[0]), 0, 0.0))
+            np.random.set_state((st[0], key, int(pos[0]), st[3], st[4]))  # the cached Gaussian stays
         return out
+
+
+def sampler_threads():
+    """Threads of a host sampler pool: NCF_SAMPLER_THREADS, else min(16, 3/4 of the
+    CPUs this process may run on) -- a GPU box grants 16 CPUs per GPU."""
+    import os
+    v = os.environ.get("NCF_SAMPLER_THREADS")
+    if v:
+        return max(1, int(v))
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, (3 * n) // 4))
 
 
 def _membership_from(train_mat, features):
@@ -151,21 +195,18 @@ class NCFData(data.Dataset):
         return self._ps_u, self._ps_i, self.labels.astype(np.float32)
 
     def _get_sampler(self):
+        """The sampler over this data set: runs from the positives (file order),
+        membership from ``train_mat``'s keys (``(u, j) in train_mat``,
+        datasets.py:61) -- any dok_matrix, duplicates or extra pairs included --
+        or from the positives when ``train_mat`` is None."""
         if self._sampler is None:
             mem = _membership_from(self.train_mat, None)
-            n_users = int(max(self._ps_u.max(initial=0) + 1, mem[2][0] if mem else 0))
-            n_items = int(max(self.num_item, mem[2][1] if mem else 0))
-            if mem is None or (len(mem[0]) == len(self._ps_u)):
-                # train_mat == the training positives (every reference call site)
+            n_users = int(max(self._ps_u.max(initial=0) + 1, mem[2][0] if mem else 0, 1))
+            n_items = int(max(self.num_item, mem[2][1] if mem else 0, 1))
+            if mem is None:
                 self._sampler = HostSampler(self._ps_u, self._ps_i, n_users, n_items)
-                if mem is not None and len(mem[0]):
-                    # guard: same set of pairs
-                    a = np.sort(self._ps_u.astype(np.int64) * n_items + self._ps_i)
-                    b = np.sort(mem[0].astype(np.int64) * n_items + mem[1])
-                    if not np.array_equal(np.unique(a), np.unique(b)):
-                        raise NotImplementedError("train_mat differs from the training positives")
             else:
-                raise NotImplementedError("train_mat differs from the training positives")
+                self._sampler = HostSampler(self._ps_u, self._ps_i, n_users, n_items, mem[0], mem[1])
         return self._sampler
 
     def ng_sample(self):

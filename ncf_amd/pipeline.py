@@ -44,21 +44,50 @@ from .data import epoch_permutation_seed
 
 
 def _mt_state():
+    """(key, pos, (has_gauss, cached_gaussian)) of numpy's global legacy generator."""
     st = np.random.get_state(legacy=True)
     if st[0] != "MT19937":
         raise RuntimeError("numpy global generator is not MT19937")
-    return np.ascontiguousarray(st[1], dtype=np.uint32).copy(), int(st[2])
+    return np.ascontiguousarray(st[1], dtype=np.uint32).copy(), int(st[2]), (int(st[3]), float(st[4]))
 
 
-def torch_words(seed, n, out):
+class WordsGen:
+    """Parallel MT19937 word generator (libncf_sampler.so ncf_words_fill: chunks of
+    the stream on `threads` host threads, each from the state jumped to its first
+    word; same words as the sequential ncf_mt_words)."""
+
+    def __init__(self, threads=None):
+        from .data import sampler_threads
+        self.threads = sampler_threads() if threads is None else int(threads)
+        self._h = L.sampler_lib().ncf_words_create(self.threads)
+        if not self._h:
+            raise RuntimeError("ncf_words_create failed")
+
+    def fill(self, key, pos, n, out):
+        if L.sampler_lib().ncf_words_fill(self._h, key.ctypes.data, pos.ctypes.data, int(n), out.ctypes.data) != 0:
+            raise RuntimeError("ncf_words_fill: bad arguments")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                L.sampler_lib().ncf_words_destroy(h)
+            except Exception:
+                pass
+
+
+def torch_words(seed, n, out, gen=None):
     """The first n 32-bit words of torch.Generator().manual_seed(seed) (MT19937 on
-    the low 32 bits of the seed) into out (uint32)."""
+    the low 32 bits of the seed) into out (uint32); `gen`: a WordsGen (parallel)."""
     key = np.empty(624, dtype=np.uint32)
     pos = np.empty(1, dtype=np.int32)
     lib = L.sampler_lib()
     lib.ncf_mt_seed(int(seed) & 0xFFFFFFFF, key.ctypes.data, pos.ctypes.data)
     if n > 0:
-        lib.ncf_mt_words(key.ctypes.data, pos.ctypes.data, int(n), out.ctypes.data)
+        if gen is not None:
+            gen.fill(key, pos, n, out)
+        else:
+            lib.ncf_mt_words(key.ctypes.data, pos.ctypes.data, int(n), out.ctypes.data)
 
 
 class _Staged:
@@ -127,6 +156,7 @@ class EpochPipeline:
         self.copy_stream = torch.cuda.Stream(device=dev)
         self.side_stream = torch.cuda.Stream(device=dev)
         self.stats = {"epochs": 0, "prefetch_hits": 0}
+        self._wordgen = WordsGen()
         self.events = None  # (start, rows+perm built, grouped) of the last epoch
 
     # ---------------------------------------------------------------- host part
@@ -142,17 +172,11 @@ class EpochPipeline:
         t_all = time.perf_counter()
         neg = self._neg_host[slot].numpy()
         words = self._words_host[slot].numpy().view(np.uint32)
-
-        def draw_words():
-            t0 = time.perf_counter()
-            torch_words(s.seed, self.n - 1, words[: self.n - 1])
-            s.host_ms["words"] = (time.perf_counter() - t0) * 1e3
-
         prev, self._uploaded[slot] = self._uploaded[slot], None
         if prev is not None:
             prev.synchronize()  # the slot's pinned buffers are no longer being read
-        t = threading.Thread(target=draw_words)
-        t.start()
+        # the negatives, then the permutation words, each on its own pool of host
+        # threads (the next epoch's negatives wait only for the negatives)
         try:
             t0 = time.perf_counter()
             if self.S == 0:
@@ -164,7 +188,9 @@ class EpochPipeline:
             s.host_ms["sample"] = (time.perf_counter() - t0) * 1e3
         finally:
             s.sampled.set()
-            t.join()
+        t0 = time.perf_counter()
+        torch_words(s.seed, self.n - 1, words[: self.n - 1], self._wordgen)
+        s.host_ms["words"] = (time.perf_counter() - t0) * 1e3
         with torch.cuda.stream(self.copy_stream):
             if self._free[slot] is not None:
                 self.copy_stream.wait_event(self._free[slot])  # the slot's device buffers
@@ -263,7 +289,7 @@ class EpochPipeline:
         earlier epochs trained: the current stream only waits for it.  The result
         is one of depth + 1 rotating buffers, valid for `depth` further calls."""
         t_enter = time.perf_counter()
-        key, pos = _mt_state()
+        key, pos, gauss = _mt_state()
         seed = epoch_permutation_seed()  # the DataLoader's two draws
         staged = self._pending.popleft() if self._pending else None
         if staged is not None:
@@ -291,7 +317,8 @@ class EpochPipeline:
                 staged.enqueued.set()
             # the builds share rows / perm / workspaces: later side-stream builds after this one
             self.side_stream.wait_stream(cur)
-        np.random.set_state(("MT19937", staged.end_key, staged.end_pos, 0, 0.0))
+        # randint draws leave the cached Gaussian of the legacy state alone
+        np.random.set_state(("MT19937", staged.end_key, staged.end_pos, gauss[0], gauss[1]))
         cur.wait_event(staged.ready)
         # everything that read the previous epoch's slot (its steps; a build on this
         # stream) is enqueued before this point
