@@ -5,25 +5,29 @@ Workload (BASELINE.json metric "training interactions/sec + HR@10, NeuMF
 factors=64 ml-1m"): NCF(6041, 3707, factor_num=16,
 num_layers=3, 'NeuMF-end') -- 64-wide MLP embeddings, tower [128,64,32,16] --
 on ml-1m-shaped synthetic data (994,169 positives, 4 sampled negatives each),
-65,536 rows per GPU per step, Adam lr 1e-3.
+global batch 65,536 (8,192 per GPU at 8 GPUs), Adam lr 1e-3.
 
 A "step" = fused fwd+loss+bwd kernel (+ the factored layer-0 expansion), tower-grad
 reduction, (RCCL gradient exchange when N > 1), dense Adam -- the whole optimizer
 step of scripts/train_neumf.py:111-115, captured into hipGraphs and replayed.
-Every epoch inside the timed region is a fresh epoch of the reference loop: new
-negatives (NCFData.ng_sample, bit-exact; host sampler, prefetched on a host thread
-while the previous epoch trains) and a new DataLoader permutation (bit-exact
-torch.randperm, on the device), packed, shuffled and grouped on the device
-(ncf_amd.pipeline).  The data set itself is resident in HBM before the timed
-region.  Per-GPU work is fixed (65,536 rows/GPU/step), so scaling is weak and
-value = all ranks' rows / max-over-ranks time.
+The timed region is whole epochs (--steps rounded up): every epoch in it is a
+fresh epoch of the reference loop -- new negatives (NCFData.ng_sample, bit-exact;
+the parallel host sampler, prefetched while the previous epoch trains) and a new
+DataLoader permutation (bit-exact torch.randperm, on the device), packed,
+shuffled and grouped on the device (ncf_amd.pipeline).  The data set itself is
+resident in HBM before the timed region.  The global batch is the reference's
+batch size at every N (strong scaling); value = rows of the timed epochs /
+max-over-ranks time.  At N > 1 `weak_scaling` also times the per-GPU batch held
+at the single-GPU size.
 
 Also reported: `e2e` -- Trainer.fit (the scripts' loop: epochs + metrics() per
 epoch) at the same config, rows per epoch / epoch wall time; `cpu_baseline` -- the
-oracle (reference model restated on torch CPU ops) on the host cores.
+oracle (reference model restated on torch CPU ops) on the host cores, in a child
+process.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, RCCL).
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 either under
+torch.distributed.run (one process per GPU, RCCL) or directly, in which case the
+script spawns its N ranks itself before any GPU call.
 """
 from __future__ import annotations
 
@@ -31,6 +35,7 @@ import argparse
 import glob
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -41,7 +46,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {
-    # name: (dataset shape, factor_num, num_layers, rows per GPU per step)
+    # name: (dataset shape, factor_num, num_layers, global batch = the reference's batch_size)
     "c3": ("ml-1m", 16, 3, 65536),     # headline: NeuMF-64 (MLP [128,64,32,16])
     "c2": ("ml-1m", 8, 3, 1024),       # NeuMF [64,32,16,8], bs 1024
     "c4": ("ml-20m", 16, 3, 65536),    # ml-20m shape
@@ -172,53 +177,129 @@ def host_facts():
     return {"nproc": os.cpu_count(), "cpus_available": avail, "cpu_model": model}
 
 
-def cpu_baseline(cfg, ds, batch, seconds, threads):
-    """The oracle (oracle/ncf_oracle.py: the reference model restated on stock
-    PyTorch CPU ops + torch.optim.Adam) timed on the host cores: (i) steady-state
-    Adam steps on `batch`-row batches of the real epoch stream for ~`seconds`, and
-    (ii) a script-equivalent epoch -- ng_sample (the oracle's C restatement),
-    the DataLoader permutation, packing, then every step of the epoch -- timed on
-    the first batches and extrapolated to the epoch's batch count."""
+class _RefLikeDataset:
+    """Per-sample view of an epoch like the reference NCFData (datasets.py:71-83):
+    __getitem__ returns python ints, batched by the stock DataLoader's collate."""
+
+    def __init__(self, users, items, labels):
+        self.u, self.i, self.y = users, items, labels
+
+    def __len__(self):
+        return len(self.u)
+
+    def __getitem__(self, idx):
+        return int(self.u[idx]), int(self.i[idx]), int(self.y[idx])
+
+
+def _oracle_steps(cfg, U, I, batch, seconds, threads, users=None, items=None, labels=None, seed=0):
+    """Adam steps of the oracle model (the reference NCF restated on stock torch CPU
+    ops + torch.optim.Adam) on `batch`-row batches for ~`seconds`: rows/s.  Batches
+    come from the given epoch stream, or are random ids in the model's id space."""
     from oracle import ncf_oracle as O
     shape, f, L, _ = CONFIGS[cfg]
-    U, I = ds["user_num"], ds["item_num"]
     torch.set_num_threads(threads)
-    torch.manual_seed(0)
-    m = O.OracleNCF(U, I, f, L, 0.0, "NeuMF-end")
+    torch.manual_seed(seed)
+    m = O.OracleNCF(U, I, f, L, 0.0, MODEL.get(cfg, "NeuMF-end"))
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
-    pu, pi = ds["train_users"], ds["train_items"]
-    t0 = time.perf_counter()
-    neg = O.ng_sample(pu, pi, I, 4, 0)
-    t_sample = time.perf_counter() - t0
-    users = np.concatenate([pu, np.repeat(pu, 4)])
-    items = np.concatenate([pi, neg])
-    labels = np.concatenate([np.ones(len(pu), np.int64), np.zeros(len(neg), np.int64)])
-    t0 = time.perf_counter()
-    perm = O.epoch_order(len(users), torch.Generator().manual_seed(0))
-    t_perm = time.perf_counter() - t0
-    nb = (len(users) + batch - 1) // batch
-    bat = lambda b: (users[perm[b * batch:(b + 1) * batch]], items[perm[b * batch:(b + 1) * batch]],  # noqa: E731
-                     labels[perm[b * batch:(b + 1) * batch]])
+    rng = np.random.default_rng(seed)
+    if users is None:
+        n = batch * 8
+        users, items = rng.integers(1, U, n), rng.integers(1, I, n)
+        labels = (rng.random(n) < 0.2).astype(np.int64)
+    nb = max(1, len(users) // batch)
+    bat = lambda b: (users[b * batch:(b + 1) * batch], items[b * batch:(b + 1) * batch],  # noqa: E731
+                     labels[b * batch:(b + 1) * batch])
     O.train_steps(m, opt, *[[x] for x in bat(0)])  # warm-up
     steps, t0 = 0, time.perf_counter()
     while True:
-        u, i, y = bat(1 + steps % (nb - 1)) if nb > 1 else bat(0)
+        u, i, y = bat((1 + steps) % nb)
         O.train_steps(m, opt, [u], [i], [y])
         steps += 1
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    step_s = el / steps
-    epoch_s = t_sample + t_perm + nb * step_s
-    return {"value": steps * batch / el, "unit": "interactions/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} x {batch}-row Adam steps of the oracle on the epoch stream of {cfg.upper()} "
-                      f"(reference NCF restated on torch CPU ops, NCF({U},{I},{f},{L})), {el:.1f} s on "
-                      f"{threads} threads",
-            "script_epoch_s": epoch_s,
-            "script_epoch_note": f"ng_sample {t_sample:.2f} s + DataLoader permutation {t_perm:.2f} s + "
-                                 f"{nb} steps x {step_s * 1e3:.1f} ms (steps timed on {steps}, extrapolated)",
-            "script_epoch_interactions_per_s": len(users) / epoch_s,
-            **host_facts(), "torch_threads": threads}
+    return {"value": steps * batch / el, "steps": steps, "seconds": round(el, 2), "threads": threads,
+            "ms_per_step": el / steps * 1e3}
+
+
+def cpu_baseline(cfg, seconds, script_epoch=True):
+    """BASELINE.md section 3 on the host cores (run in a child process that never
+    touches the GPU): the oracle -- the reference model restated on stock PyTorch CPU
+    ops + torch.optim.Adam, `kind` "port" -- timed
+      * step-only on the config's epoch stream at os.cpu_count() threads and at 16;
+      * step-only at C2 and C4 shapes (random ids) at 16 threads;
+      * a script-equivalent epoch (train_neumf.py:98-131): ng_sample (the oracle's
+        C restatement), the stock DataLoader(shuffle=True, num_workers=4) over a
+        per-sample dataset, zero_grad/forward/BCE/backward/Adam per batch, and the
+        metrics() pass (forward over the test candidates + HR/NDCG), at 16 threads."""
+    from oracle import ncf_oracle as O
+    shape, f, L, batch = CONFIGS[cfg]
+    ds, _ = make_train_data(cfg)
+    U, I = ds["user_num"], ds["item_num"]
+    pu, pi = ds["train_users"], ds["train_items"]
+    facts = host_facts()
+    t0 = time.perf_counter()
+    neg = O.ng_sample(pu, pi, I, 4, 0)
+    t_sample = time.perf_counter() - t0
+    users = np.concatenate([pu, np.repeat(pu, 4)]).astype(np.int64)
+    items = np.concatenate([pi, neg]).astype(np.int64)
+    labels = np.concatenate([np.ones(len(pu), np.int64), np.zeros(len(neg), np.int64)])
+    perm = O.epoch_order(len(users), torch.Generator().manual_seed(0))
+    su, si, sy = users[perm], items[perm], labels[perm]
+    threads_all = facts["nproc"]
+    out = {"unit": "interactions/s", "kind": "port", "cores": 16,
+           "sample": f"{cfg.upper()} step-only: {batch}-row Adam steps of the oracle NCF({U},{I},{f},{L}) on the "
+                     f"shuffled epoch stream, ~{seconds:.0f} s each at 16 threads (value) and at os.cpu_count() "
+                     f"threads; C2/C4-shape step-only and one script-equivalent epoch beside it",
+           **facts}
+    r16 = _oracle_steps(cfg, U, I, batch, seconds, 16, su, si, sy)
+    out["value"] = r16["value"]
+    out["step_only_16_threads"] = r16
+    out["step_only_all_threads"] = _oracle_steps(cfg, U, I, batch, seconds, threads_all, su, si, sy)
+    out["c2_step_only_16_threads"] = _oracle_steps("c2", 6041, 3707, 1024, seconds / 3, 16)
+    out["c4_step_only_16_threads"] = _oracle_steps("c4", 138494, 26745, 65536, seconds / 3, 16)
+    if script_epoch:
+        from torch.utils.data import DataLoader
+        torch.set_num_threads(16)
+        torch.manual_seed(0)
+        m = O.OracleNCF(U, I, f, L, 0.0, MODEL.get(cfg, "NeuMF-end"))
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        t0 = time.perf_counter()
+        neg = O.ng_sample(pu, pi, I, 4, 1)
+        items_e = np.concatenate([pi, neg]).astype(np.int64)
+        loader = DataLoader(_RefLikeDataset(users, items_e, labels), batch_size=batch, shuffle=True, num_workers=4)
+        t_loop = time.perf_counter()
+        nb = 0
+        for u, i, y in loader:
+            opt.zero_grad()
+            loss = O.bce_mean(m(u, i), y)
+            loss.backward()
+            opt.step()
+            nb += 1
+        t_eval = time.perf_counter()
+        tu = np.repeat(ds["test_users"], 100).astype(np.int64)
+        ti = np.concatenate([ds["test_items"][:, None], ds["test_negatives"]], 1).reshape(-1).astype(np.int64)
+        with torch.no_grad():
+            lg = m(torch.from_numpy(tu), torch.from_numpy(ti)).numpy()
+        HR, _ = O.metrics_np(lg, ti, 100, 10)
+        t1 = time.perf_counter()
+        out["script_epoch"] = {"seconds": t1 - t0, "interactions_per_s": len(users) / (t1 - t0),
+                               "ng_sample_s": t_loop - t0, "train_loop_s": t_eval - t_loop, "metrics_s": t1 - t_eval,
+                               "batches": nb, "HR@10": float(np.mean(HR)), "threads": 16, "num_workers": 4}
+    out["ng_sample_s"] = t_sample
+    return out
+
+
+def cpu_baseline_child(cfg, seconds, script_epoch=True):
+    """Run cpu_baseline in a child process (no HIP context: the DataLoader's worker
+    processes fork from it) and return its JSON."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--config", cfg,
+           "--cpu-seconds", str(seconds)] + ([] if script_epoch else ["--no-script-epoch"])
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=900)
+    if r.returncode != 0:
+        return {"error": r.stderr[-2000:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def make_train_data(cfg, seed=0):
@@ -278,7 +359,7 @@ def e2e_fit(cfg, ds, dev, epochs):
     from torch.utils.data import DataLoader
     from ncf_amd.data import NCFData
     from ncf_amd.trainer import Trainer
-    shape, f, nl, per_gpu = CONFIGS[cfg]
+    shape, f, nl, batch = CONFIGS[cfg]
     U, I = ds["user_num"], ds["item_num"]
     np.random.seed(1)
     torch.manual_seed(1)
@@ -287,7 +368,7 @@ def e2e_fit(cfg, ds, dev, epochs):
     tu = np.repeat(ds["test_users"], 100)
     ti = np.concatenate([ds["test_items"][:, None], ds["test_negatives"]], 1).reshape(-1)
     test = NCFData(np.stack([tu, ti], 1), I, None, 0, False)
-    tr = Trainer(model, train, DataLoader(test, batch_size=100, shuffle=False), batch_size=per_gpu, lr=1e-3,
+    tr = Trainer(model, train, DataLoader(test, batch_size=100, shuffle=False), batch_size=batch, lr=1e-3,
                  top_k=10, device=dev, verbose=False, distill=dist)
     tr.fit(1)  # graph capture, prefetch start-up
     torch.cuda.synchronize(dev)
@@ -297,7 +378,7 @@ def e2e_fit(cfg, ds, dev, epochs):
     wall = time.perf_counter() - t0
     n = len(train)
     return {"value": epochs * n / wall, "unit": "interactions/s", "wall_s": wall,
-            "epoch_device_s": [h["time"] for h in tr.history[1:]], "rows_per_epoch": n, "epochs": epochs,
+            "epoch_device_s": [h["device_time"] for h in tr.history[1:]], "rows_per_epoch": n, "epochs": epochs,
             "HR@10": [round(h["hr"], 4) for h in tr.history],
             "note": "wall clock of Trainer.fit(epochs) (per epoch: fresh negatives and permutation, the "
                     "steps, metrics() over the leave-one-out test set, the printed-line readback), after "
@@ -308,26 +389,206 @@ def e2e_fit(cfg, ds, dev, epochs):
             if tr._pipe is not None else None}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(argv, n):
+    """`bench.py --gpus N` without a launcher: N child processes of this script, one
+    per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR 127.0.0.1 / MASTER_PORT),
+    started before this process touches any GPU; rank 0's stdout is the JSON line.
+    If a rank fails the others are stopped.  Returns the worst exit code."""
+    import signal
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL, start_new_session=True))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in live:  # a failed rank: the others would wait in a collective forever
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except OSError:
+                        pass
+        time.sleep(0.05)
+    return rc
+
+
+def _max_over_ranks(x, group, dev):
+    if group is None:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def _barrier(group, dev):
+    if group is not None:
+        import torch.distributed as dist
+        if dev.type == "cuda":
+            dist.barrier(group=group, device_ids=[dev.index])
+        else:
+            dist.barrier(group=group)
+
+
+def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup, use_graph):
+    """Warm-up, then whole fresh epochs timed (>= `steps` optimizer steps, rounded up
+    to whole epochs of `global_batch`-row global batches: every epoch in the timed
+    region draws new negatives and a new permutation), then the same number of steps
+    on the last epoch stream reused (`frozen`).  Max over ranks, barrier +
+    synchronize on both sides of each timed region."""
+    eng, model, pipe = setup_engine(cfg, ds, train, world, rank, dev, group, global_batch)
+    nb = eng.num_batches
+    n_rows = eng.n_total
+    warm = max(1, -(-max(1, warmup) // nb)) * nb
+    eng.batches_done = 0
+    run_steps(eng, warm, use_graph)
+    torch.cuda.synchronize(dev)
+    epochs = max(1, -(-steps // nb))
+    k = epochs * nb
+    _barrier(group, dev)
+    torch.cuda.synchronize(dev)
+    e0 = pipe.stats["epochs"]
+    t0 = time.perf_counter()
+    run_steps(eng, k, use_graph)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    _barrier(group, dev)
+    dt = _max_over_ranks(dt, group, dev)
+    fresh = pipe.stats["epochs"] - e0
+    losses = eng.epoch_losses()
+    final_loss = float(losses[(eng.state_step() - 1) % nb])
+    # the same steps on the current epoch stream, reused (the step kernel wraps to the
+    # epoch's first batch): the device + exchange rate beside `value`
+    _barrier(group, dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    eng.run(k, use_graph=use_graph)
+    torch.cuda.synchronize(dev)
+    dtf = time.perf_counter() - t0
+    _barrier(group, dev)
+    dtf = _max_over_ranks(dtf, group, dev)
+    hm = pipe.stats.get("host_ms", [])[-epochs:]
+    host = {k2: float(np.mean([h[k2] for h in hm if k2 in h])) for k2 in ("sample", "words", "stage")
+            if any(k2 in h for h in hm)}
+    bm = pipe.stats.get("boundary_ms", [])[-epochs:]
+    if bm:
+        host["boundary_join"] = float(np.mean([x[0] for x in bm]))
+        host["boundary_rest"] = float(np.mean([x[1] for x in bm]))
+    return {"eng": eng, "model": model, "pipe": pipe, "value": epochs * n_rows / dt, "dt": dt, "steps": k,
+            "epochs": epochs, "fresh_epochs": fresh, "rows_per_epoch": n_rows, "batches_per_epoch": nb,
+            "final_loss": final_loss, "frozen_value": k * n_rows / nb / dtf, "frozen_ms_per_step": dtf / k * 1e3,
+            "epoch_host_ms": host}
+
+
+def harness_main(args, world, rank):
+    """--cpu-harness (tests only): the launch / rendezvous / timing / JSON contract of
+    this script on the CPU over gloo, with no device work -- each rank draws the
+    config's epochs through the product host sampler and takes its shard of every
+    global batch.  The line says so; it is not a measurement of the hot path."""
+    import torch.distributed as dist
+    from ncf_amd.distributed import shard_range
+    group = None
+    if world > 1:
+        dist.init_process_group("gloo")
+        group = dist.group.WORLD
+    if os.environ.get("NCF_BENCH_FAIL_RANK") == str(rank):  # tests: a rank dying after rendezvous
+        raise SystemExit(3)
+    shape, f, nl, global_batch = CONFIGS[args.config]
+    per_gpu = -(-global_batch // world)
+    ds, train = make_train_data(args.config)
+    dev = torch.device("cpu")
+    _barrier(group, dev)
+    t0 = time.perf_counter()
+    np.random.seed(0)
+    n = 0
+    for _ in range(max(1, args.harness_epochs)):
+        train.ng_sample()
+        m = len(train)
+        for b0 in range(0, m, global_batch):
+            lo, hi = shard_range(min(global_batch, m - b0), world, rank)
+            n += hi - lo
+    dt = _max_over_ranks(time.perf_counter() - t0, group, dev)
+    rows = torch.tensor([n], dtype=torch.int64)
+    if group is not None:
+        dist.all_reduce(rows, group=group)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": int(rows.item()) / dt, "unit": "interactions/s", "n_gpus": world,
+                          "harness": "cpu-gloo: host sampler + shard arithmetic only, no device work",
+                          "config": {"workload": args.config.upper(), "global_batch": global_batch,
+                                     "per_gpu_batch": per_gpu, "parallelism": f"dp{world}"}}), flush=True)
+    if group is not None:
+        dist.barrier(group=group)
+        dist.destroy_process_group()
+
+
+METRIC = "training interactions/sec + HR@10, NeuMF factors=64 ml-1m, 1/2/4/8 MI355X"
+
+
+def newest_profile(config, kernel_names):
+    """(mfma_busy_frac of the first kernel, source) from the newest SQ pass of this
+    config in profiles/ (scripts/profile.sh), or (None, None)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_prof_summary.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("config") != config:
+            continue
+        for k in d.get("kernels", []):
+            if k.get("kernel") == kernel_names[0] and k.get("mfma_busy_frac") is not None:
+                return float(k["mfma_busy_frac"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=200, help="timed steps, rounded up to whole epochs")
+    ap.add_argument("--warmup", type=int, default=20, help="warm-up steps, rounded up to whole epochs")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--kernel-steps", type=int, default=20, help="eager steps timed per kernel with HIP events")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--skip-cpu-baseline", action="store_true")
+    ap.add_argument("--no-script-epoch", action="store_true")
     ap.add_argument("--skip-eval", action="store_true")
+    ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling (global batch x N) field")
     ap.add_argument("--e2e-epochs", type=int, default=16, help="Trainer.fit epochs for the e2e figure (0: skip)")
+    ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-harness", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--harness-epochs", type=int, default=1, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if args.cpu_baseline_only:  # child of cpu_baseline_child: no GPU
+        print(json.dumps(cpu_baseline(args.config, args.cpu_seconds, not args.no_script_epoch)), flush=True)
+        return None
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # spawn the ranks ourselves, before anything touches a GPU
+        sys.exit(spawn_ranks(sys.argv[1:], args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.cpu_harness:
+        return harness_main(args, world, rank)
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run --nproc-per-node N")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     group = None
@@ -337,62 +598,19 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
         group = dist.group.WORLD
 
-    shape, f, nl, per_gpu = CONFIGS[args.config]
-    global_batch = per_gpu * world
+    shape, f, nl, global_batch = CONFIGS[args.config]
+    per_gpu = -(-global_batch // world)
+    mtype = MODEL.get(args.config, "NeuMF-end")
+    use_graph = not args.no_graph
     t_data = time.perf_counter()
     ds, train = make_train_data(args.config)
     U, I = ds["user_num"], ds["item_num"]
-    eng, model, pipe = setup_engine(args.config, ds, train, world, rank, dev, group, global_batch)
-    torch.cuda.synchronize(dev)
     t_data = time.perf_counter() - t_data
 
-    # ---- warmup (first step eager, then capture) -----------------------------
-    use_graph = not args.no_graph
-    eng.batches_done = 0
-    run_steps(eng, max(1, args.warmup), use_graph)
-    torch.cuda.synchronize(dev)
-
-    # ---- timed region ----------------------------------------------------------
-    if world > 1:
-        torch.distributed.barrier(group=group, device_ids=[local])
-    torch.cuda.synchronize(dev)
-    epochs0 = pipe.stats["epochs"]
-    t0 = time.perf_counter()
-    run_steps(eng, args.steps, use_graph)
-    torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
-    epochs_in_timed = pipe.stats["epochs"] - epochs0
-    if world > 1:
-        torch.distributed.barrier(group=group, device_ids=[local])
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=group)
-        dt = float(t.item())
-    rows = args.steps * global_batch
-    value = rows / dt
-    losses = eng.epoch_losses()
-    final_loss = float(losses[(eng.state_step() - 1) % eng.num_batches])
-
-    # ---- the same number of steps on the current epoch stream, reused (no fresh
-    # negatives / permutation: the step kernel wraps to the epoch's first batch): the
-    # device + exchange rate beside `value`, which the sequential host sampler bounds
-    # once an epoch is only a few steps long (N >= 4 at 65,536 rows per GPU)
-    if world > 1:
-        torch.distributed.barrier(group=group, device_ids=[local])
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    eng.run(args.steps, use_graph=use_graph)
-    torch.cuda.synchronize(dev)
-    dt_frozen = time.perf_counter() - t0
-    if world > 1:
-        torch.distributed.barrier(group=group, device_ids=[local])
-        t = torch.tensor([dt_frozen], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=group)
-        dt_frozen = float(t.item())
-    frozen = {"value": rows / dt_frozen, "ms_per_step": dt_frozen / args.steps * 1e3,
-              "note": "the same steps with the last epoch stream reused (no new negatives or permutation): "
-                      "device + exchange rate; `value` times fresh epochs, whose host sampler (sequential in "
-                      "the reference's NumPy stream, ~3 ms per ml-1m epoch) bounds it once an epoch is only a "
-                      "few global steps long"}
+    # ---- headline: the reference's global batch split over the N ranks (strong
+    # scaling), whole fresh epochs
+    m = measure(args.config, ds, train, world, rank, dev, group, global_batch, args.steps, args.warmup, use_graph)
+    eng, model, pipe = m["eng"], m["model"], m["pipe"]
 
     # ---- per-kernel live timing (HIP events on the launch stream) -------------
     kt = eng.time_kernels(args.kernel_steps)
@@ -403,24 +621,17 @@ def main():
         pipe_ms.append(pipe.device_ms())
     kt["epoch_rows_randperm_side_stream"] = float(np.mean([x[0] for x in pipe_ms]))
     kt["epoch_grouping_side_stream"] = float(np.mean([x[1] for x in pipe_ms]))
-    hm = pipe.stats.get("host_ms", [])[-3:]
-    kt["epoch_host_ms"] = {k: float(np.mean([h[k] for h in hm if k in h])) for k in ("sample", "words", "stage")
-                           if any(k in h for h in hm)}
-    bm = pipe.stats.get("boundary_ms", [])[1:]
-    if bm:
-        kt["epoch_host_ms"]["boundary_join"] = float(np.mean([x[0] for x in bm]))
-        kt["epoch_host_ms"]["boundary_rest"] = float(np.mean([x[1] for x in bm]))
+    kt["epoch_host_ms"] = m["epoch_host_ms"]
     kt["ncf_train_step_per_launch_b2b"] = eng.time_train_kernel(50)
     from ncf_amd import ops
     import ncf_amd._lib as L
-    mtype = MODEL.get(args.config, "NeuMF-end")
     fact = ops.fact_mode(eng.lay)
     path = L.supported(mtype, f, nl)
     dm = f * 2 ** (nl - 1)
     rows_per_launch = per_gpu
-    flops = tower_flops_per_row(f, nl, mtype) * rows_per_launch
     ms = kt["ncf_train_step_per_launch_b2b"]
-    achieved_tf = flops / (ms * 1e-3) / 1e12
+    alg_flops = tower_flops_per_row(f, nl, mtype) * rows_per_launch
+    alg_tf = alg_flops / (ms * 1e-3) / 1e12
     xflops = executed_flops(f, nl, mtype, rows_per_launch, U + I, fact, path == L.PATH_FUSED)
     executed_tf = xflops / (ms * 1e-3) / 1e12
     bytes_launch = gather_scatter_bytes_per_row(f, nl) * rows_per_launch
@@ -433,10 +644,23 @@ def main():
         kname = (f"ncf_step_kernel<{f},{nl},{mtype.split('-')[0]},FACT={str(fact).lower()}>"
                  + (f" + fact_expand_kernel<{dm}> (factored layer 0)" if fact else " (per-row layer 0)")
                  + "; launch group timed back to back")
-        traffic, traffic_src = pmc_traffic(args.config, names)
+        traffic, traffic_src = pmc_traffic(args.config, names) if world == 1 else (None, None)
+        busy, busy_src = newest_profile(args.config, names) if world == 1 else (None, None)
     else:
-        names, traffic, traffic_src = [], None, None
+        names, traffic, traffic_src, busy, busy_src = [], None, None, None, None
         kname = "layered path: all kernels of ncf_train_step (fwd/predict/bwd GEMMs)"
+
+    # ---- weak scaling (extra field): global batch x N, per-GPU batch fixed -----
+    weak = None
+    if world > 1 and not args.no_weak:
+        pipe.close()
+        w = measure(args.config, ds, train, world, rank, dev, group, global_batch * world, args.steps,
+                    args.warmup, use_graph)
+        weak = {"value": w["value"], "ms_per_step": w["dt"] / w["steps"] * 1e3, "steps": w["steps"],
+                "global_batch": global_batch * world, "per_gpu_batch": global_batch,
+                "note": "the per-GPU batch held at the single-GPU batch (a different training trajectory "
+                        "from the reference's batch size); `value` is the reference's global batch"}
+        w["pipe"].close()
 
     # ---- quality: HR@10 / NDCG@10 on the leave-one-out test set ---------------
     hr10 = ndcg10 = None
@@ -446,7 +670,8 @@ def main():
         ti = np.concatenate([ds["test_items"][:, None], ds["test_negatives"]], 1).reshape(-1)
         HR, NDCG = evaluate_arrays(model, tu, ti, 100, 10)
         hr10, ndcg10 = float(np.mean(HR)), float(np.mean(NDCG))
-    pipe.close()
+    if weak is None:
+        pipe.close()
 
     out = None
     if rank == 0:
@@ -455,22 +680,24 @@ def main():
             e2e = e2e_fit(args.config, ds, dev, args.e2e_epochs)
         cpu = None
         if not args.skip_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args.config, ds, per_gpu, args.cpu_seconds, threads=min(16, host_facts()["cpus_available"]))
+            cpu = cpu_baseline_child(args.config, args.cpu_seconds, not args.no_script_epoch)
+        dt, k = m["dt"], m["steps"]
         out = {
-            "metric": "training interactions/sec + HR@10, NeuMF factors=64 ml-1m, 1/2/4/8 MI355X",
-            "value": value,
+            "metric": METRIC,
+            "value": m["value"],
             "unit": "interactions/s",
             "n_gpus": world,
-            "steps": args.steps,
+            "steps": k,
             "warmup": args.warmup,
-            "ms_per_step": dt / args.steps * 1e3,
+            "ms_per_step": dt / k * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp32",
             "data": (f"synthetic {shape}-shaped ({U - 1:,} users x {I - 1:,} items, {len(ds['train_users']):,} "
-                     f"train positives, 4 bit-exact sampled negatives each, fresh negatives and permutation "
-                     f"every epoch: {epochs_in_timed} epoch boundaries in the timed region; seed 0)"),
+                     f"train positives, 4 bit-exact sampled negatives each); {m['epochs']} whole epochs timed "
+                     f"({k} steps, requested {args.steps}, rounded up), each with fresh negatives and permutation "
+                     f"({m['fresh_epochs']} epoch boundaries in the timed region); seed 0"),
             "config": {"workload": f"{args.config.upper()}: NCF(user_num={U}, item_num={I}, factor_num={f}, "
                                    f"num_layers={nl}, {mtype}), Adam lr 1e-3"
                                    + (f"; response distillation (T 2.0, alpha 0.5) from a random-init teacher "
@@ -478,35 +705,40 @@ def main():
                                       f"each epoch stream are one forward launch at the epoch boundary"
                                       if args.config == "c5" else ""),
                        "global_batch": global_batch, "per_gpu_batch": per_gpu, "parallelism": f"dp{world}",
-                       "mlp_layers": [int(2 * f * 2 ** (nl - 1)) >> k for k in range(nl + 1)],
-                       "dp_exchange": eng.dp_mode, "hip_graph": use_graph},
-            "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": 157.3, "unit": "TFLOP/s",
-                         "frac": achieved_tf / 157.3, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": kname, "flops_per_launch": flops, "kernel_ms": ms,
-                         "executed": {"flops_per_launch": xflops, "achieved": executed_tf,
-                                      "frac": executed_tf / 157.3,
-                                      "note": "flops the kernels execute; `achieved` counts the SURVEY 8(d) "
-                                              "per-row tower flops (6 sum s_k s_k+1 + predict), of which the "
-                                              "factored layer 0 replaces the layer-0 per-row GEMMs by "
-                                              "per-entity ones over the U + I table rows"
-                                              + ("; with it the algorithmic rate exceeds the fp32 MFMA peak"
-                                                 if achieved_tf > 157.3 else "")}},
+                       "mlp_layers": [int(2 * f * 2 ** (nl - 1)) >> j for j in range(nl + 1)],
+                       "dp_exchange": eng.dp_mode, "hip_graph": use_graph,
+                       "rows_per_epoch": m["rows_per_epoch"], "steps_per_epoch": m["batches_per_epoch"]},
+            "roofline": {"bound": "mfma", "achieved": executed_tf, "peak": 157.3, "unit": "TFLOP/s",
+                         "frac": executed_tf / 157.3, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": kname, "kernel_ms": ms, "flops_per_launch": xflops,
+                         "flops_note": "fp32 flops the kernels execute per launch (2 per MAC): per-row tower "
+                                       "layers >= 1 and predict, the fused kernel's per-row layer-0 forward, the "
+                                       "factored layer 0's per-entity GEMMs over the U + I table rows",
+                         "hw_mfma_busy": busy, "hw_mfma_busy_source": busy_src,
+                         "algorithmic": {"flops_per_launch": alg_flops, "achieved": alg_tf,
+                                         "note": "SURVEY 8(d) per-row tower flops (6 sum s_k s_k+1 + predict) x rows; "
+                                                 "the factored layer 0 does not execute the per-row layer-0 "
+                                                 "backward it counts, so this rate is not a roofline fraction"}},
             "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": 8000.0, "unit": "GB/s",
                              "frac": achieved_gbs / 8000.0, "bytes_per_launch": bytes_launch,
+                             "traffic_GBps": (traffic / (ms * 1e-3) / 1e9) if traffic else None,
                              "note": ("gather+scatter algorithmic bytes of the same launch group" if path == L.PATH_FUSED
                                       else "gather+scatter algorithmic bytes over all layered-path kernels")},
             "kernel_ms": kt,
             "adam": adam_info(kt, eng, model),
             "quality": {"HR@10": hr10, "NDCG@10": ndcg10, "epochs_trained": round(eng.state_step() / eng.num_batches, 2),
-                        "last_batch_loss": final_loss},
+                        "last_batch_loss": m["final_loss"]},
             "e2e": e2e,
-            "frozen_epoch": frozen,
+            "frozen_epoch": {"value": m["frozen_value"], "ms_per_step": m["frozen_ms_per_step"],
+                             "note": "the same steps with the last epoch stream reused (no new negatives or "
+                                     "permutation): device + exchange rate"},
+            "weak_scaling": weak,
             "cpu_baseline": cpu,
-            "setup_s": {"data+first_epoch": round(t_data, 2)},
+            "setup_s": {"data": round(t_data, 2)},
         }
         print(json.dumps(out), flush=True)
     if world > 1:
-        torch.distributed.barrier(group=group, device_ids=[local])
+        _barrier(group, dev)
         torch.distributed.destroy_process_group()
     return out
 

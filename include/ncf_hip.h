@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 12
+#define NCF_ABI_VERSION 13
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -292,6 +292,47 @@ int ncf_reduce_adam_step(const ncf_layout *lay, const void *workspace, float *pa
                          float *exp_avg, float *exp_avg_sq, const int64_t *ranges, int nranges,
                          ncf_step_ctl *ctl, double lr, double beta1, double beta2, double eps,
                          float *loss_hist, int64_t hist_len, void *stream);
+
+/*
+ * Deferred ("catch-up") Adam -- since ABI 13.  Exactly the dense Adam of
+ * ncf_reduce_adam_step (torch.optim.Adam, train_neumf.py:90,115: every row moves
+ * every step through its moments), moving only the embedding rows that need it:
+ * for a row whose gradient is exactly zero, Adam step s is a fixed per-element fp32
+ * sequence with step-s scalars, so the steps a row sat out are replayed, in order,
+ * with the same arithmetic, when the row is next needed -- bitwise the dense result.
+ *
+ * ncf_batch_touched: for every global batch b of the epoch stream (rows[0..n), batches
+ * of batch_global rows, padding rows skipped), the sorted unique user ids and item ids
+ * it holds.  touched (int32, ncf_touched_bytes): [nb][min(U, B)] users, [nb][min(I, B)]
+ * items, then [nb][2] counts (users, items); nb = ceil(n / batch_global).  U, I <= 2^20.
+ *
+ * ncf_lazy_adam_step: ncf_reduce_adam_step's tower part (slab reduction + Adam, loss,
+ * ctl commit) and, over the embedding tables, the rows of batch b = snap_batch % nb
+ * (they hold gradients) and of batch b + 1 (the next forward reads them) -- on the
+ * epoch's last batch every row instead -- each brought from last_step[row] + 1 to
+ * t = snap_t: replays with g = 0, then step t with its gradient, which is cleared.
+ * last_step: int32 [U + I] (users, then items; 0 = none since Adam state zero, or the
+ * step the optimizer state was loaded at).  step_scalars: float [ring][2], written for
+ * step t by this launch; ring >= nb + 2.  n_total / batch_global: the epoch stream's.
+ * factor_num % 4 == 0 (NCF_E_UNSUPPORTED otherwise).
+ *
+ * ncf_lazy_adam_flush: every embedding row through t = ctl->adam_t (after that step's
+ * ncf_lazy_adam_step): parameters and moments equal the dense optimizer's again --
+ * before a metrics() pass, state_dict() or a checkpoint.
+ */
+int64_t ncf_touched_bytes(int64_t n, int64_t batch_global, int user_num, int item_num);
+int ncf_batch_touched(const uint64_t *rows, int64_t n, int64_t batch_global, int user_num, int item_num,
+                      int32_t *touched, void *stream);
+int ncf_lazy_adam_step(const ncf_layout *lay, const void *workspace, float *params, float *grads,
+                       float *exp_avg, float *exp_avg_sq, const int64_t *ranges, int nranges,
+                       ncf_step_ctl *ctl, double lr, double beta1, double beta2, double eps,
+                       float *loss_hist, int64_t hist_len, const int32_t *touched, int64_t n_total,
+                       int64_t batch_global, int32_t *last_step, float *step_scalars, int64_t ring,
+                       void *stream);
+int ncf_lazy_adam_flush(const ncf_layout *lay, float *params, float *grads, float *exp_avg,
+                        float *exp_avg_sq, const int64_t *ranges, int nranges, const ncf_step_ctl *ctl,
+                        double beta1, double beta2, double eps, int32_t *last_step,
+                        const float *step_scalars, int64_t ring, void *stream);
 
 /* Plain SGD p -= lr * g (optim.SGD(lr*10) on the --pretraining path, train_neumf.py:87-88). */
 int ncf_sgd_step(float *params, float *grads, const int64_t *ranges, int nranges,

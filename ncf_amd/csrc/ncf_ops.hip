@@ -122,6 +122,16 @@ __device__ __forceinline__ void adam_f4(f4& p, f4& m, f4& v, const f4& g, float 
     }
 }
 
+// Step-t scalars in double like torch's Python scalars, by thread 0 of the block:
+// sc[0] = -(lr / (1 - beta1^t)), sc[1] = sqrt(1 - beta2^t) (torch _single_tensor_adam).
+__device__ __forceinline__ void step_scalars(int64_t t_step, double lr, double beta1, double beta2, float* sc) {
+    if (threadIdx.x == 0) {
+        const double t = (double)t_step;
+        sc[0] = (float)(-(lr / (1.0 - pow(beta1, t))));
+        sc[1] = (float)sqrt(1.0 - pow(beta2, t));
+    }
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                    float* __restrict__ v, Ranges R, const ncf_step_ctl* ctl, double lr,
                                                    double beta1, double beta2, float eps, int64_t loss_slot,
@@ -200,6 +210,69 @@ __device__ __forceinline__ bool in_ranges(const Ranges& R, int64_t i) {
     return false;
 }
 
+// Block of the tower part (blockIdx.x < nA): reduce 64 slab columns (W0's from the
+// expansion's partials), apply Adam to the active ones in place; the loss column
+// goes to the history.  sc[0..1] = (-step size, sqrt(bias correction 2)) of step t,
+// computed by thread 0 of the block after its loads are in flight.
+__device__ __forceinline__ void tower_reduce_adam_block(const float* __restrict__ slab, int lo, int stride, int rows,
+                                                        int64_t tb, int64_t tower_len, float* __restrict__ p,
+                                                        float* __restrict__ m, float* __restrict__ v, const Ranges& R,
+                                                        int64_t t_step, int64_t b_step, double lr, double beta1,
+                                                        double beta2, float eps, float* loss_hist, int64_t hist_len,
+                                                        const W0Part& wp, float* sc, f4 (*part)[16]) {
+#pragma clang fp contract(off)
+    const float w1 = (float)(1.0 - beta1);
+    const float b2 = (float)beta2;
+    const float omb2 = (float)(1.0 - beta2);
+    const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
+    const int j = lo + (blockIdx.x * 16 + c4) * 4;
+    // the updating threads' optimizer state, requested ahead of the slab reads
+    const int64_t i = tb + j;
+    const bool upd = rg == 0 && j < tower_len && in_ranges(R, i);
+    f4 pp, mm, vv;
+    if (upd) {
+        pp = *reinterpret_cast<const f4*>(p + i);
+        mm = *reinterpret_cast<const f4*>(m + i);
+        vv = *reinterpret_cast<const f4*>(v + i);
+    }
+    f4 s = f4{0.f, 0.f, 0.f, 0.f};
+    if (j < wp.cols) {
+        s = w0_part_sum(wp, j, rg);
+    } else if (j < stride) {
+        const float* q = slab + (int64_t)rg * stride + j;
+        const int per = rows / 16;
+#pragma unroll 16
+        for (int r = 0; r < per; ++r) {
+            const f4 x = *reinterpret_cast<const f4*>(q + (int64_t)r * 16 * stride);
+            s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+        }
+        if (rg < rows - 16 * per) {
+            const f4 x = *reinterpret_cast<const f4*>(q + (int64_t)per * 16 * stride);
+            s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+        }
+    }
+    part[rg][c4] = s;
+    step_scalars(t_step, lr, beta1, beta2, sc);
+    __syncthreads();
+    const float neg_step = sc[0], bc2s = sc[1];
+    if (rg == 0 && j < stride) {
+        f4 gs = part[0][c4];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) {
+            const f4 x = part[q][c4];
+            gs.x += x.x; gs.y += x.y; gs.z += x.z; gs.w += x.w;
+        }
+        if (j == tower_len) {
+            if (loss_hist != nullptr && hist_len > 0) loss_hist[((b_step % hist_len) + hist_len) % hist_len] = gs.x;
+        } else if (upd) {
+            adam_f4(pp, mm, vv, gs, w1, b2, omb2, bc2s, eps, neg_step);
+            *reinterpret_cast<f4*>(m + i) = mm;
+            *reinterpret_cast<f4*>(v + i) = vv;
+            *reinterpret_cast<f4*>(p + i) = pp;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restrict__ slab, int lo, int stride, int rows,
                                                           int nA, int64_t tb, int64_t tower_len, float* __restrict__ p,
                                                           float* __restrict__ g, float* __restrict__ m,
@@ -211,67 +284,13 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
     __shared__ f4 part[16][16];
     const int64_t t_step = ctl->snap_t;
     const int64_t b_step = ctl->snap_batch;
-    // Bias corrections in double like torch's Python scalars, by thread 0 AFTER its
-    // block's loads are in flight (the double pow costs about a memory round trip).
-    auto scalars = [&]() {
-        if (threadIdx.x == 0) {
-            const double t = (double)t_step;
-            sc[0] = (float)(-(lr / (1.0 - pow(beta1, t))));
-            sc[1] = (float)sqrt(1.0 - pow(beta2, t));
-        }
-    };
-    const float w1 = (float)(1.0 - beta1);
-    const float b2 = (float)beta2;
-    const float omb2 = (float)(1.0 - beta2);
     if ((int)blockIdx.x < nA) {
-        const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
-        const int j = lo + (blockIdx.x * 16 + c4) * 4;
-        // the updating threads' optimizer state, requested ahead of the slab reads
-        const int64_t i = tb + j;
-        const bool upd = rg == 0 && j < tower_len && in_ranges(R, i);
-        f4 pp, mm, vv;
-        if (upd) {
-            pp = *reinterpret_cast<const f4*>(p + i);
-            mm = *reinterpret_cast<const f4*>(m + i);
-            vv = *reinterpret_cast<const f4*>(v + i);
-        }
-        f4 s = f4{0.f, 0.f, 0.f, 0.f};
-        if (j < wp.cols) {
-            s = w0_part_sum(wp, j, rg);
-        } else if (j < stride) {
-            const float* q = slab + (int64_t)rg * stride + j;
-            const int per = rows / 16;
-#pragma unroll 16
-            for (int r = 0; r < per; ++r) {
-                const f4 x = *reinterpret_cast<const f4*>(q + (int64_t)r * 16 * stride);
-                s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
-            }
-            if (rg < rows - 16 * per) {
-                const f4 x = *reinterpret_cast<const f4*>(q + (int64_t)per * 16 * stride);
-                s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
-            }
-        }
-        part[rg][c4] = s;
-        scalars();
-        __syncthreads();
-        const float neg_step = sc[0], bc2s = sc[1];
-        if (rg == 0 && j < stride) {
-            f4 gs = part[0][c4];
-#pragma unroll
-            for (int q = 1; q < 16; ++q) {
-                const f4 x = part[q][c4];
-                gs.x += x.x; gs.y += x.y; gs.z += x.z; gs.w += x.w;
-            }
-            if (j == tower_len) {
-                if (loss_hist != nullptr && hist_len > 0) loss_hist[((b_step % hist_len) + hist_len) % hist_len] = gs.x;
-            } else if (upd) {
-                adam_f4(pp, mm, vv, gs, w1, b2, omb2, bc2s, eps, neg_step);
-                *reinterpret_cast<f4*>(m + i) = mm;
-                *reinterpret_cast<f4*>(v + i) = vv;
-                *reinterpret_cast<f4*>(p + i) = pp;
-            }
-        }
+        tower_reduce_adam_block(slab, lo, stride, rows, tb, tower_len, p, m, v, R, t_step, b_step, lr, beta1, beta2,
+                                eps, loss_hist, hist_len, wp, sc, part);
     } else {
+        const float w1 = (float)(1.0 - beta1);
+        const float b2 = (float)beta2;
+        const float omb2 = (float)(1.0 - beta2);
         const int64_t total = RE.prefix[RE.n];
         const int64_t nthr = (int64_t)(gridDim.x - nA) * blockDim.x;
         int64_t q = (int64_t)(blockIdx.x - nA) * blockDim.x + threadIdx.x;
@@ -286,7 +305,7 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
             pp = *reinterpret_cast<const f4*>(p + i);
         };
         if (q < total) load();  // the first element's loads fly while thread 0 computes
-        scalars();
+        step_scalars(t_step, lr, beta1, beta2, sc);
         __syncthreads();
         const float neg_step = sc[0], bc2s = sc[1];
         while (q < total) {
@@ -303,6 +322,185 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
         ctl->adam_t = t_step;
         ctl->batch = b_step + 1;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Deferred ("catch-up") Adam over the embedding tables -- exactly the dense
+// torch.optim.Adam of train_neumf.py:90,115, moving only the rows that need it.
+// For a row whose gradient is exactly zero, Adam step s is a fixed per-element fp32
+// sequence with step-s scalars (adam_f4 with g = 0), so the steps a row sat out
+// can be replayed, in order, when it is next needed, with a bitwise-identical
+// result.  last[row] (users [0, U), items [U, U + I)) is the last step applied to
+// the row; ring[s % ring_n] the step-s scalars, written by step s's launch.
+// Step t's launch (global batch b of the epoch stream) takes the rows batch b
+// touched (their gradient is in grads) and the rows batch b + 1 will read (so
+// the next forward sees current parameters); on the epoch's last batch, every
+// row instead.  A row is claimed by atomicMax(last, t) -- one group per claim --
+// and brought from last + 1 through t: the replays with g = 0, then step t with
+// its gradient (zero for a row batch b did not touch), which is then cleared.
+// Flush mode: every row through t = ctl->adam_t (all gradients already zero).
+struct LazyArgs {
+    float* p;
+    float* g;
+    float* m;
+    float* v;
+    int64_t off[4];  // Ug, Ig, Um, Im flat offsets (< 0: table inactive)
+    int w4[4];       // float4s per row of each table
+    int U, I;
+    const int32_t* touched;  // ncf_batch_touched: [nb][su] users, [nb][si] items, [nb][2] counts
+    int64_t nb, su, si;
+    int32_t* last;  // [U + I]
+    float* ring;    // [ring_n][2]
+    int64_t ring_n;
+};
+
+constexpr int LZ_GROUP = 16;  // lanes per claimed row
+
+__device__ __forceinline__ void lazy_rows(const LazyArgs& a, int64_t t, int64_t b, bool flush, float neg_t, float bc2s_t,
+                                          float w1, float b2, float omb2, float eps, int64_t gid, int64_t ngroups) {
+#pragma clang fp contract(off)
+    const int glane = threadIdx.x & (LZ_GROUP - 1);
+    const int32_t* cnt = a.touched + a.nb * (a.su + a.si);
+    const int64_t n0 = flush ? 0 : cnt[2 * b], n1 = flush ? 0 : cnt[2 * b + 1];
+    const bool next = !flush && b + 1 < a.nb;
+    const int64_t n2 = next ? cnt[2 * (b + 1)] : a.U, n3 = next ? cnt[2 * (b + 1) + 1] : a.I;
+    const int64_t total = n0 + n1 + n2 + n3;
+    const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t w = gid; w < total; w += ngroups) {
+        int side, id;
+        if (w < n0) {
+            side = 0; id = a.touched[b * a.su + w];
+        } else if (w < n0 + n1) {
+            side = 1; id = a.touched[a.nb * a.su + b * a.si + (w - n0)];
+        } else if (w < n0 + n1 + n2) {
+            side = 0; id = next ? a.touched[(b + 1) * a.su + (w - n0 - n1)] : (int)(w - n0 - n1);
+        } else {
+            side = 1; id = next ? a.touched[a.nb * a.su + (b + 1) * a.si + (w - n0 - n1 - n2)] : (int)(w - n0 - n1 - n2);
+        }
+        int old = 0;
+        if (glane == 0) {
+            int32_t* lp = a.last + (side ? a.U + id : id);
+            old = *lp;
+            if (old < (int)t) old = atomicMax(lp, (int)t);
+        }
+        old = __shfl(old, threadIdx.x & ~(LZ_GROUP - 1), 64);
+        if (old >= (int)t) continue;
+        const int sa = side, sb = side + 2;  // g table, m table of this side
+        const int wa = a.off[sa] >= 0 ? a.w4[sa] : 0, wb = a.off[sb] >= 0 ? a.w4[sb] : 0;
+        for (int k = glane; k < wa + wb; k += LZ_GROUP) {
+            const int64_t e = k < wa ? a.off[sa] + ((int64_t)id * a.w4[sa] + k) * 4
+                                     : a.off[sb] + ((int64_t)id * a.w4[sb] + (k - wa)) * 4;
+            f4 pp = *reinterpret_cast<const f4*>(a.p + e);
+            f4 mm = *reinterpret_cast<const f4*>(a.m + e);
+            f4 vv = *reinterpret_cast<const f4*>(a.v + e);
+            const f4 gg = *reinterpret_cast<const f4*>(a.g + e);
+            for (int s = old + 1; s < (int)t; ++s) {  // the steps this row sat out: g = 0
+                const float* sc = a.ring + 2 * (s % a.ring_n);
+                adam_f4(pp, mm, vv, zero, w1, b2, omb2, sc[1], eps, sc[0]);
+            }
+            adam_f4(pp, mm, vv, gg, w1, b2, omb2, bc2s_t, eps, neg_t);
+            *reinterpret_cast<f4*>(a.m + e) = mm;
+            *reinterpret_cast<f4*>(a.v + e) = vv;
+            *reinterpret_cast<f4*>(a.p + e) = pp;
+            if (gg.x != 0.f || gg.y != 0.f || gg.z != 0.f || gg.w != 0.f) *reinterpret_cast<f4*>(a.g + e) = zero;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void lazy_adam_kernel(const float* __restrict__ slab, int lo, int stride, int rows,
+                                                        int nA, int64_t tb, int64_t tower_len, Ranges R,
+                                                        ncf_step_ctl* ctl, double lr, double beta1, double beta2,
+                                                        float eps, float* loss_hist, int64_t hist_len, W0Part wp,
+                                                        LazyArgs a) {
+#pragma clang fp contract(off)
+    __shared__ float sc[2];
+    __shared__ f4 part[16][16];
+    const int64_t t_step = ctl->snap_t;
+    const int64_t b_step = ctl->snap_batch;
+    if ((int)blockIdx.x < nA) {
+        tower_reduce_adam_block(slab, lo, stride, rows, tb, tower_len, a.p, a.m, a.v, R, t_step, b_step, lr, beta1,
+                                beta2, eps, loss_hist, hist_len, wp, sc, part);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            a.ring[2 * (t_step % a.ring_n)] = sc[0];
+            a.ring[2 * (t_step % a.ring_n) + 1] = sc[1];
+        }
+    } else {
+        step_scalars(t_step, lr, beta1, beta2, sc);
+        __syncthreads();
+        const int64_t b = ((b_step % a.nb) + a.nb) % a.nb;
+        const int64_t groups_per_block = blockDim.x / LZ_GROUP;
+        const int64_t gid = (int64_t)(blockIdx.x - nA) * groups_per_block + threadIdx.x / LZ_GROUP;
+        lazy_rows(a, t_step, b, false, sc[0], sc[1], (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), eps, gid,
+                  (int64_t)(gridDim.x - nA) * groups_per_block);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctl->adam_t = t_step;
+        ctl->batch = b_step + 1;
+    }
+}
+
+__global__ __launch_bounds__(256) void lazy_flush_kernel(const ncf_step_ctl* ctl, double beta1, double beta2, float eps,
+                                                         LazyArgs a) {
+    const int64_t t = ctl->adam_t;
+    if (t <= 0) return;
+    const float* sc = a.ring + 2 * (t % a.ring_n);
+    const int64_t groups_per_block = blockDim.x / LZ_GROUP;
+    lazy_rows(a, t, 0, true, sc[0], sc[1], (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), eps,
+              (int64_t)blockIdx.x * groups_per_block + threadIdx.x / LZ_GROUP, (int64_t)gridDim.x * groups_per_block);
+}
+
+// ---------------------------------------------------------------------------
+// Rows each global batch touches (ncf_batch_touched): one block per (batch, side),
+// an LDS bitmap of the side's ids set by the batch's rows, then the set bits
+// written out in id order (block prefix scan of per-thread popcounts).
+constexpr int BT_THREADS = 1024;
+
+__global__ __launch_bounds__(BT_THREADS) void batch_touched_kernel(const uint64_t* __restrict__ rows, int64_t n,
+                                                                   int64_t B, int U, int I, int64_t nb, int64_t su,
+                                                                   int64_t si, int32_t* __restrict__ out) {
+    extern __shared__ uint32_t bits[];
+    __shared__ int wsum[BT_THREADS / 64];
+    const int64_t b = blockIdx.x >> 1;
+    const int side = blockIdx.x & 1;
+    const int N = side ? I : U;
+    const int nw = (N + 31) / 32;
+    for (int k = threadIdx.x; k < nw; k += BT_THREADS) bits[k] = 0u;
+    __syncthreads();
+    const int64_t r0 = b * B, r1 = r0 + B < n ? r0 + B : n;
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += BT_THREADS) {
+        const uint64_t row = rows[r];
+        const uint32_t u = (uint32_t)row;
+        if (u == 0xffffffffu) continue;  // padding row
+        const uint32_t id = side ? (uint32_t)((row >> 32) & 0x7fffffffu) : u;
+        if (id < (uint32_t)N) atomicOr(&bits[id >> 5], 1u << (id & 31));
+    }
+    __syncthreads();
+    const int per = (nw + BT_THREADS - 1) / BT_THREADS;
+    const int w0 = threadIdx.x * per, w1 = w0 + per < nw ? w0 + per : nw;
+    int c = 0;
+    for (int w = w0; w < w1; ++w) c += __popc(bits[w]);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int base = 0;
+    for (int q = 0; q < wv; ++q) base += wsum[q];
+    int pos = base + incl - c;
+    int32_t* dst = side ? out + nb * su + b * si : out + b * su;
+    for (int w = w0; w < w1; ++w) {
+        uint32_t x = bits[w];
+        while (x) {
+            const int k = __ffs(x) - 1;
+            x &= x - 1;
+            dst[pos++] = w * 32 + k;
+        }
+    }
+    if (threadIdx.x == BT_THREADS - 1) out[nb * (su + si) + 2 * b + side] = base + incl;
 }
 
 // ---------------------------------------------------------------------------
@@ -1455,6 +1653,110 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
                        static_cast<const float*>(workspace), lo, stride, rows, nA, lay->tower_begin, lay->tower_len,
                        params, grads, exp_avg, exp_avg_sq, R, RE, ctl, lr, beta1, beta2, (float)eps, loss_hist,
                        hist_len, w0_part(lay, workspace));
+    return launch_status();
+}
+
+// ---- deferred Adam (ABI 13)
+static int lazy_args(const ncf_layout* lay, float* params, float* grads, float* m, float* v, const int64_t* ranges,
+                     int nranges, int32_t* last, float* ring, int64_t ring_n, LazyArgs* a) {
+    const int f = lay->factor_num, dm = f << (lay->num_layers - 1);
+    if (f % 4 != 0 || lay->user_num > (1 << 20) || lay->item_num > (1 << 20)) return NCF_E_UNSUPPORTED;
+    const int64_t offs[4] = {lay->ug, lay->ig, lay->um, lay->im};
+    const int64_t widths[4] = {f, f, dm, dm};
+    const int64_t nrows[4] = {lay->user_num, lay->item_num, lay->user_num, lay->item_num};
+    memset(a, 0, sizeof(*a));
+    for (int k = 0; k < 4; ++k) {
+        const int64_t b = offs[k], e = offs[k] + nrows[k] * widths[k];
+        bool act = false;
+        for (int i = 0; i < nranges; ++i)
+            if (ranges[2 * i] < e && ranges[2 * i + 1] > b) act = true;
+        a->off[k] = act ? offs[k] : -1;
+        a->w4[k] = (int)(widths[k] / 4);
+    }
+    a->p = params;
+    a->g = grads;
+    a->m = m;
+    a->v = v;
+    a->U = lay->user_num;
+    a->I = lay->item_num;
+    a->last = last;
+    a->ring = ring;
+    a->ring_n = ring_n;
+    return NCF_OK;
+}
+
+static void touched_shape(int64_t n, int64_t B, int U, int I, int64_t* nb, int64_t* su, int64_t* si) {
+    *nb = (n + B - 1) / B;
+    *su = U < B ? U : B;
+    *si = I < B ? I : B;
+}
+
+int64_t ncf_touched_bytes(int64_t n, int64_t batch_global, int user_num, int item_num) {
+    if (n <= 0 || batch_global <= 0 || user_num <= 0 || item_num <= 0) return -1;
+    int64_t nb, su, si;
+    touched_shape(n, batch_global, user_num, item_num, &nb, &su, &si);
+    return 4 * (nb * (su + si) + 2 * nb);
+}
+
+int ncf_batch_touched(const uint64_t* rows, int64_t n, int64_t batch_global, int user_num, int item_num,
+                      int32_t* touched, void* stream) {
+    if (!rows || !touched || n <= 0 || batch_global <= 0 || user_num <= 0 || item_num <= 0) return NCF_E_ARG;
+    if (user_num > (1 << 20) || item_num > (1 << 20)) return NCF_E_UNSUPPORTED;
+    int64_t nb, su, si;
+    touched_shape(n, batch_global, user_num, item_num, &nb, &su, &si);
+    const int mx = user_num > item_num ? user_num : item_num;
+    const int64_t lds = (int64_t)((mx + 31) / 32) * 4;
+    if (lds > 64 * 1024 && ensure_lds((const void*)batch_touched_kernel, lds) != NCF_OK) return NCF_E_LAUNCH;
+    hipLaunchKernelGGL(batch_touched_kernel, dim3((unsigned)(2 * nb)), dim3(BT_THREADS), (size_t)lds,
+                       (hipStream_t)stream, rows, n, batch_global, user_num, item_num, nb, su, si, touched);
+    return launch_status();
+}
+
+int ncf_lazy_adam_step(const ncf_layout* lay, const void* workspace, float* params, float* grads, float* exp_avg,
+                       float* exp_avg_sq, const int64_t* ranges, int nranges, ncf_step_ctl* ctl, double lr,
+                       double beta1, double beta2, double eps, float* loss_hist, int64_t hist_len,
+                       const int32_t* touched, int64_t n_total, int64_t batch_global, int32_t* last_step,
+                       float* step_scalars, int64_t ring, void* stream) {
+    if (!lay || !workspace || !params || !grads || !exp_avg || !exp_avg_sq || !ranges || !ctl || !touched ||
+        !last_step || !step_scalars || n_total <= 0 || batch_global <= 0)
+        return NCF_E_ARG;
+    int err = 0;
+    Ranges R = make_ranges(ranges, nranges, &err);
+    if (err) return NCF_E_ARG;
+    LazyArgs a;
+    const int rc = lazy_args(lay, params, grads, exp_avg, exp_avg_sq, ranges, nranges, last_step, step_scalars, ring, &a);
+    if (rc != NCF_OK) return rc;
+    touched_shape(n_total, batch_global, lay->user_num, lay->item_num, &a.nb, &a.su, &a.si);
+    if (ring < a.nb + 2) return NCF_E_ARG;  // a row's gap is at most one epoch: the last batch flushes
+    a.touched = touched;
+    const int stride = (int)ncf_slab_stride(lay);
+    const int lo = slab_lo(lay);
+    const int nA = (stride - lo + 63) / 64;
+    const int rows = reduce_rows(lay);
+    const int64_t work = 2 * (a.su + a.si) > a.su + a.si + a.U + a.I ? 2 * (a.su + a.si) : a.su + a.si + a.U + a.I;
+    int64_t nB = (work + (256 / LZ_GROUP) - 1) / (256 / LZ_GROUP);
+    if (nB > 2048) nB = 2048;
+    hipLaunchKernelGGL(lazy_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
+                       static_cast<const float*>(workspace), lo, stride, rows, nA, lay->tower_begin, lay->tower_len, R,
+                       ctl, lr, beta1, beta2, (float)eps, loss_hist, hist_len, w0_part(lay, workspace), a);
+    return launch_status();
+}
+
+int ncf_lazy_adam_flush(const ncf_layout* lay, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                        const int64_t* ranges, int nranges, const ncf_step_ctl* ctl, double beta1, double beta2,
+                        double eps, int32_t* last_step, const float* step_scalars, int64_t ring, void* stream) {
+    if (!lay || !params || !grads || !exp_avg || !exp_avg_sq || !ranges || !ctl || !last_step || !step_scalars ||
+        ring <= 0)
+        return NCF_E_ARG;
+    LazyArgs a;
+    const int rc = lazy_args(lay, params, grads, exp_avg, exp_avg_sq, ranges, nranges, last_step,
+                             const_cast<float*>(step_scalars), ring, &a);
+    if (rc != NCF_OK) return rc;
+    a.nb = 1;
+    int64_t nB = ((int64_t)a.U + a.I + (256 / LZ_GROUP) - 1) / (256 / LZ_GROUP);
+    if (nB > 2048) nB = 2048;
+    hipLaunchKernelGGL(lazy_flush_kernel, dim3((unsigned)nB), dim3(256), 0, (hipStream_t)stream, ctl, beta1, beta2,
+                       (float)eps, a);
     return launch_status();
 }
 

@@ -164,6 +164,12 @@ class TrainEngine:
         # ncf_user_order output per epoch-stream buffer (key: pointer, rows)
         self._orders = {}
         self._uses_order = False
+        # deferred Adam (ncf_lazy_adam_step): per-row last step, step scalars ring,
+        # ncf_batch_touched lists per epoch-stream buffer (key: pointer, rows, batch)
+        self.lazy = False
+        self._last = None
+        self._ring = None
+        self._touched = {}
 
     # ------------------------------------------------------------------ data
     def set_epoch_stream(self, rows, batch_size, checked=False):
@@ -201,6 +207,22 @@ class TrainEngine:
             self._ctl_n = n
         else:
             self.ctl[0:1].zero_()
+        # deferred Adam: touched rows of every batch of this stream (once per epoch)
+        lazy = self._lazy_wanted()
+        if self.lazy and not lazy:
+            self.flush()  # back to dense Adam: every row current first
+        if lazy:
+            lib = L.hip()
+            if self._last is None:
+                U, I = self.model.user_num, self.model.item_num
+                self._last = torch.zeros(U + I, dtype=torch.int32, device=self.device)
+                self._ring = torch.zeros(2 * self.LAZY_RING, dtype=torch.float32, device=self.device)
+            if not self.lazy:  # rows are current as of the present step
+                self._last.copy_(self.ctl[1:2].to(torch.int32).expand_as(self._last))
+            L.check(lib.ncf_batch_touched(rows.data_ptr(), n, self.batch_size, self.model.user_num,
+                                          self.model.item_num, self._touched_buf(rows).data_ptr(),
+                                          L.stream_ptr(self.device)), "ncf_batch_touched")
+        self.lazy = lazy
         # layered factored layer 0: the rows of each rank slice by user, once per epoch
         # (the step then sums user runs before its atomics, ncf_user_order)
         self._uses_order = (os.environ.get("NCF_USER_ORDER", "1") == "1"
@@ -223,6 +245,53 @@ class TrainEngine:
             n = rows.numel()  # n int64 entries + n int32 inverse positions (ncf_user_order)
             buf = self._orders[key] = torch.empty(n + (n + 1) // 2, dtype=torch.int64, device=self.device)
         return buf
+
+    # deferred Adam: steps a row may sit out are replayed from this ring of step
+    # scalars (a row's gap is at most one epoch: the last batch brings every row up)
+    LAZY_RING = 1 << 17
+    # on by default where it moves fewer bytes than dense Adam: tables with more rows
+    # than LAZY_RATIO x the global batch (C2, C4, C5; not C3's ml-1m at 65,536)
+    LAZY_RATIO = float(os.environ.get("NCF_LAZY_RATIO", "2"))
+
+    def _lazy_wanted(self):
+        """Deferred Adam for this stream: single-process Adam (the fused optimizer
+        launch), factor_num % 4 == 0, tables <= 2^20 rows, epochs shorter than the
+        ring; NCF_LAZY_ADAM=1 / 0 forces it on / off (auto: tables larger than
+        LAZY_RATIO x the global batch)."""
+        env = os.environ.get("NCF_LAZY_ADAM", "auto")
+        if env == "0" or not self._fused_optimizer:
+            return False
+        U, I = self.model.user_num, self.model.item_num
+        if self.model.factor_num % 4 or U > (1 << 20) or I > (1 << 20) or self.num_batches + 2 > self.LAZY_RING:
+            return False
+        return env == "1" or (U + I) > self.LAZY_RATIO * self.batch_size
+
+    def _touched_buf(self, rows):
+        key = (rows.data_ptr(), rows.numel(), self.batch_size)
+        buf = self._touched.get(key)
+        if buf is None:
+            nbytes = int(L.hip().ncf_touched_bytes(rows.numel(), self.batch_size, self.model.user_num,
+                                                   self.model.item_num))
+            buf = self._touched[key] = torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=self.device)
+        return buf
+
+    def flush(self):
+        """Deferred Adam: every embedding row brought up to the current step (the
+        parameters and moments are then the dense optimizer's).  No-op otherwise."""
+        if not self.lazy:
+            return
+        L.check(L.hip().ncf_lazy_adam_flush(ctypes.byref(self.lay), self.flat.data_ptr(), self.grads.data_ptr(),
+                                            self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self._ranges,
+                                            self._nranges, self.ctl.data_ptr(), self.betas[0], self.betas[1],
+                                            self.eps, self._last.data_ptr(), self._ring.data_ptr(),
+                                            self.LAZY_RING, L.stream_ptr(self.device)), "ncf_lazy_adam_flush")
+
+    def optimizer_state_set(self):
+        """Call after writing flat / exp_avg / exp_avg_sq / ctl from outside (e.g. a
+        loaded or teacher-forced optimizer state): every row is current as of step
+        ctl.adam_t."""
+        if self._last is not None:
+            self._last.copy_(self.ctl[1:2].to(torch.int32).expand_as(self._last))
 
     def user_order_ptr(self):
         """ncf_train_step's user_order argument for the current stream (None: unused)."""
@@ -260,8 +329,8 @@ class TrainEngine:
         lo, hi = D.shard_range(min(self.batch_size, self.n_total - b0), self.world_size, self.rank)
         seg = self.rows[b0 + lo:b0 + hi]
         u = seg & 0xFFFFFFFF
-        u = u[u != 0xFFFFFFFF]  # padding rows
-        return torch.unique(u), torch.unique((seg >> 32) & 0x7FFFFFFF)
+        keep = u != 0xFFFFFFFF  # padding rows (user ~0, item 0x7FFFFFFF) touch nothing
+        return torch.unique(u[keep]), torch.unique(((seg >> 32) & 0x7FFFFFFF)[keep])
 
     def _sparse_exchange(self):
         """dp_mode "sparse": the touched rows' gradients to their owners, the dense
@@ -327,6 +396,16 @@ class TrainEngine:
 
     def _reduce_adam(self):
         st = L.stream_ptr(self.device)
+        if self.lazy:
+            L.check(L.hip().ncf_lazy_adam_step(ctypes.byref(self.lay), self.ws.data_ptr(), self.flat.data_ptr(),
+                                               self.grads.data_ptr(), self.exp_avg.data_ptr(),
+                                               self.exp_avg_sq.data_ptr(), self._ranges, self._nranges,
+                                               self.ctl.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps,
+                                               self.loss_hist.data_ptr(), self.num_batches,
+                                               self._touched_buf(self.rows).data_ptr(), self.n_total,
+                                               self.batch_size, self._last.data_ptr(), self._ring.data_ptr(),
+                                               self.LAZY_RING, st), "ncf_lazy_adam_step")
+            return
         L.check(L.hip().ncf_reduce_adam_step(ctypes.byref(self.lay), self.ws.data_ptr(), self.flat.data_ptr(),
                                              self.grads.data_ptr(), self.exp_avg.data_ptr(),
                                              self.exp_avg_sq.data_ptr(), self._ranges, self._nranges,
@@ -349,7 +428,8 @@ class TrainEngine:
         stream they run on) and return mean milliseconds per launch group."""
         st = torch.cuda.current_stream(self.device)
         if self._fused_optimizer:
-            parts = [("ncf_train_step", self._train_launch), ("ncf_reduce_adam_step", self._reduce_adam)]
+            parts = [("ncf_train_step", self._train_launch),
+                     ("ncf_lazy_adam_step" if self.lazy else "ncf_reduce_adam_step", self._reduce_adam)]
         else:
             parts = [("ncf_train_step", self._train_launch),
                      ("ncf_reduce_slab", lambda: L.check(L.hip().ncf_reduce_slab(
@@ -362,6 +442,7 @@ class TrainEngine:
                 parts.append(("all_gather", self._allgather))
         acc = {k: 0.0 for k, _ in parts}
         evs = []
+        self.flush()  # timing starts from current rows (as a fresh epoch would)
         for _ in range(n_steps):
             e = [torch.cuda.Event(enable_timing=True) for _ in range(len(parts) + 1)]
             e[0].record(st)
@@ -369,6 +450,7 @@ class TrainEngine:
                 fn()
                 e[k + 1].record(st)
             evs.append(e)
+        self.flush()
         torch.cuda.synchronize(self.device)
         for e in evs:
             for k, (name, _) in enumerate(parts):
@@ -470,6 +552,8 @@ class TrainEngine:
                 self.rows = buf
                 if self._uses_order:
                     self._order_buf(buf)  # allocated outside the capture (filled when the buffer is set)
+                if self.lazy:
+                    self._touched_buf(buf)
                 self.capture()
         finally:
             self.rows, self._graph, self._graph_k = cur
@@ -488,7 +572,15 @@ class TrainEngine:
             self._allgather()
 
     def run(self, n_steps, use_graph=True):
-        """n_steps consecutive optimizer steps (batches advance on device)."""
+        """n_steps consecutive optimizer steps (batches advance on device).  With
+        deferred Adam the embedding rows are brought up to the last step at the end
+        (ncf_lazy_adam_flush: a pass over the per-row step counters; rows the last
+        batch of an epoch already caught up cost nothing), so the parameters are the
+        dense optimizer's whenever run() returns."""
+        self._run(n_steps, use_graph)
+        self.flush()
+
+    def _run(self, n_steps, use_graph=True):
         if not use_graph:
             for _ in range(n_steps):
                 self._step_body()
@@ -548,3 +640,5 @@ class TrainEngine:
             self.exp_avg.zero_()
             self.exp_avg_sq.zero_()
         self.ctl[1] = 0
+        if self._last is not None:
+            self._last.zero_()

@@ -46,9 +46,125 @@ def _counts(rng, n_users, n_items, n_ratings, min_per_user=20):
     return c
 
 
+def _first_unique(user, item):
+    """Mask (in draw order) of the first draw of each (user, item) pair."""
+    k = user.astype(np.int64) * (1 << 32) + item.astype(np.int64)
+    order = np.argsort(k, kind="stable")
+    ks = k[order]
+    first = np.ones(len(ks), dtype=bool)
+    first[1:] = ks[1:] != ks[:-1]
+    keep = np.zeros(len(ks), dtype=bool)
+    keep[order[first]] = True
+    return keep
+
+
+def _make_large(n_users, n_items, n_ratings, seed, zipf_a, test_neg):
+    """The same design as make_dataset, vectorised for ml-20m-sized shapes (the
+    per-user Gumbel top-k over every item would draw U x I = 3.7G keys): items per
+    user drawn from the Zipf popularity with replacement and de-duplicated in draw
+    order (more draws until a user has its count; users holding more than a tenth
+    of the items take the exact Gumbel top-k), uniform timestamps, the temporal
+    leave-one-out split and 99 distinct non-interacted test negatives, sorted."""
+    rng = np.random.default_rng(seed)
+    counts = _counts(rng, n_users, n_items, n_ratings)
+    logp = -zipf_a * np.log(np.arange(1, n_items + 1, dtype=np.float64))
+    pop = np.exp(logp - logp.max())
+    cdf = np.cumsum(pop / pop.sum())
+    item_of_rank = rng.permutation(n_items)
+    heavy = counts > n_items // 10
+    users, items = [], []
+    need = np.where(heavy, 0, counts)
+    have = np.zeros(n_users, dtype=np.int64)
+    pool_u = np.zeros(0, dtype=np.int32)
+    pool_i = np.zeros(0, dtype=np.int32)
+    while True:
+        short = need - have
+        todo = np.nonzero(short > 0)[0]
+        if len(todo) == 0:
+            break
+        draws = (short[todo] * 1.25 + 8).astype(np.int64)
+        du = np.repeat(todo.astype(np.int32), draws)
+        di = item_of_rank[np.minimum(np.searchsorted(cdf, rng.random(len(du))), n_items - 1)].astype(np.int32)
+        pool_u = np.concatenate([pool_u, du])
+        pool_i = np.concatenate([pool_i, di])
+        keep = _first_unique(pool_u, pool_i)
+        pool_u, pool_i = pool_u[keep], pool_i[keep]
+        # at most `need` per user, in draw order
+        order = np.argsort(pool_u, kind="stable")
+        su = pool_u[order]
+        start = np.searchsorted(su, np.arange(n_users))
+        rank = np.arange(len(su)) - start[su]
+        ok = rank < need[su]
+        pool_u, pool_i = su[ok], pool_i[order][ok]
+        have = np.bincount(pool_u, minlength=n_users)
+    users.append(pool_u)
+    items.append(pool_i)
+    for u in np.nonzero(heavy)[0]:  # exact sampling without replacement for the heaviest users
+        keys = logp + rng.gumbel(size=n_items)
+        sel = np.argpartition(-keys, counts[u] - 1)[: counts[u]]
+        users.append(np.full(counts[u], u, dtype=np.int32))
+        items.append(item_of_rank[sel].astype(np.int32))
+    u = np.concatenate(users)
+    it = np.concatenate(items)
+    ts = rng.random(len(u))
+    order = np.lexsort((ts, u))  # per user, by timestamp
+    u, it = u[order], it[order]
+    last = np.ones(len(u), dtype=bool)
+    last[:-1] = u[1:] != u[:-1]
+    train_users = (u[~last] + 1).astype(np.int32)
+    train_items = (it[~last] + 1).astype(np.int32)
+    test_users = (u[last] + 1).astype(np.int32)
+    test_items = (it[last] + 1).astype(np.int32)
+    # test negatives: distinct ids in [1, n_items] the user never rated
+    seen = np.sort(u.astype(np.int64) * (n_items + 1) + it + 1)
+    negs = np.zeros((n_users, test_neg), dtype=np.int32)
+    filled = np.zeros(n_users, dtype=np.int64)
+    todo = np.arange(n_users)
+    while len(todo):
+        m = 2 * test_neg
+        cu = np.repeat(todo, m)
+        ci = rng.integers(1, n_items + 1, len(cu))
+        key = cu.astype(np.int64) * (n_items + 1) + ci
+        pos = np.minimum(np.searchsorted(seen, key), len(seen) - 1)
+        ok = seen[pos] != key
+        cu, ci = cu[ok], ci[ok]
+        # drop candidates already chosen for the user, then duplicates, keep draw order
+        prev = np.repeat(np.arange(n_users), test_neg).reshape(n_users, test_neg)[todo]
+        pu = prev.reshape(-1)
+        pi = negs[todo].reshape(-1)
+        pk = filled[todo][:, None] > np.arange(test_neg)[None, :]
+        allu = np.concatenate([pu[pk.reshape(-1)], cu])
+        alli = np.concatenate([pi[pk.reshape(-1)], ci])
+        keep = _first_unique(allu, alli)
+        n_prev = int(pk.sum())
+        cu, ci = cu[keep[n_prev:]], ci[keep[n_prev:]]
+        order = np.argsort(cu, kind="stable")
+        cu, ci = cu[order], ci[order]
+        start = np.searchsorted(cu, np.arange(n_users))
+        rank = np.arange(len(cu)) - start[cu] + filled[cu]
+        ok = rank < test_neg
+        negs[cu[ok], rank[ok]] = ci[ok]
+        filled = np.minimum(test_neg, filled + np.bincount(cu[ok], minlength=n_users))
+        todo = np.nonzero(filled < test_neg)[0]
+    negs.sort(axis=1)
+    return {
+        "train_users": train_users,
+        "train_items": train_items,
+        "test_users": test_users,
+        "test_items": test_items,
+        "test_negatives": negs,
+        "user_num": int(train_users.max()) + 1,
+        "item_num": int(train_items.max()) + 1,
+    }
+
+
 def make_dataset(shape="ml-1m", seed=0, zipf_a=0.8, test_neg=99):
-    """Return a dict of int32 arrays in reference order (see module docstring)."""
+    """Return a dict of int32 arrays in reference order (see module docstring).
+    Shapes above 1G user x item pairs (ml-20m) use the vectorised generator of the
+    same design (_make_large)."""
     n_users, n_items, n_ratings = SHAPES[shape] if isinstance(shape, str) else shape
+    if n_users * n_items > 1_000_000_000:
+        return _make_large(n_users, n_items, n_ratings, seed, zipf_a, test_neg)
     rng = np.random.default_rng(seed)
     counts = _counts(rng, n_users, n_items, n_ratings)
     logp = -zipf_a * np.log(np.arange(1, n_items + 1, dtype=np.float64))

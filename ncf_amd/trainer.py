@@ -139,8 +139,9 @@ class Trainer:
         self.engine.run(self.engine.num_batches, use_graph=self.use_graph)
         return float(np.mean(self.engine.epoch_losses()))
 
-    def _report(self, epoch, avg_loss, hr, ndcg, el, save_fn, snap):
-        self.history.append({"epoch": epoch + 1, "loss": avg_loss, "hr": hr, "ndcg": ndcg, "time": el})
+    def _report(self, epoch, avg_loss, hr, ndcg, el, save_fn, snap, device_time=None):
+        self.history.append({"epoch": epoch + 1, "loss": avg_loss, "hr": hr, "ndcg": ndcg, "time": el,
+                             "device_time": device_time})
         if self.verbose:
             print(f"Epoch {epoch + 1:03d}: Loss={avg_loss:.4f}, HR={hr:.3f}, NDCG={ndcg:.3f}, Time={el:.1f}s")
         if hr > self._best[0]:
@@ -153,12 +154,13 @@ class Trainer:
                         save_fn(self.model)
 
     def _report_pending(self, pending, save_fn):
-        epoch, ev0, ev1, out, snap = pending
+        epoch, ev0, ev1, out, snap, t0 = pending
         ev1.synchronize()
+        wall = time.time() - t0  # like the reference: from the epoch's start to its metrics
         avg_loss = float(np.mean(out["loss"].numpy().astype(np.float64)))
         hr = float(np.mean(out["hr"].numpy().astype(np.float64)))
         ndcg = float(np.mean(out["nd"].numpy().astype(np.float64)))
-        self._report(epoch, avg_loss, hr, ndcg, ev0.elapsed_time(ev1) / 1e3, save_fn, snap)
+        self._report(epoch, avg_loss, hr, ndcg, wall, save_fn, snap, ev0.elapsed_time(ev1) / 1e3)
 
     def fit(self, epochs, model_type=None, pretraining=False, save_fn=None):
         """The reference loop (train_neumf.py:98-144).  Single rank: epoch e's loss,
@@ -166,7 +168,9 @@ class Trainer:
         save_fn, the parameters to a device snapshot), epoch e + 1 is enqueued, and
         only then is epoch e read back, printed and checkpointed -- the same values,
         the same generator draws in the same order, no idle device between epochs.
-        Time= is the epoch's device time (steps + evaluation)."""
+        Time= (history "time") is wall-clock from the epoch's start to its metrics
+        being read back, as train_neumf.py:100,130 measures it; history
+        "device_time" is the epoch's device time (steps + evaluation)."""
         self._best = [0, 0, 0]  # hr, ndcg, epoch
         if self.world_size > 1:  # the loss readback is a collective there: in line
             for epoch in range(int(epochs)):
@@ -185,6 +189,7 @@ class Trainer:
             pending = None
             for epoch in range(int(epochs)):
                 self.model.train()
+                t0 = time.time()
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev0.record()
                 rows = self._epoch_stream()
@@ -204,7 +209,7 @@ class Trainer:
                 ev1.record()
                 if pending is not None:
                     self._report_pending(pending, save_fn)
-                pending = (epoch, ev0, ev1, out, snap)
+                pending = (epoch, ev0, ev1, out, snap, t0)
             if pending is not None:
                 self._report_pending(pending, save_fn)
         best_hr, best_ndcg, best_epoch = self._best

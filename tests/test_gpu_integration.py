@@ -23,7 +23,7 @@ def _binding():
     text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     sec = text.split("## 2.", 1)[1].split("\n## 3.", 1)[0]
     blocks = re.findall(r"```python\n(.*?)```", sec, re.S)
-    assert len(blocks) == 2, "INTEGRATION.md section 2 must hold the train and distill stubs"
+    assert len(blocks) == 3, "INTEGRATION.md section 2 must hold the train, distill and deferred-Adam stubs"
     lib = os.path.join(ROOT, "ncf_amd", "libncf_hip.so")
     ns = {}
     for b in blocks:
@@ -111,3 +111,46 @@ def test_documented_distill_step_vs_reference(golden):
     for k, v in student.state_dict().items():
         np.testing.assert_allclose(v.cpu().numpy(), g[f"cli_feature::student_t5::{k}"], rtol=1e-4, atol=1e-6,
                                    err_msg=k)
+
+
+def test_documented_deferred_adam_steps_vs_oracle():
+    """The section-2 deferred-Adam stub (ncf_batch_touched, ncf_lazy_adam_step,
+    ncf_lazy_adam_flush) on a C2-shaped stream (ml-1m ids, bs 1,024: each batch
+    touches a fraction of the rows): 6 steps, flushed, vs 6 steps of the oracle's
+    torch.optim.Adam on the same batches."""
+    from ncf_amd import ops
+    from ncf_amd.models import NCF
+    ns = _binding()
+    U, I, f, Lyr, B, T = 6041, 3707, 8, 3, 1024, 6
+    torch.manual_seed(9)
+    ref = O.OracleNCF(U, I, f, Lyr, 0.0, "NeuMF-end")
+    torch.manual_seed(9)
+    m = NCF(U, I, f, Lyr, 0.0, "NeuMF-end").to(DEV)
+    flat, _ = ops.ensure_flat(m)
+    lay = ns["layout"](m)
+    ns["_lib"].ncf_layout_tune(ctypes.byref(lay), B)
+    rng = np.random.default_rng(23)
+    n = B * T
+    users = rng.integers(1, U, n)
+    items = np.minimum(rng.zipf(1.3, n), I - 1)
+    labels = (rng.random(n) < 0.2).astype(np.int64)
+    rows = ns["pack"](torch.as_tensor(users, device=DEV), torch.as_tensor(items, device=DEV),
+                      torch.as_tensor(labels, device=DEV))
+    touched = ns["touched_lists"](rows, B, lay)
+    last, ring = ns["lazy_state"](lay, DEV)
+    grads = torch.zeros(int(lay.total), device=DEV)
+    mom, vel = torch.zeros_like(grads), torch.zeros_like(grads)
+    ctl = torch.tensor([0, 0, n, 0, 0, 0], dtype=torch.int64, device=DEV)
+    ws = ns["workspace"](ns["_lib"].ncf_workspace_bytes(ctypes.byref(lay), B), DEV)
+    rg = _ranges(m, lay)
+    for _ in range(T - 1):  # stop before the epoch's last batch: rows left behind until the flush
+        ns["train_step_lazy"](flat, grads, mom, vel, lay, rows, ctl, ws, B, rg, touched, last, ring)
+    ns["flush"](flat, grads, mom, vel, lay, ctl, rg, last, ring)
+    torch.cuda.synchronize()
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    O.train_steps(ref, opt, [users[k * B:(k + 1) * B] for k in range(T - 1)],
+                  [items[k * B:(k + 1) * B] for k in range(T - 1)], [labels[k * B:(k + 1) * B] for k in range(T - 1)])
+    for (k, v), (_, r) in zip(m.state_dict().items(), ref.state_dict().items()):
+        np.testing.assert_allclose(v.cpu().numpy(), r.numpy(), rtol=1e-4, atol=2e-5, err_msg=k)
+    assert ctl.cpu().tolist()[:2] == [T - 1, T - 1]
+    assert int(last.min()) == T - 1 and float(grads.abs().max()) == 0.0

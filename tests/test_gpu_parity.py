@@ -333,6 +333,7 @@ def _teacher_forced_steps(ref, m, eng, users, items, labels, lr=1e-3):
         ties += len(tie_u)
         eng.ctl[0] = t
         eng.ctl[1] = t
+        eng.optimizer_state_set()  # deferred Adam: every row current as of step t
         eng.run(1, use_graph=False)
         losses = O.train_steps(ref, opt, [users[t]], [items[t]], [labels[t]])
         torch.cuda.synchronize()
