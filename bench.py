@@ -137,6 +137,38 @@ def adam_info(kt, eng, model):
                 "bytes_detail": {"embedding_adam": 32 * emb, "tower_adam": 24 * tower,
                                  "slab_read": slab_rows * slab_cols * 4, "w0_partials_read": partial},
                 "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}
+    if "ncf_lazy_adam_step" in kt or "ncf_lazy_adam_step_packed" in kt:
+        # deferred Adam: the rows of batches b and b + 1 per step (every row on an
+        # epoch's last batch), from the epoch's touched lists
+        key = "ncf_lazy_adam_step" if "ncf_lazy_adam_step" in kt else "ncf_lazy_adam_step_packed"
+        ms = kt[key]
+        t = eng._touched_buf(eng.rows).cpu().numpy()
+        U, I = model.user_num, model.item_num
+        nb = eng.num_batches
+        su, si = min(U, eng.batch_size), min(I, eng.batch_size)
+        cnt = t[nb * (su + si): nb * (su + si) + 2 * nb].reshape(nb, 2)
+        lists = [(t[b * su: b * su + cnt[b, 0]], t[nb * su + b * si: nb * su + b * si + cnt[b, 1]]) for b in range(nb)]
+        wu = sum(p.numel() // U for p, a in zip(list(model.ordered_params())[:4], ops.active_mask(model)[:4])
+                 if a and p.shape[0] == U)
+        wi = sum(p.numel() // I for p, a in zip(list(model.ordered_params())[:4], ops.active_mask(model)[:4])
+                 if a and p.shape[0] == I)
+        rows_u = rows_i = grad_rows = 0
+        for b in range(nb):
+            grad_rows += len(lists[b][0]) * wu + len(lists[b][1]) * wi
+            if b + 1 < nb:
+                rows_u += len(np.union1d(lists[b][0], lists[b + 1][0]))
+                rows_i += len(np.union1d(lists[b][1], lists[b + 1][1]))
+            else:
+                rows_u += U
+                rows_i += I
+        moved = (rows_u * wu + rows_i * wi) / nb  # embedding floats read and written per step
+        b = 24 * moved + 8 * grad_rows / nb + 24 * tower + slab_rows * slab_cols * 4 + partial
+        return {"kernel": f"{key} (tower slab reduce + Adam, deferred embedding Adam)", "params": emb + tower,
+                "embedding_floats_moved_per_step": moved, "dense_embedding_floats": emb,
+                "bytes": b, "bytes_note": "p, m, v read + written (24 B) per embedding float of the rows of batches "
+                                          "b and b + 1 (every row on the epoch's last batch), their gradient read + "
+                                          "cleared (8 B) for batch b's rows, the tower as ncf_reduce_adam_step",
+                "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}
     b = 32 * (emb + tower)
     ms = kt["optimizer"]
     return {"kernel": "ncf_adam_step", "params": emb + tower, "bytes": b, "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}

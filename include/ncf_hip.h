@@ -334,6 +334,32 @@ int ncf_lazy_adam_flush(const ncf_layout *lay, float *params, float *grads, floa
                         double beta1, double beta2, double eps, int32_t *last_step,
                         const float *step_scalars, int64_t ring, void *stream);
 
+/*
+ * Data-parallel deferred Adam (dp_mode "touched"; since ABI 13).  Every rank knows
+ * the global batch, so every rank holds the same sorted lists of the rows batch b
+ * touches (ncf_batch_touched) and packs its partial gradient of exactly those rows,
+ * in list order, into one buffer of ncf_touched_packed_floats(lay, ranges, nranges,
+ * batch_global) floats:
+ *   [min(U, B)] user rows ((Ug active ? f : 0) + (Um active ? dm : 0) floats each),
+ *   [min(I, B)] item rows, then ncf_slab_stride floats of tower gradient (+ loss).
+ * ncf_touched_pack (after ncf_train_step): the slab / W0 partial reduction into the
+ * tail, the rows into the list slots (slots past the batch's count zeroed), those
+ * rows of grads cleared, stamp[row] (int64 [U + I]) = t << 32 | slot.  Then one
+ * all-reduce (sum) of the whole buffer, and ncf_lazy_adam_step_packed -- the
+ * deferred Adam of ncf_lazy_adam_step with batch b's gradients (and the tower's)
+ * read from the summed buffer, the same on every rank: no parameter all-gather.
+ */
+int64_t ncf_touched_packed_floats(const ncf_layout *lay, const int64_t *ranges, int nranges, int64_t batch_global);
+int ncf_touched_pack(const ncf_layout *lay, const void *workspace, float *grads, const int64_t *ranges,
+                     int nranges, const int32_t *touched, int64_t n_total, int64_t batch_global,
+                     const ncf_step_ctl *ctl, float *packed, int64_t *stamp, void *stream);
+int ncf_lazy_adam_step_packed(const ncf_layout *lay, float *params, float *exp_avg, float *exp_avg_sq,
+                              const int64_t *ranges, int nranges, ncf_step_ctl *ctl, double lr, double beta1,
+                              double beta2, double eps, float *loss_hist, int64_t hist_len,
+                              const int32_t *touched, int64_t n_total, int64_t batch_global,
+                              int32_t *last_step, float *step_scalars, int64_t ring, const float *packed,
+                              const int64_t *stamp, void *stream);
+
 /* Plain SGD p -= lr * g (optim.SGD(lr*10) on the --pretraining path, train_neumf.py:87-88). */
 int ncf_sgd_step(float *params, float *grads, const int64_t *ranges, int nranges,
                  ncf_step_ctl *ctl, double lr, int64_t loss_slot, float *loss_hist, int64_t hist_len,

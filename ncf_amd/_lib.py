@@ -110,6 +110,13 @@ _HIP_PROTOS = {
                                           ctypes.POINTER(c_i64), ctypes.c_int, c_vp,
                                           ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                           c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "ncf_touched_packed_floats": (c_i64, [ctypes.POINTER(NcfLayout), ctypes.POINTER(c_i64), ctypes.c_int, c_i64]),
+    "ncf_touched_pack": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.c_int,
+                                        c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "ncf_lazy_adam_step_packed": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, ctypes.POINTER(c_i64),
+                                                 ctypes.c_int, c_vp, ctypes.c_double, ctypes.c_double,
+                                                 ctypes.c_double, ctypes.c_double, c_vp, c_i64, c_vp, c_i64, c_i64,
+                                                 c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "ncf_lazy_adam_flush": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp,
                                            ctypes.POINTER(c_i64), ctypes.c_int, c_vp,
                                            ctypes.c_double, ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_i64,

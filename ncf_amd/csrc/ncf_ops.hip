@@ -219,7 +219,8 @@ __device__ __forceinline__ void tower_reduce_adam_block(const float* __restrict_
                                                         float* __restrict__ m, float* __restrict__ v, const Ranges& R,
                                                         int64_t t_step, int64_t b_step, double lr, double beta1,
                                                         double beta2, float eps, float* loss_hist, int64_t hist_len,
-                                                        const W0Part& wp, float* sc, f4 (*part)[16]) {
+                                                        const W0Part& wp, float* sc, f4 (*part)[16],
+                                                        const float* __restrict__ pre = nullptr) {
 #pragma clang fp contract(off)
     const float w1 = (float)(1.0 - beta1);
     const float b2 = (float)beta2;
@@ -236,7 +237,9 @@ __device__ __forceinline__ void tower_reduce_adam_block(const float* __restrict_
         vv = *reinterpret_cast<const f4*>(v + i);
     }
     f4 s = f4{0.f, 0.f, 0.f, 0.f};
-    if (j < wp.cols) {
+    if (pre != nullptr) {  // the summed (all-reduced) tower gradient: tail of the packed buffer
+        if (rg == 0 && j < stride) s = *reinterpret_cast<const f4*>(pre + j);
+    } else if (j < wp.cols) {
         s = w0_part_sum(wp, j, rg);
     } else if (j < stride) {
         const float* q = slab + (int64_t)rg * stride + j;
@@ -257,10 +260,12 @@ __device__ __forceinline__ void tower_reduce_adam_block(const float* __restrict_
     const float neg_step = sc[0], bc2s = sc[1];
     if (rg == 0 && j < stride) {
         f4 gs = part[0][c4];
+        if (pre == nullptr) {
 #pragma unroll
-        for (int q = 1; q < 16; ++q) {
-            const f4 x = part[q][c4];
-            gs.x += x.x; gs.y += x.y; gs.z += x.z; gs.w += x.w;
+            for (int q = 1; q < 16; ++q) {
+                const f4 x = part[q][c4];
+                gs.x += x.x; gs.y += x.y; gs.z += x.z; gs.w += x.w;
+            }
         }
         if (j == tower_len) {
             if (loss_hist != nullptr && hist_len > 0) loss_hist[((b_step % hist_len) + hist_len) % hist_len] = gs.x;
@@ -352,6 +357,13 @@ struct LazyArgs {
     int32_t* last;  // [U + I]
     float* ring;    // [ring_n][2]
     int64_t ring_n;
+    // packed mode (data parallel, ncf_touched_pack): batch b's rows' summed gradients
+    // at packed[k * wrow[side] + ...] (k = position in batch b's list, users first),
+    // stamp[row] = t << 32 | k for those rows
+    const float* packed;
+    const int64_t* stamp;
+    int64_t pk_items;  // float offset of the item rows
+    int wrow[2];       // floats per packed user / item row
 };
 
 constexpr int LZ_GROUP = 16;  // lanes per claimed row
@@ -377,23 +389,36 @@ __device__ __forceinline__ void lazy_rows(const LazyArgs& a, int64_t t, int64_t 
         } else {
             side = 1; id = next ? a.touched[a.nb * a.su + (b + 1) * a.si + (w - n0 - n1 - n2)] : (int)(w - n0 - n1 - n2);
         }
+        const int64_t slot = side ? a.U + id : id;
         int old = 0;
+        const bool in_b = w < n0 + n1;  // a row of batch b (its gradient: grads, or packed row w)
         if (glane == 0) {
-            int32_t* lp = a.last + (side ? a.U + id : id);
+            int32_t* lp = a.last + slot;
             old = *lp;
-            if (old < (int)t) old = atomicMax(lp, (int)t);
+            if (a.packed != nullptr) {
+                // each row has exactly one work item: batch b's list, or the second list
+                // for rows batch b does not hold (stamped by ncf_touched_pack)
+                if (!in_b && (a.stamp[slot] >> 32) == t) old = (int)t;
+                else if (old < (int)t) *lp = (int)t;
+            } else if (old < (int)t) {
+                old = atomicMax(lp, (int)t);
+            }
         }
         old = __shfl(old, threadIdx.x & ~(LZ_GROUP - 1), 64);
         if (old >= (int)t) continue;
         const int sa = side, sb = side + 2;  // g table, m table of this side
         const int wa = a.off[sa] >= 0 ? a.w4[sa] : 0, wb = a.off[sb] >= 0 ? a.w4[sb] : 0;
+        const float* prow = nullptr;  // packed mode: the row's summed gradient (batch b's rows)
+        if (a.packed != nullptr && in_b)
+            prow = a.packed + (side ? a.pk_items + (w - n0) * a.wrow[1] : w * a.wrow[0]);
         for (int k = glane; k < wa + wb; k += LZ_GROUP) {
             const int64_t e = k < wa ? a.off[sa] + ((int64_t)id * a.w4[sa] + k) * 4
                                      : a.off[sb] + ((int64_t)id * a.w4[sb] + (k - wa)) * 4;
             f4 pp = *reinterpret_cast<const f4*>(a.p + e);
             f4 mm = *reinterpret_cast<const f4*>(a.m + e);
             f4 vv = *reinterpret_cast<const f4*>(a.v + e);
-            const f4 gg = *reinterpret_cast<const f4*>(a.g + e);
+            const f4 gg = a.packed == nullptr ? *reinterpret_cast<const f4*>(a.g + e)
+                        : (prow != nullptr ? *reinterpret_cast<const f4*>(prow + 4 * k) : zero);
             for (int s = old + 1; s < (int)t; ++s) {  // the steps this row sat out: g = 0
                 const float* sc = a.ring + 2 * (s % a.ring_n);
                 adam_f4(pp, mm, vv, zero, w1, b2, omb2, sc[1], eps, sc[0]);
@@ -402,7 +427,8 @@ __device__ __forceinline__ void lazy_rows(const LazyArgs& a, int64_t t, int64_t 
             *reinterpret_cast<f4*>(a.m + e) = mm;
             *reinterpret_cast<f4*>(a.v + e) = vv;
             *reinterpret_cast<f4*>(a.p + e) = pp;
-            if (gg.x != 0.f || gg.y != 0.f || gg.z != 0.f || gg.w != 0.f) *reinterpret_cast<f4*>(a.g + e) = zero;
+            if (a.packed == nullptr && (gg.x != 0.f || gg.y != 0.f || gg.z != 0.f || gg.w != 0.f))
+                *reinterpret_cast<f4*>(a.g + e) = zero;
         }
     }
 }
@@ -419,7 +445,8 @@ __global__ __launch_bounds__(256) void lazy_adam_kernel(const float* __restrict_
     const int64_t b_step = ctl->snap_batch;
     if ((int)blockIdx.x < nA) {
         tower_reduce_adam_block(slab, lo, stride, rows, tb, tower_len, a.p, a.m, a.v, R, t_step, b_step, lr, beta1,
-                                beta2, eps, loss_hist, hist_len, wp, sc, part);
+                                beta2, eps, loss_hist, hist_len, wp, sc, part,
+                                a.packed != nullptr ? a.packed + a.pk_items + a.si * a.wrow[1] : nullptr);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             a.ring[2 * (t_step % a.ring_n)] = sc[0];
             a.ring[2 * (t_step % a.ring_n) + 1] = sc[1];
@@ -501,6 +528,41 @@ __global__ __launch_bounds__(BT_THREADS) void batch_touched_kernel(const uint64_
         }
     }
     if (threadIdx.x == BT_THREADS - 1) out[nb * (su + si) + 2 * b + side] = base + incl;
+}
+
+// ncf_touched_pack: this rank's gradient of batch b's rows (users, then items; each
+// row its active tables' floats, g table first) into packed rows in list order,
+// the rows of grads cleared, stamp[row] = t << 32 | k; list slots past the batch's
+// count are zeroed so the all-reduce adds nothing stale.  One group per row slot.
+__global__ __launch_bounds__(256) void touched_pack_kernel(const ncf_step_ctl* __restrict__ ctl, LazyArgs a,
+                                                           float* __restrict__ packed) {
+    const int glane = threadIdx.x & (LZ_GROUP - 1);
+    const int64_t t = ctl->snap_t;
+    const int64_t b = ((ctl->snap_batch % a.nb) + a.nb) % a.nb;
+    const int32_t* cnt = a.touched + a.nb * (a.su + a.si);
+    const int64_t nu = cnt[2 * b], ni = cnt[2 * b + 1];
+    const int64_t groups = (int64_t)gridDim.x * (blockDim.x / LZ_GROUP);
+    const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t w = (int64_t)blockIdx.x * (blockDim.x / LZ_GROUP) + threadIdx.x / LZ_GROUP; w < a.su + a.si;
+         w += groups) {
+        const int side = w < a.su ? 0 : 1;
+        const int64_t k = side ? w - a.su : w;
+        float* dst = packed + (side ? a.pk_items + k * a.wrow[1] : k * a.wrow[0]);
+        const int sa = side, sb = side + 2;
+        const int wa = a.off[sa] >= 0 ? a.w4[sa] : 0, wb = a.off[sb] >= 0 ? a.w4[sb] : 0;
+        if (k >= (side ? ni : nu)) {
+            for (int c = glane; c < wa + wb; c += LZ_GROUP) *reinterpret_cast<f4*>(dst + 4 * c) = zero;
+            continue;
+        }
+        const int id = side ? a.touched[a.nb * a.su + b * a.si + k] : a.touched[b * a.su + k];
+        if (glane == 0) const_cast<int64_t*>(a.stamp)[side ? a.U + id : id] = (t << 32) | k;
+        for (int c = glane; c < wa + wb; c += LZ_GROUP) {
+            const int64_t e = c < wa ? a.off[sa] + ((int64_t)id * a.w4[sa] + c) * 4
+                                     : a.off[sb] + ((int64_t)id * a.w4[sb] + (c - wa)) * 4;
+            *reinterpret_cast<f4*>(dst + 4 * c) = *reinterpret_cast<const f4*>(a.g + e);
+            *reinterpret_cast<f4*>(a.g + e) = zero;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1739,6 +1801,91 @@ int ncf_lazy_adam_step(const ncf_layout* lay, const void* workspace, float* para
     hipLaunchKernelGGL(lazy_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
                        static_cast<const float*>(workspace), lo, stride, rows, nA, lay->tower_begin, lay->tower_len, R,
                        ctl, lr, beta1, beta2, (float)eps, loss_hist, hist_len, w0_part(lay, workspace), a);
+    return launch_status();
+}
+
+// packed mode geometry: floats per packed user / item row, the item rows' offset,
+// the tail (tower gradient + loss, ncf_slab_stride floats) and the total
+static int packed_geometry(const ncf_layout* lay, const LazyArgs& a, int64_t su, int64_t si, int* wrow,
+                           int64_t* pk_items, int64_t* tail, int64_t* total) {
+    wrow[0] = 4 * ((a.off[0] >= 0 ? a.w4[0] : 0) + (a.off[2] >= 0 ? a.w4[2] : 0));
+    wrow[1] = 4 * ((a.off[1] >= 0 ? a.w4[1] : 0) + (a.off[3] >= 0 ? a.w4[3] : 0));
+    *pk_items = su * wrow[0];
+    *tail = *pk_items + si * wrow[1];
+    *total = *tail + ncf_slab_stride(lay);
+    return NCF_OK;
+}
+
+int64_t ncf_touched_packed_floats(const ncf_layout* lay, const int64_t* ranges, int nranges, int64_t batch_global) {
+    if (!lay || !ranges || batch_global <= 0) return -1;
+    LazyArgs a;
+    if (lazy_args(lay, nullptr, nullptr, nullptr, nullptr, ranges, nranges, nullptr, nullptr, 1, &a) != NCF_OK)
+        return -1;
+    int64_t nb, su, si, pk, tail, total;
+    int wrow[2];
+    touched_shape(1, batch_global, lay->user_num, lay->item_num, &nb, &su, &si);
+    packed_geometry(lay, a, su, si, wrow, &pk, &tail, &total);
+    return total;
+}
+
+int ncf_touched_pack(const ncf_layout* lay, const void* workspace, float* grads, const int64_t* ranges, int nranges,
+                     const int32_t* touched, int64_t n_total, int64_t batch_global, const ncf_step_ctl* ctl,
+                     float* packed, int64_t* stamp, void* stream) {
+    if (!lay || !workspace || !grads || !ranges || !touched || !ctl || !packed || !stamp || n_total <= 0 ||
+        batch_global <= 0)
+        return NCF_E_ARG;
+    LazyArgs a;
+    const int rc = lazy_args(lay, nullptr, grads, nullptr, nullptr, ranges, nranges, nullptr, nullptr, 1, &a);
+    if (rc != NCF_OK) return rc;
+    touched_shape(n_total, batch_global, lay->user_num, lay->item_num, &a.nb, &a.su, &a.si);
+    a.touched = touched;
+    a.stamp = stamp;
+    int64_t tail, total;
+    packed_geometry(lay, a, a.su, a.si, a.wrow, &a.pk_items, &tail, &total);
+    // tower gradient (slab rows, W0 partials; loss at tower_len) into the tail
+    const int stride = (int)ncf_slab_stride(lay);
+    const int lo = slab_lo(lay);
+    hipLaunchKernelGGL(reduce_slab_kernel, dim3((stride - lo + 63) / 64), dim3(256), 0, (hipStream_t)stream,
+                       static_cast<const float*>(workspace), packed + tail, lo, stride, reduce_rows(lay),
+                       (ncf_step_ctl*)nullptr, w0_part(lay, workspace));
+    // tail[0, lo) is never written: it stays as allocated (zero), and sums to zero
+    int64_t nB = (a.su + a.si + (256 / LZ_GROUP) - 1) / (256 / LZ_GROUP);
+    if (nB > 2048) nB = 2048;
+    hipLaunchKernelGGL(touched_pack_kernel, dim3((unsigned)nB), dim3(256), 0, (hipStream_t)stream, ctl, a, packed);
+    return launch_status();
+}
+
+int ncf_lazy_adam_step_packed(const ncf_layout* lay, float* params, float* exp_avg, float* exp_avg_sq,
+                              const int64_t* ranges, int nranges, ncf_step_ctl* ctl, double lr, double beta1,
+                              double beta2, double eps, float* loss_hist, int64_t hist_len, const int32_t* touched,
+                              int64_t n_total, int64_t batch_global, int32_t* last_step, float* step_scalars,
+                              int64_t ring, const float* packed, const int64_t* stamp, void* stream) {
+    if (!lay || !params || !exp_avg || !exp_avg_sq || !ranges || !ctl || !touched || !last_step || !step_scalars ||
+        !packed || !stamp || n_total <= 0 || batch_global <= 0)
+        return NCF_E_ARG;
+    int err = 0;
+    Ranges R = make_ranges(ranges, nranges, &err);
+    if (err) return NCF_E_ARG;
+    LazyArgs a;
+    const int rc = lazy_args(lay, params, nullptr, exp_avg, exp_avg_sq, ranges, nranges, last_step, step_scalars,
+                             ring, &a);
+    if (rc != NCF_OK) return rc;
+    touched_shape(n_total, batch_global, lay->user_num, lay->item_num, &a.nb, &a.su, &a.si);
+    if (ring < a.nb + 2) return NCF_E_ARG;
+    a.touched = touched;
+    a.packed = packed;
+    a.stamp = stamp;
+    int64_t tail, total;
+    packed_geometry(lay, a, a.su, a.si, a.wrow, &a.pk_items, &tail, &total);
+    const int stride = (int)ncf_slab_stride(lay);
+    const int lo = slab_lo(lay);
+    const int nA = (stride - lo + 63) / 64;
+    const int64_t work = 2 * (a.su + a.si) > a.su + a.si + a.U + a.I ? 2 * (a.su + a.si) : a.su + a.si + a.U + a.I;
+    int64_t nB = (work + (256 / LZ_GROUP) - 1) / (256 / LZ_GROUP);
+    if (nB > 2048) nB = 2048;
+    hipLaunchKernelGGL(lazy_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)nullptr, lo, stride, 0, nA, lay->tower_begin, lay->tower_len, R, ctl, lr, beta1,
+                       beta2, (float)eps, loss_hist, hist_len, W0Part{nullptr, 0, 0, 0, 0}, a);
     return launch_status();
 }
 

@@ -63,10 +63,10 @@ class HostSampler:
         redone sequentially, threads, blocks, ns: words / walk / end state / chain,
         window bits) of this sampler."""
         import ctypes
-        out = (ctypes.c_int64 * 11)()
-        L.sampler_lib().ncf_sampler_stats(self._h, out, 11)
+        out = (ctypes.c_int64 * 13)()
+        L.sampler_lib().ncf_sampler_stats(self._h, out, 13)
         keys = ("parallel", "sequential", "run_fallbacks", "epoch_fallbacks", "threads", "blocks",
-                "words_ns", "walk_ns", "end_ns", "chain_ns", "window_bits")
+                "words_ns", "walk_ns", "end_ns", "chain_ns", "window_bits", "tab_thread_ns", "fin_thread_ns")
         return dict(zip(keys, list(out)))
 
     def __del__(self):
@@ -107,8 +107,10 @@ class HostSampler:
 
 
 def sampler_threads():
-    """Threads of a host sampler pool: NCF_SAMPLER_THREADS, else min(16, 3/4 of the
-    CPUs this process may run on) -- a GPU box grants 16 CPUs per GPU."""
+    """Threads of a host sampler pool: NCF_SAMPLER_THREADS, else min(8, half the CPUs
+    this process may run on) -- a GPU box grants 16 CPUs per GPU, and the rest are
+    the training loop's (graph replays, the epoch pipeline's staging, the HIP runtime):
+    the pool only has to finish an epoch's draws while the previous epoch trains."""
     import os
     v = os.environ.get("NCF_SAMPLER_THREADS")
     if v:
@@ -117,7 +119,7 @@ def sampler_threads():
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(16, (3 * n) // 4))
+    return max(1, min(8, n // 2))
 
 
 def _membership_from(train_mat, features):

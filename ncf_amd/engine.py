@@ -71,7 +71,13 @@ class TrainEngine:
     ALLREDUCE_MAX_FLOATS = 4 << 20
 
     @classmethod
-    def default_dp_mode(cls, total_floats):
+    def default_dp_mode(cls, total_floats, touched_ok=False):
+        """world > 1: "touched" (the rows each global batch touches, packed and
+        all-reduced, then replicated deferred Adam: no parameter all-gather) where the
+        model supports deferred Adam; else one all-reduce up to ALLREDUCE_MAX_FLOATS,
+        zero1 above."""
+        if touched_ok:
+            return "touched"
         return "allreduce" if total_floats <= cls.ALLREDUCE_MAX_FLOATS else "zero1"
 
     def __init__(self, model, lr=1e-3, optimizer="adam", betas=(0.9, 0.999), eps=1e-8,
@@ -83,13 +89,17 @@ class TrainEngine:
         self.distill = distill
         self.world_size, self.rank, self.group = int(world_size), int(rank), process_group
         lay = L.layout(model.user_num, model.item_num, model.factor_num, model.num_layers, model.model_type)
+        touched_ok = (optimizer == "adam" and model.factor_num % 4 == 0 and model.user_num <= (1 << 20)
+                      and model.item_num <= (1 << 20))
         if dp_mode is None:
-            dp_mode = os.environ.get("NCF_DP_MODE", self.default_dp_mode(int(lay.total))) \
+            dp_mode = os.environ.get("NCF_DP_MODE", self.default_dp_mode(int(lay.total), touched_ok)) \
                 if self.world_size > 1 else "single"
         # an explicit exchange mode stands at world 1 (a one-rank group still runs the
         # real collectives: how the captured-collective graph is tested on one GPU)
-        if dp_mode not in ("single", "zero1", "allreduce", "sparse"):
+        if dp_mode not in ("single", "zero1", "allreduce", "sparse", "touched"):
             raise ValueError(f"dp_mode {dp_mode!r}")
+        if dp_mode == "touched" and not touched_ok:
+            raise ValueError("dp_mode 'touched' needs Adam, factor_num % 4 == 0 and tables of <= 2^20 rows")
         self.dp_mode = dp_mode
         if dp_mode in ("zero1", "sparse"):
             # flat buffers padded to world x shard floats; rank r owns [r*S, (r+1)*S)
@@ -169,7 +179,12 @@ class TrainEngine:
         self.lazy = False
         self._last = None
         self._ring = None
-        self._touched = {}
+        self._touched_lists = {}
+        if dp_mode == "touched":  # packed gradients of the touched rows + tower, all-reduced
+            self._packed = torch.zeros(int(L.hip().ncf_touched_packed_floats(ctypes.byref(self.lay), self._ranges,
+                                                                             self._nranges, 1)),
+                                       dtype=torch.float32, device=dev)  # resized per batch size
+            self._stamp = torch.zeros(model.user_num + model.item_num, dtype=torch.int64, device=dev)
 
     # ------------------------------------------------------------------ data
     def set_epoch_stream(self, rows, batch_size, checked=False):
@@ -211,6 +226,12 @@ class TrainEngine:
         lazy = self._lazy_wanted()
         if self.lazy and not lazy:
             self.flush()  # back to dense Adam: every row current first
+        if self.dp_mode == "touched":
+            pf = int(L.hip().ncf_touched_packed_floats(ctypes.byref(self.lay), self._ranges, self._nranges,
+                                                       self.batch_size))
+            if self._packed.numel() != pf:
+                self._packed = torch.zeros(pf, dtype=torch.float32, device=self.device)
+                self._drop_graphs()
         if lazy:
             lib = L.hip()
             if self._last is None:
@@ -258,6 +279,8 @@ class TrainEngine:
         launch), factor_num % 4 == 0, tables <= 2^20 rows, epochs shorter than the
         ring; NCF_LAZY_ADAM=1 / 0 forces it on / off (auto: tables larger than
         LAZY_RATIO x the global batch)."""
+        if self.dp_mode == "touched":
+            return True
         env = os.environ.get("NCF_LAZY_ADAM", "auto")
         if env == "0" or not self._fused_optimizer:
             return False
@@ -268,11 +291,11 @@ class TrainEngine:
 
     def _touched_buf(self, rows):
         key = (rows.data_ptr(), rows.numel(), self.batch_size)
-        buf = self._touched.get(key)
+        buf = self._touched_lists.get(key)
         if buf is None:
             nbytes = int(L.hip().ncf_touched_bytes(rows.numel(), self.batch_size, self.model.user_num,
                                                    self.model.item_num))
-            buf = self._touched[key] = torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=self.device)
+            buf = self._touched_lists[key] = torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=self.device)
         return buf
 
     def flush(self):
@@ -303,9 +326,18 @@ class TrainEngine:
 
     # ------------------------------------------------------------------ step
     def _compute(self):
-        """Launches 1-2: fused (or layered) step + slab reduction (advances ctl)."""
+        """Launches 1-2: fused (or layered) step + slab reduction (advances ctl);
+        dp_mode "touched": step + ncf_touched_pack (the touched rows' and the tower's
+        gradients into the buffer the all-reduce sums; ctl advances in the optimizer)."""
         st = L.stream_ptr(self.device)
         self._train_launch()
+        if self.dp_mode == "touched":
+            L.check(L.hip().ncf_touched_pack(ctypes.byref(self.lay), self.ws.data_ptr(), self.grads.data_ptr(),
+                                             self._ranges, self._nranges, self._touched_buf(self.rows).data_ptr(),
+                                             self.n_total, self.batch_size, self.ctl.data_ptr(),
+                                             self._packed.data_ptr(), self._stamp.data_ptr(), st),
+                    "ncf_touched_pack")
+            return
         L.check(L.hip().ncf_reduce_slab(ctypes.byref(self.lay), self.ws.data_ptr(), self.grads.data_ptr(),
                                         self.ctl.data_ptr(), st), "ncf_reduce_slab")
 
@@ -315,7 +347,9 @@ class TrainEngine:
         allreduce: in-place sum of the whole flat gradient."""
         if self.dp_mode == "single":
             return
-        if self.dp_mode == "zero1":
+        if self.dp_mode == "touched":
+            D.allreduce_flat_grads(self._packed, self.group)
+        elif self.dp_mode == "zero1":
             D.reduce_scatter_flat(self.gshard, self.grads, self.rank, self.group)
         elif self.dp_mode == "sparse":
             self._sparse_exchange()
@@ -355,6 +389,16 @@ class TrainEngine:
         st = L.stream_ptr(self.device)
         lib = L.hip()
         hist_len = self.num_batches
+        if self.dp_mode == "touched":
+            L.check(lib.ncf_lazy_adam_step_packed(ctypes.byref(self.lay), self.flat.data_ptr(), self.exp_avg.data_ptr(),
+                                                  self.exp_avg_sq.data_ptr(), self._ranges, self._nranges,
+                                                  self.ctl.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps,
+                                                  self.loss_hist.data_ptr(), hist_len,
+                                                  self._touched_buf(self.rows).data_ptr(), self.n_total,
+                                                  self.batch_size, self._last.data_ptr(), self._ring.data_ptr(),
+                                                  self.LAZY_RING, self._packed.data_ptr(), self._stamp.data_ptr(),
+                                                  st), "ncf_lazy_adam_step_packed")
+            return
         if self.dp_mode in ("zero1", "sparse"):
             if self.dp_mode == "zero1":  # the shard gradient is in gshard: clear the local bucket now
                 L.check(lib.ncf_zero_f32(self.grads.data_ptr(), self.grads.numel(), st), "ncf_zero_f32")
@@ -438,6 +482,9 @@ class TrainEngine:
                      ({"zero1": "reduce_scatter", "sparse": "sparse_exchange"}.get(self.dp_mode, "allreduce"),
                       self._allreduce),
                      ("optimizer", self._optimize)]
+            if self.dp_mode == "touched":  # the pack is part of _compute
+                parts = [("ncf_train_step+ncf_touched_pack", self._compute), ("allreduce", self._allreduce),
+                         ("ncf_lazy_adam_step_packed", self._optimize)]
             if self.dp_mode in ("zero1", "sparse"):
                 parts.append(("all_gather", self._allgather))
         acc = {k: 0.0 for k, _ in parts}
@@ -528,7 +575,7 @@ class TrainEngine:
                 self._graph_k = self._graph_of(body)
         else:
             self._graph = (self._graph_of(self._compute), self._graph_of(self._optimize))
-            if self.dp_mode == "allreduce":
+            if self.dp_mode in ("allreduce", "touched"):
                 # step t's optimizer and step t + 1's compute in one graph: one replay and
                 # one collective per step from the host (run())
                 def opt_compute():

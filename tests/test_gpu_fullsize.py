@@ -15,10 +15,12 @@ seeds and the same init:
   * the epoch's mean loss to 1e-3 relative, and HR@10 / NDCG@10 of metrics()
     (metrics.py:4-25) on the leave-one-out test set within 0.01 of the oracle's.
 
-Configs: C2 (NCF(8,3), bs 1,024: tuned launch shape, per-row layer 0), C3
+Configs: C2 (NCF(8,3), bs 1,024: tuned launch shape, per-row layer 0, deferred Adam), C3
 (NCF(16,3), bs 65,536: fused kernel, factored layer 0), the reference's CLI
-default NCF(32,3) at bs 65,536 (layered path, step chain, user order) and the stress
-NCF(64,4) (layered path, dm-512 factored layer 0 with the GEMM expansion)."""
+default NCF(32,3) at bs 65,536 (layered path, step chain, user order), the stress
+NCF(64,4) (layered path, dm-512 factored layer 0 with the GEMM expansion) and C4
+(NCF(16,3) at the ml-20m shape, bs 65,536: 99.3M rows, 1,516 steps, per-row layer 0,
+deferred Adam)."""
 import numpy as np
 import pytest
 import torch
@@ -29,10 +31,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
-def _data():
+def _data(shape="ml-1m"):
     from ncf_amd import synthetic
     from ncf_amd.data import NCFData
-    ds = synthetic.make_dataset("ml-1m", seed=0)
+    ds = synthetic.make_dataset(shape, seed=0)
     I = ds["item_num"]
     train = NCFData(np.stack([ds["train_users"], ds["train_items"]], 1), I, None, 4, True)
     tu = np.repeat(ds["test_users"], 100)
@@ -46,13 +48,14 @@ def _data():
 # there to ~4e-5 relative; every step is held to 1e-5 teacher-forced.
 @pytest.mark.parametrize("name,f,L,B,forced,late_rtol", [("c2", 8, 3, 1024, 20, 1e-5), ("c3", 16, 3, 65536, 6, 1e-5),
                                                           ("cli", 32, 3, 65536, 4, 1e-5),
-                                                          ("stress", 64, 4, 65536, 3, 1e-4)])
+                                                          ("stress", 64, 4, 65536, 3, 1e-4),
+                                                          ("c4", 16, 3, 65536, 3, 1e-5)])
 def test_full_epoch_vs_oracle(name, f, L, B, forced, late_rtol):
     from torch.utils.data import DataLoader
     from ncf_amd.models import NCF
     from ncf_amd.trainer import Trainer
     from test_gpu_parity import _teacher_forced_steps
-    ds, train, test, tu, ti = _data()
+    ds, train, test, tu, ti = _data("ml-20m" if name == "c4" else "ml-1m")
     U, I = ds["user_num"], ds["item_num"]
     pu, pi = ds["train_users"], ds["train_items"]
     torch.set_num_threads(min(16, torch.get_num_threads()))
@@ -89,7 +92,11 @@ def test_full_epoch_vs_oracle(name, f, L, B, forced, late_rtol):
     bi = [items[perm[b * B:(b + 1) * B]] for b in range(nb)]
     by = [labels[perm[b * B:(b + 1) * B]] for b in range(nb)]
     opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
-    losses = np.asarray(O.train_steps(ref, opt, bu, bi, by), dtype=np.float64)
+    losses = []
+    for c in range(0, nb, 100):  # progress lines: a long CPU epoch must not look hung
+        losses += O.train_steps(ref, opt, bu[c:c + 100], bi[c:c + 100], by[c:c + 100])
+        print(f"[{name}] oracle steps {len(losses)}/{nb}", flush=True)
+    losses = np.asarray(losses, dtype=np.float64)
     with torch.no_grad():
         logits = ref(torch.as_tensor(tu, dtype=torch.int64), torch.as_tensor(ti, dtype=torch.int64)).numpy()
     HR, NDCG = O.metrics_np(logits, ti, 100, 10)

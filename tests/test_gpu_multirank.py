@@ -2,7 +2,8 @@
 processes) run TrainEngine with world_size=2 -- row shards inside
 ncf_train_step, the gradient exchange between the compute and optimizer graphs
 (zero1: reduce-scatter, Adam on the rank's shard, in-place all-gather of the
-parameters; allreduce: all-reduce, replicated Adam) -- and must (a) stay
+parameters; allreduce: all-reduce, replicated Adam; touched: the rows the global
+batch touches packed, all-reduced, replicated deferred Adam) -- and must (a) stay
 bitwise identical to each other
 and (b) match a single-rank run over the same global batches (per-step loss
 rtol 1e-5; parameters rtol 1e-4 / atol 1e-6: the summed shard gradients differ
@@ -56,7 +57,12 @@ def _worker(rank, world, port, mt, f, nl, use_graph, dp_mode, q):
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
-    flat, losses = _run(world, rank, dist.group.WORLD, mt, f, nl, use_graph, dp_mode)
+    try:
+        flat, losses = _run(world, rank, dist.group.WORLD, mt, f, nl, use_graph, dp_mode)
+    except Exception:  # report instead of leaving the other rank waiting in a collective
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+        os._exit(1)
     q.put((rank, flat, losses))
     dist.barrier()
     dist.destroy_process_group()
@@ -71,7 +77,12 @@ def _free_port():
 @pytest.mark.parametrize("mt,f,nl,use_graph,dp_mode", [("NeuMF-end", 16, 3, True, "zero1"),
                                                        ("NeuMF-end", 16, 3, False, "zero1"),
                                                        ("NeuMF-end", 16, 3, True, "allreduce"),
-                                                       ("NeuMF-end", 16, 3, True, None),  # default: allreduce
+                                                       ("NeuMF-end", 16, 3, True, None),  # default: touched
+                                                       ("NeuMF-end", 16, 3, True, "touched"),
+                                                       ("NeuMF-end", 16, 3, False, "touched"),
+                                                       ("GMF", 16, 3, True, "touched"),
+                                                       ("MLP", 8, 2, True, "touched"),
+                                                       ("NeuMF-end", 32, 3, True, "touched"),
                                                        ("NeuMF-end", 16, 3, False, "allreduce"),
                                                        ("NeuMF-end", 16, 3, True, "sparse"),
                                                        ("NeuMF-end", 16, 3, False, "sparse"),
@@ -79,7 +90,15 @@ def _free_port():
                                                        ("NeuMF-end", 32, 3, True, "zero1"),
                                                        ("GMF", 16, 3, True, "zero1")])
 def test_two_ranks_match_single_rank(mt, f, nl, use_graph, dp_mode):
-    world = 2
+    _ranks_match_single_rank(2, mt, f, nl, use_graph, dp_mode)
+
+
+def test_three_ranks_touched_match_single_rank():
+    """dp_mode "touched" at world 3 (B = 1000: shards of 334 / 334 / 332 rows)."""
+    _ranks_match_single_rank(3, "NeuMF-end", 16, 3, True, "touched")
+
+
+def _ranks_match_single_rank(world, mt, f, nl, use_graph, dp_mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -90,11 +109,16 @@ def test_two_ranks_match_single_rank(mt, f, nl, use_graph, dp_mode):
     res = {}
     for _ in range(world):
         r, flat, losses = q.get(timeout=300)
+        if flat is None:
+            for p in procs:
+                p.kill()
+            raise AssertionError(f"rank {r} failed:\n{losses}")
         res[r] = (flat, losses)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert np.array_equal(res[0][0], res[1][0]), "ranks diverged"
+    for r in range(1, world):
+        assert np.array_equal(res[0][0], res[r][0]), "ranks diverged"
     flat1, losses1 = _run(1, 0, None, mt, f, nl, use_graph)
     np.testing.assert_allclose(res[0][1], losses1, rtol=1e-5)
     np.testing.assert_allclose(res[0][0], flat1, rtol=1e-4, atol=1e-6)
@@ -114,7 +138,7 @@ def _rccl_worker(port, dp_mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dp_mode", ["zero1", "allreduce"])
+@pytest.mark.parametrize("dp_mode", ["zero1", "allreduce", "touched"])
 def test_rccl_collective_captured_in_step_graph(dp_mode):
     """NCF_CAPTURE_ALLREDUCE=1 on backend nccl (RCCL): the gradient exchange is
     captured inside the step graphs.  One GPU holds one RCCL rank, so a one-rank
