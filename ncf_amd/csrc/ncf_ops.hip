@@ -1,6 +1,7 @@
 // Optimizer, reduction, epoch-shuffle and evaluation kernels + the C ABI
 // (include/ncf_hip.h) of libncf_hip.so.  gfx950 only.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "ncf_kernels.h"
@@ -364,72 +365,149 @@ struct LazyArgs {
     const int64_t* stamp;
     int64_t pk_items;  // float offset of the item rows
     int wrow[2];       // floats per packed user / item row
+    int span;          // rolling catch-up: every row is brought up at least every `span` steps
 };
 
 constexpr int LZ_GROUP = 16;  // lanes per claimed row
+constexpr int LZ_WIN = 512;   // step scalars of the last LZ_WIN steps staged in LDS per block
+
+// The block's copy of the step scalars ring[s] for s in [t - LZ_WIN, t) (replays read
+// LDS; older steps, which only an unusually long gap needs, read the ring).
+__device__ __forceinline__ void stage_ring(const LazyArgs& a, int64_t t, float2* win) {
+    for (int k = threadIdx.x; k < LZ_WIN; k += blockDim.x) {
+        const int64_t s = t - LZ_WIN + k;
+        win[k] = s >= 1 ? reinterpret_cast<const float2*>(a.ring)[s % a.ring_n] : float2{0.f, 0.f};
+    }
+}
 
 __device__ __forceinline__ void lazy_rows(const LazyArgs& a, int64_t t, int64_t b, bool flush, float neg_t, float bc2s_t,
-                                          float w1, float b2, float omb2, float eps, int64_t gid, int64_t ngroups) {
+                                          float w1, float b2, float omb2, float eps, int64_t gid, int64_t ngroups,
+                                          const float2* win) {
 #pragma clang fp contract(off)
     const int glane = threadIdx.x & (LZ_GROUP - 1);
     const int32_t* cnt = a.touched + a.nb * (a.su + a.si);
     const int64_t n0 = flush ? 0 : cnt[2 * b], n1 = flush ? 0 : cnt[2 * b + 1];
     const bool next = !flush && b + 1 < a.nb;
     const int64_t n2 = next ? cnt[2 * (b + 1)] : a.U, n3 = next ? cnt[2 * (b + 1) + 1] : a.I;
-    const int64_t total = n0 + n1 + n2 + n3;
+    // rolling catch-up (not on a dense pass): slice t % span of the users and of the
+    // items, so no row falls more than `span` steps behind (replays stay short)
+    const bool roll = next && a.span > 0;
+    const int64_t sl = roll ? t % a.span : 0;
+    const int64_t lu = roll ? sl * a.U / a.span : 0, hu = roll ? (sl + 1) * a.U / a.span : 0;
+    const int64_t li = roll ? sl * a.I / a.span : 0, hi = roll ? (sl + 1) * a.I / a.span : 0;
+    const int64_t n4 = hu - lu, n5 = hi - li;
+    const int64_t total = n0 + n1 + n2 + n3 + n4 + n5;
     const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
-    for (int64_t w = gid; w < total; w += ngroups) {
-        int side, id;
-        if (w < n0) {
-            side = 0; id = a.touched[b * a.su + w];
-        } else if (w < n0 + n1) {
-            side = 1; id = a.touched[a.nb * a.su + b * a.si + (w - n0)];
-        } else if (w < n0 + n1 + n2) {
-            side = 0; id = next ? a.touched[(b + 1) * a.su + (w - n0 - n1)] : (int)(w - n0 - n1);
+    // work item w -> (side, id); batch lists are read from `touched`
+    auto decode = [&](int64_t w, int& side, int& id) {
+        int64_t q = w;
+        if (q < n0) {
+            side = 0; id = a.touched[b * a.su + q];
+        } else if ((q -= n0) < n1) {
+            side = 1; id = a.touched[a.nb * a.su + b * a.si + q];
+        } else if ((q -= n1) < n2) {
+            side = 0; id = next ? a.touched[(b + 1) * a.su + q] : (int)q;
+        } else if ((q -= n2) < n3) {
+            side = 1; id = next ? a.touched[a.nb * a.su + (b + 1) * a.si + q] : (int)q;
+        } else if ((q -= n3) < n4) {
+            side = 0; id = (int)(lu + q);
         } else {
-            side = 1; id = next ? a.touched[a.nb * a.su + (b + 1) * a.si + (w - n0 - n1 - n2)] : (int)(w - n0 - n1 - n2);
+            side = 1; id = (int)(li + q - n4);
         }
+    };
+    // one row: float4 slot k of its active tables (g table first) -> flat index
+    auto elem = [&](int side, int id, int k, int wa) -> int64_t {
+        return k < wa ? a.off[side] + ((int64_t)id * a.w4[side] + k) * 4
+                      : a.off[side + 2] + ((int64_t)id * a.w4[side + 2] + (k - wa)) * 4;
+    };
+    constexpr int NK = 2;  // float4 slots per lane held in registers (rows of up to 128 floats)
+    int64_t w = gid;
+    int side = 0, id = 0;
+    if (w < total) decode(w, side, id);
+    while (w < total) {
         const int64_t slot = side ? a.U + id : id;
-        int old = 0;
         const bool in_b = w < n0 + n1;  // a row of batch b (its gradient: grads, or packed row w)
+        // claim (lane 0) and the row's state (all lanes) in flight together: the loads
+        // of a row another group claims are simply dropped
+        int old = 0;
         if (glane == 0) {
             int32_t* lp = a.last + slot;
             old = *lp;
-            if (a.packed != nullptr) {
-                // each row has exactly one work item: batch b's list, or the second list
-                // for rows batch b does not hold (stamped by ncf_touched_pack)
-                if (!in_b && (a.stamp[slot] >> 32) == t) old = (int)t;
-                else if (old < (int)t) *lp = (int)t;
+            if (a.packed != nullptr && in_b) {
+                // packed mode: batch b's rows have exactly one work item (its list); the
+                // other lists skip them (stamped by ncf_touched_pack) and claim the rest
+                if (old < (int)t) *lp = (int)t;
+            } else if (a.packed != nullptr && (a.stamp[slot] >> 32) == t) {
+                old = (int)t;
             } else if (old < (int)t) {
                 old = atomicMax(lp, (int)t);
             }
         }
-        old = __shfl(old, threadIdx.x & ~(LZ_GROUP - 1), 64);
-        if (old >= (int)t) continue;
-        const int sa = side, sb = side + 2;  // g table, m table of this side
-        const int wa = a.off[sa] >= 0 ? a.w4[sa] : 0, wb = a.off[sb] >= 0 ? a.w4[sb] : 0;
+        const int wa = a.off[side] >= 0 ? a.w4[side] : 0, wb = a.off[side + 2] >= 0 ? a.w4[side + 2] : 0;
+        const int W4 = wa + wb;
         const float* prow = nullptr;  // packed mode: the row's summed gradient (batch b's rows)
         if (a.packed != nullptr && in_b)
             prow = a.packed + (side ? a.pk_items + (w - n0) * a.wrow[1] : w * a.wrow[0]);
-        for (int k = glane; k < wa + wb; k += LZ_GROUP) {
-            const int64_t e = k < wa ? a.off[sa] + ((int64_t)id * a.w4[sa] + k) * 4
-                                     : a.off[sb] + ((int64_t)id * a.w4[sb] + (k - wa)) * 4;
-            f4 pp = *reinterpret_cast<const f4*>(a.p + e);
-            f4 mm = *reinterpret_cast<const f4*>(a.m + e);
-            f4 vv = *reinterpret_cast<const f4*>(a.v + e);
-            const f4 gg = a.packed == nullptr ? *reinterpret_cast<const f4*>(a.g + e)
-                        : (prow != nullptr ? *reinterpret_cast<const f4*>(prow + 4 * k) : zero);
-            for (int s = old + 1; s < (int)t; ++s) {  // the steps this row sat out: g = 0
-                const float* sc = a.ring + 2 * (s % a.ring_n);
-                adam_f4(pp, mm, vv, zero, w1, b2, omb2, sc[1], eps, sc[0]);
+        f4 pp[NK], mm[NK], vv[NK], gg[NK];
+        int64_t ek[NK];
+#pragma unroll
+        for (int j = 0; j < NK; ++j) {
+            const int k = glane + j * LZ_GROUP;
+            if (k < W4) {
+                ek[j] = elem(side, id, k, wa);
+                pp[j] = *reinterpret_cast<const f4*>(a.p + ek[j]);
+                mm[j] = *reinterpret_cast<const f4*>(a.m + ek[j]);
+                vv[j] = *reinterpret_cast<const f4*>(a.v + ek[j]);
+                gg[j] = a.packed == nullptr ? *reinterpret_cast<const f4*>(a.g + ek[j])
+                      : (prow != nullptr ? *reinterpret_cast<const f4*>(prow + 4 * k) : zero);
             }
-            adam_f4(pp, mm, vv, gg, w1, b2, omb2, bc2s_t, eps, neg_t);
-            *reinterpret_cast<f4*>(a.m + e) = mm;
-            *reinterpret_cast<f4*>(a.v + e) = vv;
-            *reinterpret_cast<f4*>(a.p + e) = pp;
-            if (a.packed == nullptr && (gg.x != 0.f || gg.y != 0.f || gg.z != 0.f || gg.w != 0.f))
-                *reinterpret_cast<f4*>(a.g + e) = zero;
         }
+        // the next item's id requested before this one is waited for
+        const int64_t w2 = w + ngroups;
+        int side2 = 0, id2 = 0;
+        if (w2 < total) decode(w2, side2, id2);
+        old = __shfl(old, threadIdx.x & ~(LZ_GROUP - 1), 64);
+        if (old < (int)t) {
+#pragma unroll
+            for (int j = 0; j < NK; ++j) {
+                const int k = glane + j * LZ_GROUP;
+                if (k >= W4) continue;
+                for (int s = old + 1; s < (int)t; ++s) {  // the steps this row sat out: g = 0
+                    const int64_t kw = s - (t - LZ_WIN);
+                    const float2 sc = kw >= 0 ? win[kw] : reinterpret_cast<const float2*>(a.ring)[s % a.ring_n];
+                    adam_f4(pp[j], mm[j], vv[j], zero, w1, b2, omb2, sc.y, eps, sc.x);
+                }
+                adam_f4(pp[j], mm[j], vv[j], gg[j], w1, b2, omb2, bc2s_t, eps, neg_t);
+                *reinterpret_cast<f4*>(a.m + ek[j]) = mm[j];
+                *reinterpret_cast<f4*>(a.v + ek[j]) = vv[j];
+                *reinterpret_cast<f4*>(a.p + ek[j]) = pp[j];
+                if (a.packed == nullptr && (gg[j].x != 0.f || gg[j].y != 0.f || gg[j].z != 0.f || gg[j].w != 0.f))
+                    *reinterpret_cast<f4*>(a.g + ek[j]) = zero;
+            }
+            // rows wider than NK * LZ_GROUP float4 (f + dm > 128): the rest one slot at a time
+            for (int k = glane + NK * LZ_GROUP; k < W4; k += LZ_GROUP) {
+                const int64_t e = elem(side, id, k, wa);
+                f4 p1 = *reinterpret_cast<const f4*>(a.p + e);
+                f4 m1 = *reinterpret_cast<const f4*>(a.m + e);
+                f4 v1 = *reinterpret_cast<const f4*>(a.v + e);
+                const f4 g1 = a.packed == nullptr ? *reinterpret_cast<const f4*>(a.g + e)
+                            : (prow != nullptr ? *reinterpret_cast<const f4*>(prow + 4 * k) : zero);
+                for (int s = old + 1; s < (int)t; ++s) {
+                    const int64_t kw = s - (t - LZ_WIN);
+                    const float2 sc = kw >= 0 ? win[kw] : reinterpret_cast<const float2*>(a.ring)[s % a.ring_n];
+                    adam_f4(p1, m1, v1, zero, w1, b2, omb2, sc.y, eps, sc.x);
+                }
+                adam_f4(p1, m1, v1, g1, w1, b2, omb2, bc2s_t, eps, neg_t);
+                *reinterpret_cast<f4*>(a.m + e) = m1;
+                *reinterpret_cast<f4*>(a.v + e) = v1;
+                *reinterpret_cast<f4*>(a.p + e) = p1;
+                if (a.packed == nullptr && (g1.x != 0.f || g1.y != 0.f || g1.z != 0.f || g1.w != 0.f))
+                    *reinterpret_cast<f4*>(a.g + e) = zero;
+            }
+        }
+        w = w2;
+        side = side2;
+        id = id2;
     }
 }
 
@@ -452,13 +530,15 @@ __global__ __launch_bounds__(256) void lazy_adam_kernel(const float* __restrict_
             a.ring[2 * (t_step % a.ring_n) + 1] = sc[1];
         }
     } else {
+        __shared__ float2 win[LZ_WIN];
+        stage_ring(a, t_step, win);
         step_scalars(t_step, lr, beta1, beta2, sc);
         __syncthreads();
         const int64_t b = ((b_step % a.nb) + a.nb) % a.nb;
         const int64_t groups_per_block = blockDim.x / LZ_GROUP;
         const int64_t gid = (int64_t)(blockIdx.x - nA) * groups_per_block + threadIdx.x / LZ_GROUP;
         lazy_rows(a, t_step, b, false, sc[0], sc[1], (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), eps, gid,
-                  (int64_t)(gridDim.x - nA) * groups_per_block);
+                  (int64_t)(gridDim.x - nA) * groups_per_block, win);
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         ctl->adam_t = t_step;
@@ -470,10 +550,14 @@ __global__ __launch_bounds__(256) void lazy_flush_kernel(const ncf_step_ctl* ctl
                                                          LazyArgs a) {
     const int64_t t = ctl->adam_t;
     if (t <= 0) return;
+    __shared__ float2 win[LZ_WIN];
+    stage_ring(a, t, win);
+    __syncthreads();
     const float* sc = a.ring + 2 * (t % a.ring_n);
     const int64_t groups_per_block = blockDim.x / LZ_GROUP;
     lazy_rows(a, t, 0, true, sc[0], sc[1], (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), eps,
-              (int64_t)blockIdx.x * groups_per_block + threadIdx.x / LZ_GROUP, (int64_t)gridDim.x * groups_per_block);
+              (int64_t)blockIdx.x * groups_per_block + threadIdx.x / LZ_GROUP, (int64_t)gridDim.x * groups_per_block,
+              win);
 }
 
 // ---------------------------------------------------------------------------
@@ -1735,6 +1819,12 @@ static int lazy_args(const ncf_layout* lay, float* params, float* grads, float* 
         a->off[k] = act ? offs[k] : -1;
         a->w4[k] = (int)(widths[k] / 4);
     }
+    static const int span = [] {
+        const char* e = getenv("NCF_LAZY_SPAN");
+        const int v = e ? atoi(e) : 32;
+        return v < 0 ? 0 : (v > LZ_WIN - 2 ? LZ_WIN - 2 : v);
+    }();
+    a->span = span;
     a->p = params;
     a->g = grads;
     a->m = m;

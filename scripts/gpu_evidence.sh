@@ -23,12 +23,18 @@ run() {  # name, seconds, cmd...
     return 0
 }
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider
+run pytest_gpu 900 python -u -m pytest tests -m gpu -v -s -x --timeout 300 --timeout-method thread -p no:cacheprovider
 run bench 600 python bench.py
 for cfg in ${CONFIGS:-c2 c4 cli stress c5}; do
-    run "bench_$cfg" 300 python bench.py --config "$cfg" --steps 200 --warmup 20 --skip-cpu-baseline --e2e-epochs 0
+    run "bench_$cfg" 300 python bench.py --config "$cfg" --steps 200 --warmup 20 --skip-cpu-baseline --e2e-epochs ${E2E:-2}
     tail -1 "gpurun_out/bench_$cfg.log" >> gpurun_out/configs.jsonl
 done
+if [ "${SAMPLER:-1}" = "1" ]; then
+    for shape in ml-1m ml-20m; do
+        run "sampler_$shape" 300 python scripts/sampler_bench.py --shape $shape --passes 6
+        tail -1 "gpurun_out/sampler_$shape.log" >> gpurun_out/sampler.jsonl
+    done
+fi
 if [ "${PROFILE:-1}" = "1" ]; then
     for cfg in ${PROFILE_CONFIGS:-c3}; do  # scripts/profile.sh writes fixed names: keep a copy per config
         export CONFIG=$cfg

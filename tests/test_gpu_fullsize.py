@@ -45,11 +45,13 @@ def _data(shape="ml-1m"):
 
 # late_rtol: free-running loss tolerance past the first 10 steps.  NCF(64,4) (6.4M
 # parameters) turns at step 10 (loss 0.457 -> 0.475) and the two fp32 trajectories part
-# there to ~4e-5 relative; every step is held to 1e-5 teacher-forced.
+# there to ~4e-5 relative; C4 (13.2M parameters) parts to ~3.6e-5 from step ~12 (a third
+# of the first 100 losses beyond 1e-5 on the MI355X); every step is held to 1e-5
+# teacher-forced.
 @pytest.mark.parametrize("name,f,L,B,forced,late_rtol", [("c2", 8, 3, 1024, 20, 1e-5), ("c3", 16, 3, 65536, 6, 1e-5),
                                                           ("cli", 32, 3, 65536, 4, 1e-5),
                                                           ("stress", 64, 4, 65536, 3, 1e-4),
-                                                          ("c4", 16, 3, 65536, 3, 1e-5)])
+                                                          ("c4", 16, 3, 65536, 3, 1e-4)])
 def test_full_epoch_vs_oracle(name, f, L, B, forced, late_rtol):
     from torch.utils.data import DataLoader
     from ncf_amd.models import NCF
