@@ -138,36 +138,28 @@ def adam_info(kt, eng, model):
                                  "slab_read": slab_rows * slab_cols * 4, "w0_partials_read": partial},
                 "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}
     if "ncf_lazy_adam_step" in kt or "ncf_lazy_adam_step_packed" in kt:
-        # deferred Adam: the rows of batches b and b + 1 per step (every row on an
-        # epoch's last batch), from the epoch's touched lists
+        # deferred Adam: the rows of lists A, B, C per step (include/ncf_hip.h
+        # ncf_batch_touched), from the epoch's touched lists
         key = "ncf_lazy_adam_step" if "ncf_lazy_adam_step" in kt else "ncf_lazy_adam_step_packed"
         ms = kt[key]
-        t = eng._touched_buf(eng.rows).cpu().numpy()
+        from ncf_amd.engine import touched_segments
         U, I = model.user_num, model.item_num
         nb = eng.num_batches
-        su, si = min(U, eng.batch_size), min(I, eng.batch_size)
-        cnt = t[nb * (su + si): nb * (su + si) + 2 * nb].reshape(nb, 2)
-        lists = [(t[b * su: b * su + cnt[b, 0]], t[nb * su + b * si: nb * su + b * si + cnt[b, 1]]) for b in range(nb)]
+        lists = touched_segments(eng._touched_buf(eng.rows).cpu().numpy(), nb)
         wu = sum(p.numel() // U for p, a in zip(list(model.ordered_params())[:4], ops.active_mask(model)[:4])
                  if a and p.shape[0] == U)
         wi = sum(p.numel() // I for p, a in zip(list(model.ordered_params())[:4], ops.active_mask(model)[:4])
                  if a and p.shape[0] == I)
-        rows_u = rows_i = grad_rows = 0
-        for b in range(nb):
-            grad_rows += len(lists[b][0]) * wu + len(lists[b][1]) * wi
-            if b + 1 < nb:
-                rows_u += len(np.union1d(lists[b][0], lists[b + 1][0]))
-                rows_i += len(np.union1d(lists[b][1], lists[b + 1][1]))
-            else:
-                rows_u += U
-                rows_i += I
+        rows_u = sum(len(lists[b][k]) for b in range(nb) for k in (0, 2, 4))
+        rows_i = sum(len(lists[b][k]) for b in range(nb) for k in (1, 3, 5))
+        grad_rows = sum(len(lists[b][0]) * wu + len(lists[b][1]) * wi for b in range(nb))
         moved = (rows_u * wu + rows_i * wi) / nb  # embedding floats read and written per step
         b = 24 * moved + 8 * grad_rows / nb + 24 * tower + slab_rows * slab_cols * 4 + partial
         return {"kernel": f"{key} (tower slab reduce + Adam, deferred embedding Adam)", "params": emb + tower,
                 "embedding_floats_moved_per_step": moved, "dense_embedding_floats": emb,
-                "bytes": b, "bytes_note": "p, m, v read + written (24 B) per embedding float of the rows of batches "
-                                          "b and b + 1 (every row on the epoch's last batch), their gradient read + "
-                                          "cleared (8 B) for batch b's rows, the tower as ncf_reduce_adam_step",
+                "bytes": b, "bytes_note": "p, m, v read + written (24 B) per embedding float of the rows "
+                                          "of lists A, B, C (every row on the epoch's last batch), the gradient read "
+                                          "+ cleared (8 B) for list A's rows, the tower as ncf_reduce_adam_step",
                 "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}
     b = 32 * (emb + tower)
     ms = kt["optimizer"]
@@ -479,21 +471,22 @@ def _barrier(group, dev):
             dist.barrier(group=group)
 
 
-def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup, use_graph):
+def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup, use_graph, whole_epochs=True):
     """Warm-up, then whole fresh epochs timed (>= `steps` optimizer steps, rounded up
     to whole epochs of `global_batch`-row global batches: every epoch in the timed
     region draws new negatives and a new permutation), then the same number of steps
     on the last epoch stream reused (`frozen`).  Max over ranks, barrier +
-    synchronize on both sides of each timed region."""
+    synchronize on both sides of each timed region.  whole_epochs=False (--profile-run:
+    rocprofv3 passes serialise every launch): exactly `warmup` and `steps` steps."""
     eng, model, pipe = setup_engine(cfg, ds, train, world, rank, dev, group, global_batch)
     nb = eng.num_batches
     n_rows = eng.n_total
-    warm = max(1, -(-max(1, warmup) // nb)) * nb
+    warm = max(1, -(-max(1, warmup) // nb)) * nb if whole_epochs else max(1, warmup)
     eng.batches_done = 0
     run_steps(eng, warm, use_graph)
     torch.cuda.synchronize(dev)
-    epochs = max(1, -(-steps // nb))
-    k = epochs * nb
+    epochs = max(1, -(-steps // nb)) if whole_epochs else steps / nb
+    k = int(round(epochs * nb))
     _barrier(group, dev)
     torch.cuda.synchronize(dev)
     e0 = pipe.stats["epochs"]
@@ -516,10 +509,11 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
     dtf = time.perf_counter() - t0
     _barrier(group, dev)
     dtf = _max_over_ranks(dtf, group, dev)
-    hm = pipe.stats.get("host_ms", [])[-epochs:]
+    ne = max(1, int(np.ceil(epochs)))
+    hm = pipe.stats.get("host_ms", [])[-ne:]
     host = {k2: float(np.mean([h[k2] for h in hm if k2 in h])) for k2 in ("sample", "words", "stage")
             if any(k2 in h for h in hm)}
-    bm = pipe.stats.get("boundary_ms", [])[-epochs:]
+    bm = pipe.stats.get("boundary_ms", [])[-ne:]
     if bm:
         host["boundary_join"] = float(np.mean([x[0] for x in bm]))
         host["boundary_rest"] = float(np.mean([x[1] for x in bm]))
@@ -603,6 +597,8 @@ def main():
     ap.add_argument("--skip-eval", action="store_true")
     ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling (global batch x N) field")
     ap.add_argument("--e2e-epochs", type=int, default=16, help="Trainer.fit epochs for the e2e figure (0: skip)")
+    ap.add_argument("--profile-run", action="store_true",
+                    help="exactly --warmup/--steps steps (not whole epochs): for rocprofv3 passes, not a bench line")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-harness", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--harness-epochs", type=int, default=1, help=argparse.SUPPRESS)
@@ -641,7 +637,8 @@ def main():
 
     # ---- headline: the reference's global batch split over the N ranks (strong
     # scaling), whole fresh epochs
-    m = measure(args.config, ds, train, world, rank, dev, group, global_batch, args.steps, args.warmup, use_graph)
+    m = measure(args.config, ds, train, world, rank, dev, group, global_batch, args.steps, args.warmup, use_graph,
+                whole_epochs=not args.profile_run)
     eng, model, pipe = m["eng"], m["model"], m["pipe"]
 
     # ---- per-kernel live timing (HIP events on the launch stream) -------------

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 13
+#define NCF_ABI_VERSION 14
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -301,20 +301,26 @@ int ncf_reduce_adam_step(const ncf_layout *lay, const void *workspace, float *pa
  * sequence with step-s scalars, so the steps a row sat out are replayed, in order,
  * with the same arithmetic, when the row is next needed -- bitwise the dense result.
  *
- * ncf_batch_touched: for every global batch b of the epoch stream (rows[0..n), batches
- * of batch_global rows, padding rows skipped), the sorted unique user ids and item ids
- * it holds.  touched (int32, ncf_touched_bytes): [nb][min(U, B)] users, [nb][min(I, B)]
- * items, then [nb][2] counts (users, items); nb = ceil(n / batch_global).  U, I <= 2^20.
+ * ncf_batch_touched (layout since ABI 14): for every global batch b of the epoch stream
+ * (rows[0..n), batches of batch_global rows, padding rows skipped) and each side
+ * (users, items), three disjoint sorted id lists:
+ *   A_b = the ids batch b holds (their gradient is this step's),
+ *   B_b = the ids batch b + 1 holds that A_b does not (the next forward reads them);
+ *         on the epoch's last batch, every id not in A_b,
+ *   C_b = the ids of slice (b % span) that are in neither (rolling catch-up: no row
+ *         falls more than span steps behind; span = NCF_LAZY_SPAN, default 32).
+ * touched (ncf_touched_bytes bytes, 8-byte aligned): int64 seg[6 nb + 1] -- list
+ * k = 2 * list + side of batch b is ids[seg[6b + k] .. seg[6b + k + 1]) -- then the
+ * int32 ids.  nb = ceil(n / batch_global).  U, I <= 2^19 (two LDS bitmaps per block).
  *
  * ncf_lazy_adam_step: ncf_reduce_adam_step's tower part (slab reduction + Adam, loss,
- * ctl commit) and, over the embedding tables, the rows of batch b = snap_batch % nb
- * (they hold gradients) and of batch b + 1 (the next forward reads them) -- on the
- * epoch's last batch every row instead -- each brought from last_step[row] + 1 to
- * t = snap_t: replays with g = 0, then step t with its gradient, which is cleared.
- * last_step: int32 [U + I] (users, then items; 0 = none since Adam state zero, or the
- * step the optimizer state was loaded at).  step_scalars: float [ring][2], written for
- * step t by this launch; ring >= nb + 2.  n_total / batch_global: the epoch stream's.
- * factor_num % 4 == 0 (NCF_E_UNSUPPORTED otherwise).
+ * ctl commit) and, over the embedding tables, the rows of batch b = snap_batch % nb's
+ * three lists, each brought from last_step[row] + 1 to t = snap_t: replays with g = 0,
+ * then step t (A rows: with their gradient, which is cleared).  The lists are
+ * disjoint: no atomics.  last_step: int32 [U + I] (users, then items; 0 = none since
+ * Adam state zero, or the step the optimizer state was loaded at).  step_scalars:
+ * float [ring][2], written for step t by this launch; ring >= 514.  n_total /
+ * batch_global: the epoch stream's.  factor_num % 4 == 0 (NCF_E_UNSUPPORTED otherwise).
  *
  * ncf_lazy_adam_flush: every embedding row through t = ctl->adam_t (after that step's
  * ncf_lazy_adam_step): parameters and moments equal the dense optimizer's again --
@@ -336,15 +342,15 @@ int ncf_lazy_adam_flush(const ncf_layout *lay, float *params, float *grads, floa
 
 /*
  * Data-parallel deferred Adam (dp_mode "touched"; since ABI 13).  Every rank knows
- * the global batch, so every rank holds the same sorted lists of the rows batch b
+ * the global batch, so every rank holds the same lists A_b of the rows batch b
  * touches (ncf_batch_touched) and packs its partial gradient of exactly those rows,
  * in list order, into one buffer of ncf_touched_packed_floats(lay, ranges, nranges,
  * batch_global) floats:
  *   [min(U, B)] user rows ((Ug active ? f : 0) + (Um active ? dm : 0) floats each),
  *   [min(I, B)] item rows, then ncf_slab_stride floats of tower gradient (+ loss).
  * ncf_touched_pack (after ncf_train_step): the slab / W0 partial reduction into the
- * tail, the rows into the list slots (slots past the batch's count zeroed), those
- * rows of grads cleared, stamp[row] (int64 [U + I]) = t << 32 | slot.  Then one
+ * tail, batch b's A rows into the list slots (slots past the list's count zeroed),
+ * those rows of grads cleared.  Then one
  * all-reduce (sum) of the whole buffer, and ncf_lazy_adam_step_packed -- the
  * deferred Adam of ncf_lazy_adam_step with batch b's gradients (and the tower's)
  * read from the summed buffer, the same on every rank: no parameter all-gather.
@@ -352,13 +358,13 @@ int ncf_lazy_adam_flush(const ncf_layout *lay, float *params, float *grads, floa
 int64_t ncf_touched_packed_floats(const ncf_layout *lay, const int64_t *ranges, int nranges, int64_t batch_global);
 int ncf_touched_pack(const ncf_layout *lay, const void *workspace, float *grads, const int64_t *ranges,
                      int nranges, const int32_t *touched, int64_t n_total, int64_t batch_global,
-                     const ncf_step_ctl *ctl, float *packed, int64_t *stamp, void *stream);
+                     const ncf_step_ctl *ctl, float *packed, void *stream);
 int ncf_lazy_adam_step_packed(const ncf_layout *lay, float *params, float *exp_avg, float *exp_avg_sq,
                               const int64_t *ranges, int nranges, ncf_step_ctl *ctl, double lr, double beta1,
                               double beta2, double eps, float *loss_hist, int64_t hist_len,
                               const int32_t *touched, int64_t n_total, int64_t batch_global,
                               int32_t *last_step, float *step_scalars, int64_t ring, const float *packed,
-                              const int64_t *stamp, void *stream);
+                              void *stream);
 
 /* Plain SGD p -= lr * g (optim.SGD(lr*10) on the --pretraining path, train_neumf.py:87-88). */
 int ncf_sgd_step(float *params, float *grads, const int64_t *ranges, int nranges,

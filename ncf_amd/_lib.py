@@ -29,7 +29,7 @@ NCF_E_ARG = -2
 NCF_E_LAUNCH = -3
 MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
 DZ_BCE, DZ_DLOGIT, DZ_KD = 0, 1, 2
-ABI_VERSION = 13  # include/ncf_hip.h NCF_ABI_VERSION
+ABI_VERSION = 14  # include/ncf_hip.h NCF_ABI_VERSION
 PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 LAYOUT_PER_ROW_L0, LAYOUT_WG_SHIFT, LAYOUT_WG_MASK = 0x1, 8, 0xFFF  # ncf_layout.flags (ncf_layout_tune)
 LAYOUT_LAYERED = 0x2  # ncf_layout.flags: training on the layered path even where a fused kernel exists
@@ -112,11 +112,11 @@ _HIP_PROTOS = {
                                           c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "ncf_touched_packed_floats": (c_i64, [ctypes.POINTER(NcfLayout), ctypes.POINTER(c_i64), ctypes.c_int, c_i64]),
     "ncf_touched_pack": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.c_int,
-                                        c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+                                        c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "ncf_lazy_adam_step_packed": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, ctypes.POINTER(c_i64),
                                                  ctypes.c_int, c_vp, ctypes.c_double, ctypes.c_double,
                                                  ctypes.c_double, ctypes.c_double, c_vp, c_i64, c_vp, c_i64, c_i64,
-                                                 c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+                                                 c_vp, c_vp, c_i64, c_vp, c_vp]),
     "ncf_lazy_adam_flush": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp,
                                            ctypes.POINTER(c_i64), ctypes.c_int, c_vp,
                                            ctypes.c_double, ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_i64,

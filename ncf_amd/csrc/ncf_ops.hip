@@ -338,13 +338,22 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
 // can be replayed, in order, when it is next needed, with a bitwise-identical
 // result.  last[row] (users [0, U), items [U, U + I)) is the last step applied to
 // the row; ring[s % ring_n] the step-s scalars, written by step s's launch.
-// Step t's launch (global batch b of the epoch stream) takes the rows batch b
-// touched (their gradient is in grads) and the rows batch b + 1 will read (so
-// the next forward sees current parameters); on the epoch's last batch, every
-// row instead.  A row is claimed by atomicMax(last, t) -- one group per claim --
-// and brought from last + 1 through t: the replays with g = 0, then step t with
-// its gradient (zero for a row batch b did not touch), which is then cleared.
-// Flush mode: every row through t = ctl->adam_t (all gradients already zero).
+//
+// ncf_batch_touched builds, per global batch b of the epoch stream and per side
+// (users, items), three disjoint sorted lists (segments k = 2 * list + side):
+//   A_b = the rows batch b touches            (their gradient is in grads)
+//   B_b = the rows batch b + 1 touches, not A_b (the next forward reads them);
+//         on the epoch's last batch: every row not in A_b
+//   C_b = the rows of slice (b % span) of the side's ids, in neither
+//         (rolling catch-up: no row falls more than `span` steps behind)
+// Step t's launch brings every listed row from last + 1 through t: the replays
+// with g = 0, then step t with its gradient (A rows; zero for B and C rows, whose
+// gradient is not read).  A rows sat out nothing (they were in A or B the step
+// before), B and C rows at most `span` steps, whose scalars are staged in LDS.
+// The lists are disjoint, so no row is claimed twice: no atomics.  Each wave
+// takes whole rows -- floor(64 / W) rows of W float4 side by side, or one row
+// looped over 64 lanes -- so a row's lanes read last before any of them writes it.
+// Flush: every row through t = ctl->adam_t (all gradients zero by then).
 struct LazyArgs {
     float* p;
     float* g;
@@ -353,26 +362,23 @@ struct LazyArgs {
     int64_t off[4];  // Ug, Ig, Um, Im flat offsets (< 0: table inactive)
     int w4[4];       // float4s per row of each table
     int U, I;
-    const int32_t* touched;  // ncf_batch_touched: [nb][su] users, [nb][si] items, [nb][2] counts
-    int64_t nb, su, si;
+    const int64_t* seg;  // ncf_batch_touched: [nb * 6 + 1] list offsets (segment k of batch b: 6b + k)
+    const int32_t* ids;  // the lists' ids
+    int64_t nb;
     int32_t* last;  // [U + I]
     float* ring;    // [ring_n][2]
     int64_t ring_n;
-    // packed mode (data parallel, ncf_touched_pack): batch b's rows' summed gradients
-    // at packed[k * wrow[side] + ...] (k = position in batch b's list, users first),
-    // stamp[row] = t << 32 | k for those rows
+    // packed mode (data parallel, ncf_touched_pack): A_b's summed gradients at
+    // packed[k * wrow[side] + ...] (k = position in A_b's list, users first)
     const float* packed;
-    const int64_t* stamp;
     int64_t pk_items;  // float offset of the item rows
+    int64_t pk_tail;   // float offset of the tower gradient
     int wrow[2];       // floats per packed user / item row
-    int span;          // rolling catch-up: every row is brought up at least every `span` steps
 };
 
-constexpr int LZ_GROUP = 16;  // lanes per claimed row
-constexpr int LZ_WIN = 512;   // step scalars of the last LZ_WIN steps staged in LDS per block
+constexpr int LZ_WIN = 512;  // step scalars of the last LZ_WIN steps staged in LDS per block
 
-// The block's copy of the step scalars ring[s] for s in [t - LZ_WIN, t) (replays read
-// LDS; older steps, which only an unusually long gap needs, read the ring).
+// The block's copy of the step scalars ring[s] for s in [t - LZ_WIN, t).
 __device__ __forceinline__ void stage_ring(const LazyArgs& a, int64_t t, float2* win) {
     for (int k = threadIdx.x; k < LZ_WIN; k += blockDim.x) {
         const int64_t s = t - LZ_WIN + k;
@@ -380,134 +386,94 @@ __device__ __forceinline__ void stage_ring(const LazyArgs& a, int64_t t, float2*
     }
 }
 
-__device__ __forceinline__ void lazy_rows(const LazyArgs& a, int64_t t, int64_t b, bool flush, float neg_t, float bc2s_t,
-                                          float w1, float b2, float omb2, float eps, int64_t gid, int64_t ngroups,
-                                          const float2* win) {
+__device__ __forceinline__ int lz_row_w4(const LazyArgs& a, int side) {
+    return (a.off[side] >= 0 ? a.w4[side] : 0) + (a.off[side + 2] >= 0 ? a.w4[side + 2] : 0);
+}
+
+// flat index of float4 slot k of a row (g table first, then m table)
+__device__ __forceinline__ int64_t lz_elem(const LazyArgs& a, int side, int id, int k) {
+    const int wa = a.off[side] >= 0 ? a.w4[side] : 0;
+    return k < wa ? a.off[side] + ((int64_t)id * a.w4[side] + k) * 4
+                  : a.off[side + 2] + ((int64_t)id * a.w4[side + 2] + (k - wa)) * 4;
+}
+
+// Bring one float4 of a row from `old` + 1 through t (grad: step t's gradient, or
+// null for zero) and store it.
+__device__ __forceinline__ void lz_update(const LazyArgs& a, int64_t e, int old, int64_t t, const float* grad,
+                                          bool clear_g, float neg_t, float bc2s_t, float w1, float b2, float omb2,
+                                          float eps, const float2* win) {
 #pragma clang fp contract(off)
-    const int glane = threadIdx.x & (LZ_GROUP - 1);
-    const int32_t* cnt = a.touched + a.nb * (a.su + a.si);
-    const int64_t n0 = flush ? 0 : cnt[2 * b], n1 = flush ? 0 : cnt[2 * b + 1];
-    const bool next = !flush && b + 1 < a.nb;
-    const int64_t n2 = next ? cnt[2 * (b + 1)] : a.U, n3 = next ? cnt[2 * (b + 1) + 1] : a.I;
-    // rolling catch-up (not on a dense pass): slice t % span of the users and of the
-    // items, so no row falls more than `span` steps behind (replays stay short)
-    const bool roll = next && a.span > 0;
-    const int64_t sl = roll ? t % a.span : 0;
-    const int64_t lu = roll ? sl * a.U / a.span : 0, hu = roll ? (sl + 1) * a.U / a.span : 0;
-    const int64_t li = roll ? sl * a.I / a.span : 0, hi = roll ? (sl + 1) * a.I / a.span : 0;
-    const int64_t n4 = hu - lu, n5 = hi - li;
-    const int64_t total = n0 + n1 + n2 + n3 + n4 + n5;
     const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
-    // work item w -> (side, id); batch lists are read from `touched`
-    auto decode = [&](int64_t w, int& side, int& id) {
-        int64_t q = w;
-        if (q < n0) {
-            side = 0; id = a.touched[b * a.su + q];
-        } else if ((q -= n0) < n1) {
-            side = 1; id = a.touched[a.nb * a.su + b * a.si + q];
-        } else if ((q -= n1) < n2) {
-            side = 0; id = next ? a.touched[(b + 1) * a.su + q] : (int)q;
-        } else if ((q -= n2) < n3) {
-            side = 1; id = next ? a.touched[a.nb * a.su + (b + 1) * a.si + q] : (int)q;
-        } else if ((q -= n3) < n4) {
-            side = 0; id = (int)(lu + q);
+    f4 pp = *reinterpret_cast<const f4*>(a.p + e);
+    f4 mm = *reinterpret_cast<const f4*>(a.m + e);
+    f4 vv = *reinterpret_cast<const f4*>(a.v + e);
+    const f4 gg = grad != nullptr ? *reinterpret_cast<const f4*>(grad) : zero;
+    for (int s = old + 1; s < (int)t; ++s) {  // the steps this row sat out: g = 0
+        const int64_t kw = s - (t - LZ_WIN);
+        const float2 sc = kw >= 0 ? win[kw] : reinterpret_cast<const float2*>(a.ring)[s % a.ring_n];
+        adam_f4(pp, mm, vv, zero, w1, b2, omb2, sc.y, eps, sc.x);
+    }
+    adam_f4(pp, mm, vv, gg, w1, b2, omb2, bc2s_t, eps, neg_t);
+    *reinterpret_cast<f4*>(a.m + e) = mm;
+    *reinterpret_cast<f4*>(a.v + e) = vv;
+    *reinterpret_cast<f4*>(a.p + e) = pp;
+    if (clear_g) *reinterpret_cast<f4*>(a.g + e) = zero;
+}
+
+// The embedding rows of step t, batch b (flush: every row), one wave task per
+// group of rows; tasks per segment: ceil(rows / rows per wave).
+__device__ __forceinline__ void lazy_rows(const LazyArgs& a, int64_t t, int64_t b, bool flush, float neg_t,
+                                          float bc2s_t, float w1, float b2, float omb2, float eps,
+                                          const float2* win, int64_t wave, int64_t nwaves) {
+    const int lane = threadIdx.x & 63;
+    int64_t n[6], first[6];  // the six segments (flush: every user, every item as segments 2, 3)
+    for (int k = 0; k < 6; ++k) {
+        if (flush) {
+            n[k] = k == 2 ? a.U : (k == 3 ? a.I : 0);
+            first[k] = 0;
         } else {
-            side = 1; id = (int)(li + q - n4);
+            first[k] = a.seg[6 * b + k];
+            n[k] = a.seg[6 * b + k + 1] - first[k];
         }
-    };
-    // one row: float4 slot k of its active tables (g table first) -> flat index
-    auto elem = [&](int side, int id, int k, int wa) -> int64_t {
-        return k < wa ? a.off[side] + ((int64_t)id * a.w4[side] + k) * 4
-                      : a.off[side + 2] + ((int64_t)id * a.w4[side + 2] + (k - wa)) * 4;
-    };
-    constexpr int NK = 2;  // float4 slots per lane held in registers (rows of up to 128 floats)
-    int64_t w = gid;
-    int side = 0, id = 0;
-    if (w < total) decode(w, side, id);
-    while (w < total) {
-        const int64_t slot = side ? a.U + id : id;
-        const bool in_b = w < n0 + n1;  // a row of batch b (its gradient: grads, or packed row w)
-        // claim (lane 0) and the row's state (all lanes) in flight together: the loads
-        // of a row another group claims are simply dropped
-        int old = 0;
-        if (glane == 0) {
-            int32_t* lp = a.last + slot;
-            old = *lp;
-            if (a.packed != nullptr && in_b) {
-                // packed mode: batch b's rows have exactly one work item (its list); the
-                // other lists skip them (stamped by ncf_touched_pack) and claim the rest
-                if (old < (int)t) *lp = (int)t;
-            } else if (a.packed != nullptr && (a.stamp[slot] >> 32) == t) {
-                old = (int)t;
-            } else if (old < (int)t) {
-                old = atomicMax(lp, (int)t);
-            }
-        }
-        const int wa = a.off[side] >= 0 ? a.w4[side] : 0, wb = a.off[side + 2] >= 0 ? a.w4[side + 2] : 0;
-        const int W4 = wa + wb;
-        const float* prow = nullptr;  // packed mode: the row's summed gradient (batch b's rows)
-        if (a.packed != nullptr && in_b)
-            prow = a.packed + (side ? a.pk_items + (w - n0) * a.wrow[1] : w * a.wrow[0]);
-        f4 pp[NK], mm[NK], vv[NK], gg[NK];
-        int64_t ek[NK];
-#pragma unroll
-        for (int j = 0; j < NK; ++j) {
-            const int k = glane + j * LZ_GROUP;
-            if (k < W4) {
-                ek[j] = elem(side, id, k, wa);
-                pp[j] = *reinterpret_cast<const f4*>(a.p + ek[j]);
-                mm[j] = *reinterpret_cast<const f4*>(a.m + ek[j]);
-                vv[j] = *reinterpret_cast<const f4*>(a.v + ek[j]);
-                gg[j] = a.packed == nullptr ? *reinterpret_cast<const f4*>(a.g + ek[j])
-                      : (prow != nullptr ? *reinterpret_cast<const f4*>(prow + 4 * k) : zero);
-            }
-        }
-        // the next item's id requested before this one is waited for
-        const int64_t w2 = w + ngroups;
-        int side2 = 0, id2 = 0;
-        if (w2 < total) decode(w2, side2, id2);
-        old = __shfl(old, threadIdx.x & ~(LZ_GROUP - 1), 64);
+    }
+    int W[2], per[2];
+    for (int sd = 0; sd < 2; ++sd) {
+        W[sd] = lz_row_w4(a, sd);
+        per[sd] = W[sd] == 0 ? 0 : (W[sd] <= 64 ? 64 / W[sd] : 1);
+    }
+    int64_t tasks[6], tsum = 0;
+    for (int k = 0; k < 6; ++k) {
+        const int sd = k & 1;
+        tasks[k] = per[sd] == 0 ? 0 : (n[k] + per[sd] - 1) / per[sd];
+        tsum += tasks[k];
+    }
+    for (int64_t task = wave; task < tsum; task += nwaves) {
+        int k = 0;
+        int64_t q = task;
+        while (q >= tasks[k]) q -= tasks[k++];
+        const int sd = k & 1;
+        const int w = W[sd];
+        const int r = w <= 64 ? lane / w : 0;  // this lane's row of the task
+        const int64_t item = q * per[sd] + r;
+        if (r >= per[sd] || item >= n[k]) continue;
+        const int id = flush ? (int)item : a.ids[first[k] + item];
+        const int64_t slot = sd ? a.U + id : id;
+        const int old = a.last[slot];
+        const bool is_a = k < 2;  // A rows carry step t's gradient
         if (old < (int)t) {
-#pragma unroll
-            for (int j = 0; j < NK; ++j) {
-                const int k = glane + j * LZ_GROUP;
-                if (k >= W4) continue;
-                for (int s = old + 1; s < (int)t; ++s) {  // the steps this row sat out: g = 0
-                    const int64_t kw = s - (t - LZ_WIN);
-                    const float2 sc = kw >= 0 ? win[kw] : reinterpret_cast<const float2*>(a.ring)[s % a.ring_n];
-                    adam_f4(pp[j], mm[j], vv[j], zero, w1, b2, omb2, sc.y, eps, sc.x);
-                }
-                adam_f4(pp[j], mm[j], vv[j], gg[j], w1, b2, omb2, bc2s_t, eps, neg_t);
-                *reinterpret_cast<f4*>(a.m + ek[j]) = mm[j];
-                *reinterpret_cast<f4*>(a.v + ek[j]) = vv[j];
-                *reinterpret_cast<f4*>(a.p + ek[j]) = pp[j];
-                if (a.packed == nullptr && (gg[j].x != 0.f || gg[j].y != 0.f || gg[j].z != 0.f || gg[j].w != 0.f))
-                    *reinterpret_cast<f4*>(a.g + ek[j]) = zero;
+            const int k0 = w <= 64 ? lane - r * w : lane, kstep = w <= 64 ? w : 64;
+            for (int kk = k0; kk < w; kk += kstep) {
+                const int64_t e = lz_elem(a, sd, id, kk);
+                const float* grad = nullptr;
+                if (is_a)
+                    grad = a.packed != nullptr
+                               ? a.packed + (sd ? a.pk_items + item * a.wrow[1] : item * a.wrow[0]) + 4 * kk
+                               : a.g + e;
+                lz_update(a, e, old, t, grad, is_a && a.packed == nullptr, neg_t, bc2s_t, w1, b2, omb2, eps, win);
             }
-            // rows wider than NK * LZ_GROUP float4 (f + dm > 128): the rest one slot at a time
-            for (int k = glane + NK * LZ_GROUP; k < W4; k += LZ_GROUP) {
-                const int64_t e = elem(side, id, k, wa);
-                f4 p1 = *reinterpret_cast<const f4*>(a.p + e);
-                f4 m1 = *reinterpret_cast<const f4*>(a.m + e);
-                f4 v1 = *reinterpret_cast<const f4*>(a.v + e);
-                const f4 g1 = a.packed == nullptr ? *reinterpret_cast<const f4*>(a.g + e)
-                            : (prow != nullptr ? *reinterpret_cast<const f4*>(prow + 4 * k) : zero);
-                for (int s = old + 1; s < (int)t; ++s) {
-                    const int64_t kw = s - (t - LZ_WIN);
-                    const float2 sc = kw >= 0 ? win[kw] : reinterpret_cast<const float2*>(a.ring)[s % a.ring_n];
-                    adam_f4(p1, m1, v1, zero, w1, b2, omb2, sc.y, eps, sc.x);
-                }
-                adam_f4(p1, m1, v1, g1, w1, b2, omb2, bc2s_t, eps, neg_t);
-                *reinterpret_cast<f4*>(a.m + e) = m1;
-                *reinterpret_cast<f4*>(a.v + e) = v1;
-                *reinterpret_cast<f4*>(a.p + e) = p1;
-                if (a.packed == nullptr && (g1.x != 0.f || g1.y != 0.f || g1.z != 0.f || g1.w != 0.f))
-                    *reinterpret_cast<f4*>(a.g + e) = zero;
-            }
+            // every lane of the row has read `last` (one wave, in program order): publish t
+            if (lane == (w <= 64 ? r * w : 0)) a.last[slot] = (int)t;
         }
-        w = w2;
-        side = side2;
-        id = id2;
     }
 }
 
@@ -519,26 +485,25 @@ __global__ __launch_bounds__(256) void lazy_adam_kernel(const float* __restrict_
 #pragma clang fp contract(off)
     __shared__ float sc[2];
     __shared__ f4 part[16][16];
+    __shared__ float2 win[LZ_WIN];
     const int64_t t_step = ctl->snap_t;
     const int64_t b_step = ctl->snap_batch;
     if ((int)blockIdx.x < nA) {
         tower_reduce_adam_block(slab, lo, stride, rows, tb, tower_len, a.p, a.m, a.v, R, t_step, b_step, lr, beta1,
                                 beta2, eps, loss_hist, hist_len, wp, sc, part,
-                                a.packed != nullptr ? a.packed + a.pk_items + a.si * a.wrow[1] : nullptr);
+                                a.packed != nullptr ? a.packed + a.pk_tail : nullptr);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             a.ring[2 * (t_step % a.ring_n)] = sc[0];
             a.ring[2 * (t_step % a.ring_n) + 1] = sc[1];
         }
     } else {
-        __shared__ float2 win[LZ_WIN];
         stage_ring(a, t_step, win);
         step_scalars(t_step, lr, beta1, beta2, sc);
         __syncthreads();
         const int64_t b = ((b_step % a.nb) + a.nb) % a.nb;
-        const int64_t groups_per_block = blockDim.x / LZ_GROUP;
-        const int64_t gid = (int64_t)(blockIdx.x - nA) * groups_per_block + threadIdx.x / LZ_GROUP;
-        lazy_rows(a, t_step, b, false, sc[0], sc[1], (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), eps, gid,
-                  (int64_t)(gridDim.x - nA) * groups_per_block, win);
+        const int64_t wpb = blockDim.x >> 6;
+        lazy_rows(a, t_step, b, false, sc[0], sc[1], (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), eps, win,
+                  (int64_t)(blockIdx.x - nA) * wpb + (threadIdx.x >> 6), (int64_t)(gridDim.x - nA) * wpb);
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         ctl->adam_t = t_step;
@@ -554,42 +519,19 @@ __global__ __launch_bounds__(256) void lazy_flush_kernel(const ncf_step_ctl* ctl
     stage_ring(a, t, win);
     __syncthreads();
     const float* sc = a.ring + 2 * (t % a.ring_n);
-    const int64_t groups_per_block = blockDim.x / LZ_GROUP;
-    lazy_rows(a, t, 0, true, sc[0], sc[1], (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), eps,
-              (int64_t)blockIdx.x * groups_per_block + threadIdx.x / LZ_GROUP, (int64_t)gridDim.x * groups_per_block,
-              win);
+    const int64_t wpb = blockDim.x >> 6;
+    lazy_rows(a, t, 0, true, sc[0], sc[1], (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), eps, win,
+              (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6), (int64_t)gridDim.x * wpb);
 }
 
 // ---------------------------------------------------------------------------
-// Rows each global batch touches (ncf_batch_touched): one block per (batch, side),
-// an LDS bitmap of the side's ids set by the batch's rows, then the set bits
-// written out in id order (block prefix scan of per-thread popcounts).
+// ncf_batch_touched: per (global batch b, side) block, LDS bitmaps of the side's ids
+// in batch b and in batch b + 1; the three lists A, B, C of lazy_rows' comment.
+// Pass 0 counts them into seg[6 b + k + 1]; a one-block scan turns the counts into
+// offsets; pass 1 writes the ids in order (block prefix scans of popcounts).
 constexpr int BT_THREADS = 1024;
 
-__global__ __launch_bounds__(BT_THREADS) void batch_touched_kernel(const uint64_t* __restrict__ rows, int64_t n,
-                                                                   int64_t B, int U, int I, int64_t nb, int64_t su,
-                                                                   int64_t si, int32_t* __restrict__ out) {
-    extern __shared__ uint32_t bits[];
-    __shared__ int wsum[BT_THREADS / 64];
-    const int64_t b = blockIdx.x >> 1;
-    const int side = blockIdx.x & 1;
-    const int N = side ? I : U;
-    const int nw = (N + 31) / 32;
-    for (int k = threadIdx.x; k < nw; k += BT_THREADS) bits[k] = 0u;
-    __syncthreads();
-    const int64_t r0 = b * B, r1 = r0 + B < n ? r0 + B : n;
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += BT_THREADS) {
-        const uint64_t row = rows[r];
-        const uint32_t u = (uint32_t)row;
-        if (u == 0xffffffffu) continue;  // padding row
-        const uint32_t id = side ? (uint32_t)((row >> 32) & 0x7fffffffu) : u;
-        if (id < (uint32_t)N) atomicOr(&bits[id >> 5], 1u << (id & 31));
-    }
-    __syncthreads();
-    const int per = (nw + BT_THREADS - 1) / BT_THREADS;
-    const int w0 = threadIdx.x * per, w1 = w0 + per < nw ? w0 + per : nw;
-    int c = 0;
-    for (int w = w0; w < w1; ++w) c += __popc(bits[w]);
+__device__ __forceinline__ int bt_block_scan(int c, int* wsum, int* total) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int incl = c;
 #pragma unroll
@@ -597,53 +539,154 @@ __global__ __launch_bounds__(BT_THREADS) void batch_touched_kernel(const uint64_
         const int y = __shfl_up(incl, d, 64);
         if (lane >= d) incl += y;
     }
+    __syncthreads();
     if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    int base = 0;
-    for (int q = 0; q < wv; ++q) base += wsum[q];
-    int pos = base + incl - c;
-    int32_t* dst = side ? out + nb * su + b * si : out + b * su;
-    for (int w = w0; w < w1; ++w) {
-        uint32_t x = bits[w];
-        while (x) {
-            const int k = __ffs(x) - 1;
-            x &= x - 1;
-            dst[pos++] = w * 32 + k;
-        }
+    int base = 0, all = 0;
+    for (int q = 0; q < BT_THREADS / 64; ++q) {
+        if (q < wv) base += wsum[q];
+        all += wsum[q];
     }
-    if (threadIdx.x == BT_THREADS - 1) out[nb * (su + si) + 2 * b + side] = base + incl;
+    *total = all;
+    return base + incl - c;
 }
 
-// ncf_touched_pack: this rank's gradient of batch b's rows (users, then items; each
-// row its active tables' floats, g table first) into packed rows in list order,
-// the rows of grads cleared, stamp[row] = t << 32 | k; list slots past the batch's
-// count are zeroed so the all-reduce adds nothing stale.  One group per row slot.
-__global__ __launch_bounds__(256) void touched_pack_kernel(const ncf_step_ctl* __restrict__ ctl, LazyArgs a,
-                                                           float* __restrict__ packed) {
-    const int glane = threadIdx.x & (LZ_GROUP - 1);
-    const int64_t t = ctl->snap_t;
+__global__ __launch_bounds__(BT_THREADS) void batch_touched_kernel(const uint64_t* __restrict__ rows, int64_t n,
+                                                                   int64_t B, int U, int I, int64_t nb, int span,
+                                                                   int pass, int64_t* __restrict__ seg,
+                                                                   int32_t* __restrict__ ids) {
+    extern __shared__ uint32_t bits[];  // [cur | nxt], nw words each
+    __shared__ int wsum[BT_THREADS / 64];
+    const int64_t b = blockIdx.x >> 1;
+    const int side = blockIdx.x & 1;
+    const int N = side ? I : U;
+    const int nw = (N + 31) / 32;
+    uint32_t* cur = bits;
+    uint32_t* nxt = bits + nw;
+    const bool last_b = b + 1 >= nb;
+    for (int k = threadIdx.x; k < 2 * nw; k += BT_THREADS) bits[k] = 0u;
+    __syncthreads();
+    for (int h = 0; h < (last_b ? 1 : 2); ++h) {
+        uint32_t* bm = h ? nxt : cur;
+        const int64_t r0 = (b + h) * B, r1 = r0 + B < n ? r0 + B : n;
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += BT_THREADS) {
+            const uint64_t row = rows[r];
+            const uint32_t u = (uint32_t)row;
+            if (u == 0xffffffffu) continue;  // padding row
+            const uint32_t id = side ? (uint32_t)((row >> 32) & 0x7fffffffu) : u;
+            if (id < (uint32_t)N) atomicOr(&bm[id >> 5], 1u << (id & 31));
+        }
+    }
+    __syncthreads();
+    // slice (b % span) of the ids: [lo, hi)
+    const int64_t sl = span > 0 ? b % span : 0;
+    const int lo = span > 0 ? (int)(sl * N / span) : 0, hi = span > 0 ? (int)((sl + 1) * N / span) : 0;
+    const int per = (nw + BT_THREADS - 1) / BT_THREADS;
+    const int w0 = threadIdx.x * per, w1 = w0 + per < nw ? w0 + per : nw;
+    auto slice_mask = [&](int w) -> uint32_t {  // bits of word w inside [lo, hi)
+        const int a0 = w * 32, a1 = a0 + 32;
+        if (last_b || a1 <= lo || a0 >= hi) return 0u;
+        uint32_t m = 0xffffffffu;
+        if (lo > a0) m &= 0xffffffffu << (lo - a0);
+        if (hi < a1) m &= 0xffffffffu >> (a1 - hi);
+        return m;
+    };
+    auto tail_mask = [&](int w) -> uint32_t {  // ids < N
+        const int a1 = w * 32 + 32;
+        return a1 <= N ? 0xffffffffu : (0xffffffffu >> (a1 - N));
+    };
+    for (int list = 0; list < 3; ++list) {
+        auto word = [&](int w) -> uint32_t {
+            const uint32_t c = cur[w], x = nxt[w];
+            if (list == 0) return c;
+            if (list == 1) return last_b ? (~c & tail_mask(w)) : (x & ~c);
+            return slice_mask(w) & ~c & ~x;
+        };
+        int c = 0;
+        for (int w = w0; w < w1; ++w) c += __popc(word(w));
+        int total;
+        const int pos0 = bt_block_scan(c, wsum, &total);
+        const int64_t k = 6 * b + 2 * list + side;
+        if (pass == 0) {
+            if (threadIdx.x == 0) seg[k + 1] = total;
+        } else {
+            int32_t* dst = ids + seg[k];
+            int pos = pos0;
+            for (int w = w0; w < w1; ++w) {
+                uint32_t x = word(w);
+                while (x) {
+                    const int q = __ffs(x) - 1;
+                    x &= x - 1;
+                    dst[pos++] = w * 32 + q;
+                }
+            }
+        }
+    }
+}
+
+// counts (seg[1 .. m]) -> offsets (seg[0 .. m]), one block
+__global__ __launch_bounds__(BT_THREADS) void touched_scan_kernel(int64_t* __restrict__ seg, int64_t m) {
+    __shared__ int64_t wsum[BT_THREADS / 64];
+    const int per = (int)((m + BT_THREADS - 1) / BT_THREADS);
+    const int64_t i0 = (int64_t)threadIdx.x * per, i1 = i0 + per < m ? i0 + per : m;
+    int64_t c = 0;
+    for (int64_t i = i0; i < i1; ++i) c += seg[i + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int64_t incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int64_t base = 0;
+    for (int q = 0; q < wv; ++q) base += wsum[q];
+    int64_t run = base + incl - c;
+    __syncthreads();
+    for (int64_t i = i0; i < i1; ++i) {
+        const int64_t v = seg[i + 1];
+        seg[i + 1] = run + v;  // inclusive: seg[i + 1] = offset of segment i + 1
+        run += v;
+    }
+    if (threadIdx.x == 0) seg[0] = 0;
+}
+
+// ncf_touched_pack: this rank's gradient of batch b's A rows (users, then items;
+// each row its active tables' floats, g table first) into packed slots in list
+// order, those rows of grads cleared; slots past the batch's count are zeroed so
+// the all-reduce adds nothing stale.  One wave task per group of rows.
+__global__ __launch_bounds__(256) void touched_pack_kernel(const ncf_step_ctl* __restrict__ ctl, LazyArgs a, int64_t su,
+                                                           int64_t si, float* __restrict__ packed) {
+    const int lane = threadIdx.x & 63;
     const int64_t b = ((ctl->snap_batch % a.nb) + a.nb) % a.nb;
-    const int32_t* cnt = a.touched + a.nb * (a.su + a.si);
-    const int64_t nu = cnt[2 * b], ni = cnt[2 * b + 1];
-    const int64_t groups = (int64_t)gridDim.x * (blockDim.x / LZ_GROUP);
+    const int64_t nu = a.seg[6 * b + 1] - a.seg[6 * b], ni = a.seg[6 * b + 2] - a.seg[6 * b + 1];
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
-    for (int64_t w = (int64_t)blockIdx.x * (blockDim.x / LZ_GROUP) + threadIdx.x / LZ_GROUP; w < a.su + a.si;
-         w += groups) {
-        const int side = w < a.su ? 0 : 1;
-        const int64_t k = side ? w - a.su : w;
-        float* dst = packed + (side ? a.pk_items + k * a.wrow[1] : k * a.wrow[0]);
-        const int sa = side, sb = side + 2;
-        const int wa = a.off[sa] >= 0 ? a.w4[sa] : 0, wb = a.off[sb] >= 0 ? a.w4[sb] : 0;
-        if (k >= (side ? ni : nu)) {
-            for (int c = glane; c < wa + wb; c += LZ_GROUP) *reinterpret_cast<f4*>(dst + 4 * c) = zero;
+    int W[2], per[2];
+    for (int sd = 0; sd < 2; ++sd) {
+        W[sd] = lz_row_w4(a, sd);
+        per[sd] = W[sd] == 0 ? 0 : (W[sd] <= 64 ? 64 / W[sd] : 1);
+    }
+    const int64_t tu = per[0] ? (su + per[0] - 1) / per[0] : 0, ti = per[1] ? (si + per[1] - 1) / per[1] : 0;
+    for (int64_t task = wave; task < tu + ti; task += nwaves) {
+        const int sd = task < tu ? 0 : 1;
+        const int64_t q = sd ? task - tu : task;
+        const int w = W[sd];
+        const int r = w <= 64 ? lane / w : 0;
+        const int64_t item = q * per[sd] + r;
+        if (r >= per[sd] || item >= (sd ? si : su)) continue;
+        float* dst = packed + (sd ? a.pk_items + item * a.wrow[1] : item * a.wrow[0]);
+        const int k0 = w <= 64 ? lane - r * w : lane, kstep = w <= 64 ? w : 64;
+        if (item >= (sd ? ni : nu)) {
+            for (int kk = k0; kk < w; kk += kstep) *reinterpret_cast<f4*>(dst + 4 * kk) = zero;
             continue;
         }
-        const int id = side ? a.touched[a.nb * a.su + b * a.si + k] : a.touched[b * a.su + k];
-        if (glane == 0) const_cast<int64_t*>(a.stamp)[side ? a.U + id : id] = (t << 32) | k;
-        for (int c = glane; c < wa + wb; c += LZ_GROUP) {
-            const int64_t e = c < wa ? a.off[sa] + ((int64_t)id * a.w4[sa] + c) * 4
-                                     : a.off[sb] + ((int64_t)id * a.w4[sb] + (c - wa)) * 4;
-            *reinterpret_cast<f4*>(dst + 4 * c) = *reinterpret_cast<const f4*>(a.g + e);
+        const int id = a.ids[a.seg[6 * b + sd] + item];
+        for (int kk = k0; kk < w; kk += kstep) {
+            const int64_t e = lz_elem(a, sd, id, kk);
+            *reinterpret_cast<f4*>(dst + 4 * kk) = *reinterpret_cast<const f4*>(a.g + e);
             *reinterpret_cast<f4*>(a.g + e) = zero;
         }
     }
@@ -1802,11 +1845,24 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
     return launch_status();
 }
 
-// ---- deferred Adam (ABI 13)
+// ---- deferred Adam (ABI 14)
+// C-list slice count: a row not touched by two consecutive batches falls at most
+// this many steps behind (NCF_LAZY_SPAN, default 32, < LZ_WIN)
+static int lazy_span() {
+    static const int span = [] {
+        const char* e = getenv("NCF_LAZY_SPAN");
+        const int v = e ? atoi(e) : 32;
+        return v < 1 ? 1 : (v > LZ_WIN - 2 ? LZ_WIN - 2 : v);
+    }();
+    return span;
+}
+
+constexpr int LZ_MAX_ROWS = 1 << 19;  // per side: two LDS bitmaps of the ids in ncf_batch_touched
+
 static int lazy_args(const ncf_layout* lay, float* params, float* grads, float* m, float* v, const int64_t* ranges,
                      int nranges, int32_t* last, float* ring, int64_t ring_n, LazyArgs* a) {
     const int f = lay->factor_num, dm = f << (lay->num_layers - 1);
-    if (f % 4 != 0 || lay->user_num > (1 << 20) || lay->item_num > (1 << 20)) return NCF_E_UNSUPPORTED;
+    if (f % 4 != 0 || lay->user_num > LZ_MAX_ROWS || lay->item_num > LZ_MAX_ROWS) return NCF_E_UNSUPPORTED;
     const int64_t offs[4] = {lay->ug, lay->ig, lay->um, lay->im};
     const int64_t widths[4] = {f, f, dm, dm};
     const int64_t nrows[4] = {lay->user_num, lay->item_num, lay->user_num, lay->item_num};
@@ -1819,12 +1875,6 @@ static int lazy_args(const ncf_layout* lay, float* params, float* grads, float* 
         a->off[k] = act ? offs[k] : -1;
         a->w4[k] = (int)(widths[k] / 4);
     }
-    static const int span = [] {
-        const char* e = getenv("NCF_LAZY_SPAN");
-        const int v = e ? atoi(e) : 32;
-        return v < 0 ? 0 : (v > LZ_WIN - 2 ? LZ_WIN - 2 : v);
-    }();
-    a->span = span;
     a->p = params;
     a->g = grads;
     a->m = m;
@@ -1837,31 +1887,76 @@ static int lazy_args(const ncf_layout* lay, float* params, float* grads, float* 
     return NCF_OK;
 }
 
-static void touched_shape(int64_t n, int64_t B, int U, int I, int64_t* nb, int64_t* su, int64_t* si) {
-    *nb = (n + B - 1) / B;
-    *su = U < B ? U : B;
-    *si = I < B ? I : B;
+// touched-list geometry: batches, per-batch A slots per side, id capacity
+struct TouchedShape {
+    int64_t nb, su, si, segs, cap;
+};
+
+static TouchedShape touched_shape(int64_t n, int64_t B, int U, int I) {
+    TouchedShape t;
+    t.nb = (n + B - 1) / B;
+    t.su = U < B ? U : B;
+    t.si = I < B ? I : B;
+    t.segs = 6 * t.nb + 1;
+    const int span = lazy_span();
+    // per batch and side: |A| + |B| <= min(N, 2 min(N, B)), |C| <= N / span + 1; the
+    // last batch lists every id once
+    const int64_t ab = (U < 2 * t.su ? U : 2 * t.su) + (I < 2 * t.si ? I : 2 * t.si);
+    t.cap = t.nb * (ab + U / span + I / span + 2) + U + I;
+    return t;
 }
 
 int64_t ncf_touched_bytes(int64_t n, int64_t batch_global, int user_num, int item_num) {
     if (n <= 0 || batch_global <= 0 || user_num <= 0 || item_num <= 0) return -1;
-    int64_t nb, su, si;
-    touched_shape(n, batch_global, user_num, item_num, &nb, &su, &si);
-    return 4 * (nb * (su + si) + 2 * nb);
+    const TouchedShape t = touched_shape(n, batch_global, user_num, item_num);
+    return (8 * t.segs + 4 * t.cap + 15) / 16 * 16;
+}
+
+static void touched_lists(LazyArgs* a, const int32_t* touched, const TouchedShape& t) {
+    a->nb = t.nb;
+    a->seg = reinterpret_cast<const int64_t*>(touched);
+    a->ids = touched + 2 * t.segs;
 }
 
 int ncf_batch_touched(const uint64_t* rows, int64_t n, int64_t batch_global, int user_num, int item_num,
                       int32_t* touched, void* stream) {
     if (!rows || !touched || n <= 0 || batch_global <= 0 || user_num <= 0 || item_num <= 0) return NCF_E_ARG;
-    if (user_num > (1 << 20) || item_num > (1 << 20)) return NCF_E_UNSUPPORTED;
-    int64_t nb, su, si;
-    touched_shape(n, batch_global, user_num, item_num, &nb, &su, &si);
+    if ((reinterpret_cast<uintptr_t>(touched) & 7) != 0) return NCF_E_ARG;
+    if (user_num > LZ_MAX_ROWS || item_num > LZ_MAX_ROWS) return NCF_E_UNSUPPORTED;
+    const TouchedShape t = touched_shape(n, batch_global, user_num, item_num);
     const int mx = user_num > item_num ? user_num : item_num;
-    const int64_t lds = (int64_t)((mx + 31) / 32) * 4;
+    const int64_t lds = 2 * (int64_t)((mx + 31) / 32) * 4;
     if (lds > 64 * 1024 && ensure_lds((const void*)batch_touched_kernel, lds) != NCF_OK) return NCF_E_LAUNCH;
-    hipLaunchKernelGGL(batch_touched_kernel, dim3((unsigned)(2 * nb)), dim3(BT_THREADS), (size_t)lds,
-                       (hipStream_t)stream, rows, n, batch_global, user_num, item_num, nb, su, si, touched);
+    int64_t* seg = reinterpret_cast<int64_t*>(touched);
+    int32_t* ids = touched + 2 * t.segs;
+    const int span = lazy_span();
+    hipLaunchKernelGGL(batch_touched_kernel, dim3((unsigned)(2 * t.nb)), dim3(BT_THREADS), (size_t)lds,
+                       (hipStream_t)stream, rows, n, batch_global, user_num, item_num, t.nb, span, 0, seg, ids);
+    hipLaunchKernelGGL(touched_scan_kernel, dim3(1), dim3(BT_THREADS), 0, (hipStream_t)stream, seg, t.segs - 1);
+    hipLaunchKernelGGL(batch_touched_kernel, dim3((unsigned)(2 * t.nb)), dim3(BT_THREADS), (size_t)lds,
+                       (hipStream_t)stream, rows, n, batch_global, user_num, item_num, t.nb, span, 1, seg, ids);
     return launch_status();
+}
+
+// blocks for one step's rows: an upper bound of its wave tasks, 4 waves a block
+static int64_t lazy_blocks(const LazyArgs& a, int64_t rows_u, int64_t rows_i) {
+    int64_t waves = 0;
+    for (int sd = 0; sd < 2; ++sd) {
+        const int w = (a.off[sd] >= 0 ? a.w4[sd] : 0) + (a.off[sd + 2] >= 0 ? a.w4[sd + 2] : 0);
+        if (w == 0) continue;
+        const int per = w <= 64 ? 64 / w : 1;
+        waves += ((sd ? rows_i : rows_u) + per - 1) / per;
+    }
+    int64_t nB = (waves + 3) / 4;
+    if (nB > 2048) nB = 2048;
+    return nB < 1 ? 1 : nB;
+}
+
+static int64_t step_blocks(const LazyArgs& a, const TouchedShape& t) {
+    const int span = lazy_span();
+    const int64_t ru = (a.U < 2 * t.su ? a.U : 2 * t.su) + a.U / span + 1;
+    const int64_t ri = (a.I < 2 * t.si ? a.I : 2 * t.si) + a.I / span + 1;
+    return lazy_blocks(a, ru, ri);
 }
 
 int ncf_lazy_adam_step(const ncf_layout* lay, const void* workspace, float* params, float* grads, float* exp_avg,
@@ -1870,7 +1965,7 @@ int ncf_lazy_adam_step(const ncf_layout* lay, const void* workspace, float* para
                        const int32_t* touched, int64_t n_total, int64_t batch_global, int32_t* last_step,
                        float* step_scalars, int64_t ring, void* stream) {
     if (!lay || !workspace || !params || !grads || !exp_avg || !exp_avg_sq || !ranges || !ctl || !touched ||
-        !last_step || !step_scalars || n_total <= 0 || batch_global <= 0)
+        !last_step || !step_scalars || n_total <= 0 || batch_global <= 0 || ring < LZ_WIN + 2)
         return NCF_E_ARG;
     int err = 0;
     Ranges R = make_ranges(ranges, nranges, &err);
@@ -1878,16 +1973,13 @@ int ncf_lazy_adam_step(const ncf_layout* lay, const void* workspace, float* para
     LazyArgs a;
     const int rc = lazy_args(lay, params, grads, exp_avg, exp_avg_sq, ranges, nranges, last_step, step_scalars, ring, &a);
     if (rc != NCF_OK) return rc;
-    touched_shape(n_total, batch_global, lay->user_num, lay->item_num, &a.nb, &a.su, &a.si);
-    if (ring < a.nb + 2) return NCF_E_ARG;  // a row's gap is at most one epoch: the last batch flushes
-    a.touched = touched;
+    const TouchedShape t = touched_shape(n_total, batch_global, lay->user_num, lay->item_num);
+    touched_lists(&a, touched, t);
     const int stride = (int)ncf_slab_stride(lay);
     const int lo = slab_lo(lay);
     const int nA = (stride - lo + 63) / 64;
     const int rows = reduce_rows(lay);
-    const int64_t work = 2 * (a.su + a.si) > a.su + a.si + a.U + a.I ? 2 * (a.su + a.si) : a.su + a.si + a.U + a.I;
-    int64_t nB = (work + (256 / LZ_GROUP) - 1) / (256 / LZ_GROUP);
-    if (nB > 2048) nB = 2048;
+    const int64_t nB = step_blocks(a, t);
     hipLaunchKernelGGL(lazy_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
                        static_cast<const float*>(workspace), lo, stride, rows, nA, lay->tower_begin, lay->tower_len, R,
                        ctl, lr, beta1, beta2, (float)eps, loss_hist, hist_len, w0_part(lay, workspace), a);
@@ -1896,14 +1988,12 @@ int ncf_lazy_adam_step(const ncf_layout* lay, const void* workspace, float* para
 
 // packed mode geometry: floats per packed user / item row, the item rows' offset,
 // the tail (tower gradient + loss, ncf_slab_stride floats) and the total
-static int packed_geometry(const ncf_layout* lay, const LazyArgs& a, int64_t su, int64_t si, int* wrow,
-                           int64_t* pk_items, int64_t* tail, int64_t* total) {
-    wrow[0] = 4 * ((a.off[0] >= 0 ? a.w4[0] : 0) + (a.off[2] >= 0 ? a.w4[2] : 0));
-    wrow[1] = 4 * ((a.off[1] >= 0 ? a.w4[1] : 0) + (a.off[3] >= 0 ? a.w4[3] : 0));
-    *pk_items = su * wrow[0];
-    *tail = *pk_items + si * wrow[1];
-    *total = *tail + ncf_slab_stride(lay);
-    return NCF_OK;
+static void packed_geometry(const ncf_layout* lay, LazyArgs* a, int64_t su, int64_t si, int64_t* total) {
+    a->wrow[0] = 4 * ((a->off[0] >= 0 ? a->w4[0] : 0) + (a->off[2] >= 0 ? a->w4[2] : 0));
+    a->wrow[1] = 4 * ((a->off[1] >= 0 ? a->w4[1] : 0) + (a->off[3] >= 0 ? a->w4[3] : 0));
+    a->pk_items = su * a->wrow[0];
+    a->pk_tail = a->pk_items + si * a->wrow[1];
+    *total = a->pk_tail + ncf_slab_stride(lay);
 }
 
 int64_t ncf_touched_packed_floats(const ncf_layout* lay, const int64_t* ranges, int nranges, int64_t batch_global) {
@@ -1911,37 +2001,33 @@ int64_t ncf_touched_packed_floats(const ncf_layout* lay, const int64_t* ranges, 
     LazyArgs a;
     if (lazy_args(lay, nullptr, nullptr, nullptr, nullptr, ranges, nranges, nullptr, nullptr, 1, &a) != NCF_OK)
         return -1;
-    int64_t nb, su, si, pk, tail, total;
-    int wrow[2];
-    touched_shape(1, batch_global, lay->user_num, lay->item_num, &nb, &su, &si);
-    packed_geometry(lay, a, su, si, wrow, &pk, &tail, &total);
+    const TouchedShape t = touched_shape(1, batch_global, lay->user_num, lay->item_num);
+    int64_t total;
+    packed_geometry(lay, &a, t.su, t.si, &total);
     return total;
 }
 
 int ncf_touched_pack(const ncf_layout* lay, const void* workspace, float* grads, const int64_t* ranges, int nranges,
                      const int32_t* touched, int64_t n_total, int64_t batch_global, const ncf_step_ctl* ctl,
-                     float* packed, int64_t* stamp, void* stream) {
-    if (!lay || !workspace || !grads || !ranges || !touched || !ctl || !packed || !stamp || n_total <= 0 ||
-        batch_global <= 0)
+                     float* packed, void* stream) {
+    if (!lay || !workspace || !grads || !ranges || !touched || !ctl || !packed || n_total <= 0 || batch_global <= 0)
         return NCF_E_ARG;
     LazyArgs a;
     const int rc = lazy_args(lay, nullptr, grads, nullptr, nullptr, ranges, nranges, nullptr, nullptr, 1, &a);
     if (rc != NCF_OK) return rc;
-    touched_shape(n_total, batch_global, lay->user_num, lay->item_num, &a.nb, &a.su, &a.si);
-    a.touched = touched;
-    a.stamp = stamp;
-    int64_t tail, total;
-    packed_geometry(lay, a, a.su, a.si, a.wrow, &a.pk_items, &tail, &total);
+    const TouchedShape t = touched_shape(n_total, batch_global, lay->user_num, lay->item_num);
+    touched_lists(&a, touched, t);
+    int64_t total;
+    packed_geometry(lay, &a, t.su, t.si, &total);
     // tower gradient (slab rows, W0 partials; loss at tower_len) into the tail
     const int stride = (int)ncf_slab_stride(lay);
     const int lo = slab_lo(lay);
     hipLaunchKernelGGL(reduce_slab_kernel, dim3((stride - lo + 63) / 64), dim3(256), 0, (hipStream_t)stream,
-                       static_cast<const float*>(workspace), packed + tail, lo, stride, reduce_rows(lay),
+                       static_cast<const float*>(workspace), packed + a.pk_tail, lo, stride, reduce_rows(lay),
                        (ncf_step_ctl*)nullptr, w0_part(lay, workspace));
     // tail[0, lo) is never written: it stays as allocated (zero), and sums to zero
-    int64_t nB = (a.su + a.si + (256 / LZ_GROUP) - 1) / (256 / LZ_GROUP);
-    if (nB > 2048) nB = 2048;
-    hipLaunchKernelGGL(touched_pack_kernel, dim3((unsigned)nB), dim3(256), 0, (hipStream_t)stream, ctl, a, packed);
+    hipLaunchKernelGGL(touched_pack_kernel, dim3((unsigned)lazy_blocks(a, t.su, t.si)), dim3(256), 0,
+                       (hipStream_t)stream, ctl, a, t.su, t.si, packed);
     return launch_status();
 }
 
@@ -1949,9 +2035,9 @@ int ncf_lazy_adam_step_packed(const ncf_layout* lay, float* params, float* exp_a
                               const int64_t* ranges, int nranges, ncf_step_ctl* ctl, double lr, double beta1,
                               double beta2, double eps, float* loss_hist, int64_t hist_len, const int32_t* touched,
                               int64_t n_total, int64_t batch_global, int32_t* last_step, float* step_scalars,
-                              int64_t ring, const float* packed, const int64_t* stamp, void* stream) {
+                              int64_t ring, const float* packed, void* stream) {
     if (!lay || !params || !exp_avg || !exp_avg_sq || !ranges || !ctl || !touched || !last_step || !step_scalars ||
-        !packed || !stamp || n_total <= 0 || batch_global <= 0)
+        !packed || n_total <= 0 || batch_global <= 0 || ring < LZ_WIN + 2)
         return NCF_E_ARG;
     int err = 0;
     Ranges R = make_ranges(ranges, nranges, &err);
@@ -1960,19 +2046,15 @@ int ncf_lazy_adam_step_packed(const ncf_layout* lay, float* params, float* exp_a
     const int rc = lazy_args(lay, params, nullptr, exp_avg, exp_avg_sq, ranges, nranges, last_step, step_scalars,
                              ring, &a);
     if (rc != NCF_OK) return rc;
-    touched_shape(n_total, batch_global, lay->user_num, lay->item_num, &a.nb, &a.su, &a.si);
-    if (ring < a.nb + 2) return NCF_E_ARG;
-    a.touched = touched;
+    const TouchedShape t = touched_shape(n_total, batch_global, lay->user_num, lay->item_num);
+    touched_lists(&a, touched, t);
     a.packed = packed;
-    a.stamp = stamp;
-    int64_t tail, total;
-    packed_geometry(lay, a, a.su, a.si, a.wrow, &a.pk_items, &tail, &total);
+    int64_t total;
+    packed_geometry(lay, &a, t.su, t.si, &total);
     const int stride = (int)ncf_slab_stride(lay);
     const int lo = slab_lo(lay);
     const int nA = (stride - lo + 63) / 64;
-    const int64_t work = 2 * (a.su + a.si) > a.su + a.si + a.U + a.I ? 2 * (a.su + a.si) : a.su + a.si + a.U + a.I;
-    int64_t nB = (work + (256 / LZ_GROUP) - 1) / (256 / LZ_GROUP);
-    if (nB > 2048) nB = 2048;
+    const int64_t nB = step_blocks(a, t);
     hipLaunchKernelGGL(lazy_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
                        (const float*)nullptr, lo, stride, 0, nA, lay->tower_begin, lay->tower_len, R, ctl, lr, beta1,
                        beta2, (float)eps, loss_hist, hist_len, W0Part{nullptr, 0, 0, 0, 0}, a);
@@ -1983,17 +2065,15 @@ int ncf_lazy_adam_flush(const ncf_layout* lay, float* params, float* grads, floa
                         const int64_t* ranges, int nranges, const ncf_step_ctl* ctl, double beta1, double beta2,
                         double eps, int32_t* last_step, const float* step_scalars, int64_t ring, void* stream) {
     if (!lay || !params || !grads || !exp_avg || !exp_avg_sq || !ranges || !ctl || !last_step || !step_scalars ||
-        ring <= 0)
+        ring < LZ_WIN + 2)
         return NCF_E_ARG;
     LazyArgs a;
     const int rc = lazy_args(lay, params, grads, exp_avg, exp_avg_sq, ranges, nranges, last_step,
                              const_cast<float*>(step_scalars), ring, &a);
     if (rc != NCF_OK) return rc;
     a.nb = 1;
-    int64_t nB = ((int64_t)a.U + a.I + (256 / LZ_GROUP) - 1) / (256 / LZ_GROUP);
-    if (nB > 2048) nB = 2048;
-    hipLaunchKernelGGL(lazy_flush_kernel, dim3((unsigned)nB), dim3(256), 0, (hipStream_t)stream, ctl, beta1, beta2,
-                       (float)eps, a);
+    hipLaunchKernelGGL(lazy_flush_kernel, dim3((unsigned)lazy_blocks(a, a.U, a.I)), dim3(256), 0, (hipStream_t)stream,
+                       ctl, beta1, beta2, (float)eps, a);
     return launch_status();
 }
 

@@ -61,6 +61,15 @@ def _active_ranges(model, lay, extra=None):
     return merged
 
 
+def touched_segments(buf, nb):
+    """Host view of an ncf_batch_touched buffer (int32 numpy copy): [b][k] id arrays,
+    k = 2 * list + side (lists A, B, C; side 0 users, 1 items) -- include/ncf_hip.h."""
+    import numpy as np
+    seg = np.ascontiguousarray(buf[:2 * (6 * nb + 1)]).view(np.int64)
+    ids = buf[2 * (6 * nb + 1):]
+    return [[ids[seg[6 * b + k]:seg[6 * b + k + 1]] for k in range(6)] for b in range(nb)]
+
+
 class TrainEngine:
     # world > 1 default exchange: one all-reduce + replicated Adam up to this many flat
     # floats, zero1 (reduce-scatter, shard Adam, all-gather: the same wire bytes) above.
@@ -89,8 +98,8 @@ class TrainEngine:
         self.distill = distill
         self.world_size, self.rank, self.group = int(world_size), int(rank), process_group
         lay = L.layout(model.user_num, model.item_num, model.factor_num, model.num_layers, model.model_type)
-        touched_ok = (optimizer == "adam" and model.factor_num % 4 == 0 and model.user_num <= (1 << 20)
-                      and model.item_num <= (1 << 20))
+        touched_ok = (optimizer == "adam" and model.factor_num % 4 == 0 and model.user_num <= (1 << 19)
+                      and model.item_num <= (1 << 19))
         if dp_mode is None:
             dp_mode = os.environ.get("NCF_DP_MODE", self.default_dp_mode(int(lay.total), touched_ok)) \
                 if self.world_size > 1 else "single"
@@ -99,7 +108,7 @@ class TrainEngine:
         if dp_mode not in ("single", "zero1", "allreduce", "sparse", "touched"):
             raise ValueError(f"dp_mode {dp_mode!r}")
         if dp_mode == "touched" and not touched_ok:
-            raise ValueError("dp_mode 'touched' needs Adam, factor_num % 4 == 0 and tables of <= 2^20 rows")
+            raise ValueError("dp_mode 'touched' needs Adam, factor_num % 4 == 0 and tables of <= 2^19 rows")
         self.dp_mode = dp_mode
         if dp_mode in ("zero1", "sparse"):
             # flat buffers padded to world x shard floats; rank r owns [r*S, (r+1)*S)
@@ -184,7 +193,6 @@ class TrainEngine:
             self._packed = torch.zeros(int(L.hip().ncf_touched_packed_floats(ctypes.byref(self.lay), self._ranges,
                                                                              self._nranges, 1)),
                                        dtype=torch.float32, device=dev)  # resized per batch size
-            self._stamp = torch.zeros(model.user_num + model.item_num, dtype=torch.int64, device=dev)
 
     # ------------------------------------------------------------------ data
     def set_epoch_stream(self, rows, batch_size, checked=False):
@@ -268,8 +276,8 @@ class TrainEngine:
         return buf
 
     # deferred Adam: steps a row may sit out are replayed from this ring of step
-    # scalars (a row's gap is at most one epoch: the last batch brings every row up)
-    LAZY_RING = 1 << 17
+    # scalars (a row's gap is at most NCF_LAZY_SPAN steps; > 514 entries required)
+    LAZY_RING = 1 << 12
     # on by default where it moves fewer bytes than dense Adam: tables with more rows
     # than LAZY_RATIO x the global batch (C2, C4, C5; not C3's ml-1m at 65,536)
     LAZY_RATIO = float(os.environ.get("NCF_LAZY_RATIO", "2"))
@@ -277,7 +285,7 @@ class TrainEngine:
     def _lazy_wanted(self):
         """Deferred Adam for this stream (always with dp_mode "touched"): single-process
         Adam (the fused optimizer launch), factor_num % 4 == 0, tables <= 2^20 rows,
-        epochs shorter than the ring; NCF_LAZY_ADAM=1 turns it on for single-process
+        tables <= 2^19 rows; NCF_LAZY_ADAM=1 turns it on for single-process
         training (auto: tables larger than LAZY_RATIO x the global batch), 0 (the
         default) keeps the dense launch, measured faster on MI355X at C2, C4 and C5
         (DESIGN 3.2a)."""
@@ -287,7 +295,7 @@ class TrainEngine:
         if env == "0" or not self._fused_optimizer:
             return False
         U, I = self.model.user_num, self.model.item_num
-        if self.model.factor_num % 4 or U > (1 << 20) or I > (1 << 20) or self.num_batches + 2 > self.LAZY_RING:
+        if self.model.factor_num % 4 or U > (1 << 19) or I > (1 << 19):
             return False
         return env == "1" or (U + I) > self.LAZY_RATIO * self.batch_size
 
@@ -337,7 +345,7 @@ class TrainEngine:
             L.check(L.hip().ncf_touched_pack(ctypes.byref(self.lay), self.ws.data_ptr(), self.grads.data_ptr(),
                                              self._ranges, self._nranges, self._touched_buf(self.rows).data_ptr(),
                                              self.n_total, self.batch_size, self.ctl.data_ptr(),
-                                             self._packed.data_ptr(), self._stamp.data_ptr(), st),
+                                             self._packed.data_ptr(), st),
                     "ncf_touched_pack")
             return
         L.check(L.hip().ncf_reduce_slab(ctypes.byref(self.lay), self.ws.data_ptr(), self.grads.data_ptr(),
@@ -398,8 +406,8 @@ class TrainEngine:
                                                   self.loss_hist.data_ptr(), hist_len,
                                                   self._touched_buf(self.rows).data_ptr(), self.n_total,
                                                   self.batch_size, self._last.data_ptr(), self._ring.data_ptr(),
-                                                  self.LAZY_RING, self._packed.data_ptr(), self._stamp.data_ptr(),
-                                                  st), "ncf_lazy_adam_step_packed")
+                                                  self.LAZY_RING, self._packed.data_ptr(), st),
+                                                  "ncf_lazy_adam_step_packed")
             return
         if self.dp_mode in ("zero1", "sparse"):
             if self.dp_mode == "zero1":  # the shard gradient is in gshard: clear the local bucket now

@@ -10,7 +10,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 CONFIG="${CONFIG:-c3}"
-ARGS="--config $CONFIG --steps ${STEPS:-60} --warmup 5 --skip-cpu-baseline --skip-eval --kernel-steps 5 --e2e-epochs 0"
+ARGS="--config $CONFIG --steps ${STEPS:-60} --warmup 5 --skip-cpu-baseline --skip-eval --kernel-steps 5 --e2e-epochs 0 --profile-run"
 step() {
     local name=$1; shift
     echo "== $name"

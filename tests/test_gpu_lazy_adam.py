@@ -1,8 +1,9 @@
-"""Deferred ("catch-up") Adam (ncf_lazy_adam_step / ncf_lazy_adam_flush, ABI 13) vs
+"""Deferred ("catch-up") Adam (ncf_lazy_adam_step / ncf_lazy_adam_flush, ABI 14) vs
 the dense optimizer launch (ncf_reduce_adam_step: torch.optim.Adam of
 train_neumf.py:90,115 over every row every step) -- bitwise, on deterministic
 gradients at the C4 id space (138,494 users x 26,745 items), over two epochs of
-batches; plus the per-batch touched-row lists (ncf_batch_touched) vs numpy."""
+batches; plus the per-batch A / B / C lists (ncf_batch_touched) vs numpy."""
+import os
 import ctypes
 
 import numpy as np
@@ -28,28 +29,53 @@ def _stream(nb, B, seed):
     return rows, n
 
 
+SPAN = int(os.environ.get("NCF_LAZY_SPAN", "32"))
+
+
+def _batch_ids(rows, b, B):
+    seg = rows[b * B:(b + 1) * B]
+    seg = seg[(seg & 0xFFFFFFFF) != 0xFFFFFFFF]
+    return np.unique(seg & 0xFFFFFFFF), np.unique((seg >> 32) & 0x7FFFFFFF)
+
+
+def _expected_lists(rows, n, B):
+    """[b][k] (k = 2 * list + side) per include/ncf_hip.h ncf_batch_touched."""
+    nb = -(-n // B)
+    R = [_batch_ids(rows, b, B) for b in range(nb)]
+    out = []
+    for b in range(nb):
+        lists = [None] * 6
+        for side, N in ((0, U), (1, I)):
+            a = R[b][side]
+            if b + 1 < nb:
+                nx = np.setdiff1d(R[b + 1][side], a)
+                sl = b % SPAN
+                c = np.arange(sl * N // SPAN, (sl + 1) * N // SPAN)
+                c = np.setdiff1d(c, np.union1d(a, R[b + 1][side]))
+            else:
+                nx = np.setdiff1d(np.arange(N), a)
+                c = np.zeros(0, np.int64)
+            lists[side], lists[2 + side], lists[4 + side] = a, nx, c
+        out.append(lists)
+    return out
+
+
 def test_batch_touched_lists_match_numpy():
     import ncf_amd._lib as L
+    from ncf_amd.engine import touched_segments
     lib = L.hip()
     dev = torch.device("cuda", 0)
-    for B, nb, seed in ((4096, 9, 0), (65536, 3, 1), (1000, 5, 2)):
+    for B, nb, seed in ((4096, 9, 0), (65536, 3, 1), (1000, 40, 2)):
         rows, n = _stream(nb, B, seed)
         rd = torch.from_numpy(rows).to(dev)
         nbytes = lib.ncf_touched_bytes(n, B, U, I)
         buf = torch.full(((nbytes + 3) // 4,), -7, dtype=torch.int32, device=dev)
         L.check(lib.ncf_batch_touched(rd.data_ptr(), n, B, U, I, buf.data_ptr(), L.stream_ptr(dev)), "touched")
-        t = buf.cpu().numpy()
-        su, si, k = min(U, B), min(I, B), -(-n // B)
-        assert k == nb
-        cnt = t[k * (su + si): k * (su + si) + 2 * k].reshape(k, 2)
-        for b in range(k):
-            seg = rows[b * B:(b + 1) * B]
-            seg = seg[(seg & 0xFFFFFFFF) != 0xFFFFFFFF]
-            eu = np.unique(seg & 0xFFFFFFFF)
-            ei = np.unique((seg >> 32) & 0x7FFFFFFF)
-            assert cnt[b, 0] == len(eu) and cnt[b, 1] == len(ei)
-            assert np.array_equal(t[b * su: b * su + len(eu)], eu)
-            assert np.array_equal(t[k * su + b * si: k * su + b * si + len(ei)], ei)
+        got = touched_segments(buf.cpu().numpy(), nb)
+        want = _expected_lists(rows, n, B)
+        for b in range(nb):
+            for k in range(6):
+                assert np.array_equal(got[b][k], want[b][k]), f"B={B} batch {b} list {k}"
 
 
 def _ranges(lay):
@@ -78,11 +104,10 @@ def test_lazy_adam_bitwise_equals_dense_over_two_epochs():
     rd = torch.from_numpy(rows).to(dev)
     touched = torch.empty((lib.ncf_touched_bytes(n, B, U, I) + 3) // 4, dtype=torch.int32, device=dev)
     L.check(lib.ncf_batch_touched(rd.data_ptr(), n, B, U, I, touched.data_ptr(), st), "touched")
-    tl = touched.cpu().numpy()
-    su, si = min(U, B), min(I, B)
-    cnt = tl[nb * (su + si):].reshape(nb, 2)
-    users_of = [tl[b * su: b * su + cnt[b, 0]] for b in range(nb)]
-    items_of = [tl[nb * su + b * si: nb * su + b * si + cnt[b, 1]] for b in range(nb)]
+    from ncf_amd.engine import touched_segments
+    lists = touched_segments(touched.cpu().numpy(), nb)
+    users_of = [lists[b][0] for b in range(nb)]
+    items_of = [lists[b][1] for b in range(nb)]
 
     total = int(lay.total)
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -154,6 +179,8 @@ def test_lazy_adam_bitwise_equals_dense_over_two_epochs():
         else:  # the epoch's last batch brought every row up
             for k in ("p", "m", "v"):
                 assert torch.equal(A[k], Bb[k]), f"epoch end {k} step {t}"
+        # rolling catch-up: no row more than SPAN steps behind
+        assert int(last.min()) >= t - SPAN, f"step {t}: a row sat out {t - int(last.min())} steps"
         if t in (7, 41):
             flush_and_compare(f"step {t}")
     flush_and_compare("end")

@@ -29,6 +29,17 @@ def test_library_exports_every_declared_symbol(header, lib):
         assert hasattr(so, n), f"{lib} does not export {n}"
 
 
+def test_integration_stub_abi_matches_header():
+    """INTEGRATION.md's binding asserts the header's ABI version (the GPU
+    integration tests exec that block)."""
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "ncf_hip.h")).read()
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    want = int(re.search(r"#define NCF_ABI_VERSION (\d+)", hdr).group(1))
+    assert int(re.search(r"ncf_abi_version\(\) == (\d+)", doc).group(1)) == want
+
+
 def test_abi_version_and_layout():
     import ncf_amd._lib as L
     import re
