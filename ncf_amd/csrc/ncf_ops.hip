@@ -4,6 +4,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+#include <unordered_map>
+
 #include "ncf_kernels.h"
 #include "ncf_layered.h"
 
@@ -125,27 +128,97 @@ __device__ __forceinline__ void adam_f4(f4& p, f4& m, f4& v, const f4& g, float 
 
 // Step-t scalars in double like torch's Python scalars, by thread 0 of the block:
 // sc[0] = -(lr / (1 - beta1^t)), sc[1] = sqrt(1 - beta2^t) (torch _single_tensor_adam).
-__device__ __forceinline__ void step_scalars(int64_t t_step, double lr, double beta1, double beta2, float* sc) {
+// The two double pows take ~2.5 us on one lane -- longer than the launch's loads --
+// so each optimizer launch also computes step t + 1's pair (one lane of block 0,
+// beside its other work) into a per-control-block cache entry, and step t + 1's
+// launch reads it instead: entry [t & 1] is only written by the launch of step t - 1
+// (a finished kernel), never by the launch that reads it.  The entry holds its
+// inputs (t, lr, beta1, beta2); any mismatch -- first step, a reloaded or
+// teacher-forced state, another optimizer on the same control block -- computes
+// the pair again, so the cached value is always the one pow gives.
+struct ScCache {
+    int64_t t;
+    double lr, beta1, beta2;
+    float sc0, sc1;
+    int64_t pad;
+};
+constexpr int SC_SLOTS = 1024;
+__device__ ScCache g_sc_cache[SC_SLOTS][2];
+
+__device__ __forceinline__ void step_pair(int64_t t_step, double lr, double beta1, double beta2, float* a, float* b) {
+    const double t = (double)t_step;
+    *a = (float)(-(lr / (1.0 - pow(beta1, t))));
+    *b = (float)sqrt(1.0 - pow(beta2, t));
+}
+
+// thread 0: the cache entry of step t, requested (issue early, resolve late)
+__device__ __forceinline__ ScCache sc_peek(const ScCache* cache, int64_t t_step) {
+    ScCache e;
+    e.t = -1;
+    if (threadIdx.x == 0 && cache != nullptr) e = cache[t_step & 1];
+    return e;
+}
+
+__device__ __forceinline__ void sc_resolve(const ScCache& e, int64_t t_step, double lr, double beta1, double beta2,
+                                           float* sc) {
     if (threadIdx.x == 0) {
-        const double t = (double)t_step;
-        sc[0] = (float)(-(lr / (1.0 - pow(beta1, t))));
-        sc[1] = (float)sqrt(1.0 - pow(beta2, t));
+        if (e.t == t_step && e.lr == lr && e.beta1 == beta1 && e.beta2 == beta2) {
+            sc[0] = e.sc0;
+            sc[1] = e.sc1;
+        } else {
+            step_pair(t_step, lr, beta1, beta2, &sc[0], &sc[1]);
+        }
     }
+}
+
+__device__ __forceinline__ void step_scalars(const ScCache* cache, int64_t t_step, double lr, double beta1,
+                                             double beta2, float* sc) {
+    sc_resolve(sc_peek(cache, t_step), t_step, lr, beta1, beta2, sc);
+}
+
+// step t + 1's entry, by lane 0 of wave 1 of block 0 (vector stores)
+__device__ __forceinline__ void step_scalars_ahead(ScCache* cache, int64_t t_step, double lr, double beta1,
+                                                   double beta2) {
+    if (cache == nullptr || blockIdx.x != 0 || threadIdx.x != 64) return;
+    ScCache e;
+    e.t = t_step + 1;
+    e.lr = lr;
+    e.beta1 = beta1;
+    e.beta2 = beta2;
+    e.pad = 0;
+    step_pair(t_step + 1, lr, beta1, beta2, &e.sc0, &e.sc1);
+    cache[(t_step + 1) & 1] = e;
+}
+
+// The step-scalar cache entry pair of a control block (see ScCache): one slot per
+// ctl pointer seen, for the life of the process; null (always recompute) past
+// SC_SLOTS control blocks.
+static ScCache* sc_cache_for(const void* ctl) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, int> slots;
+    static ScCache* base = nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (base == nullptr && hipGetSymbolAddress((void**)&base, HIP_SYMBOL(g_sc_cache)) != hipSuccess) {
+        base = nullptr;
+        return nullptr;
+    }
+    auto it = slots.find(ctl);
+    if (it != slots.end()) return base + 2 * it->second;
+    if ((int)slots.size() >= SC_SLOTS) return nullptr;
+    const int k = (int)slots.size();
+    slots.emplace(ctl, k);
+    return base + 2 * k;
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                                    float* __restrict__ v, Ranges R, const ncf_step_ctl* ctl, double lr,
                                                    double beta1, double beta2, float eps, int64_t loss_slot,
-                                                   float* loss_hist, int64_t hist_len) {
+                                                   float* loss_hist, int64_t hist_len, ScCache* scc) {
 #pragma clang fp contract(off)
     __shared__ float sc[2];
-    if (threadIdx.x == 0) {  // bias corrections once per block, in double like torch's Python scalars
-        const double t = (double)ctl->adam_t;  // advanced by ncf_reduce_slab
-        const double bc1 = 1.0 - pow(beta1, t);
-        const double bc2 = 1.0 - pow(beta2, t);
-        sc[0] = (float)(-(lr / bc1));
-        sc[1] = (float)sqrt(bc2);
-    }
+    const int64_t t_step = ctl->adam_t;  // advanced by ncf_reduce_slab
+    step_scalars(scc, t_step, lr, beta1, beta2, sc);
+    step_scalars_ahead(scc, t_step, lr, beta1, beta2);
     __syncthreads();
     const float neg_step = sc[0], bc2s = sc[1];
     const float w1 = (float)(1.0 - beta1);
@@ -221,8 +294,9 @@ __device__ __forceinline__ void tower_reduce_adam_block(const float* __restrict_
                                                         int64_t t_step, int64_t b_step, double lr, double beta1,
                                                         double beta2, float eps, float* loss_hist, int64_t hist_len,
                                                         const W0Part& wp, float* sc, f4 (*part)[16],
-                                                        const float* __restrict__ pre = nullptr) {
+                                                        const ScCache* scc, const float* __restrict__ pre = nullptr) {
 #pragma clang fp contract(off)
+    const ScCache sce = sc_peek(scc, t_step);  // arrives with the first slab loads
     const float w1 = (float)(1.0 - beta1);
     const float b2 = (float)beta2;
     const float omb2 = (float)(1.0 - beta2);
@@ -256,7 +330,7 @@ __device__ __forceinline__ void tower_reduce_adam_block(const float* __restrict_
         }
     }
     part[rg][c4] = s;
-    step_scalars(t_step, lr, beta1, beta2, sc);
+    sc_resolve(sce, t_step, lr, beta1, beta2, sc);
     __syncthreads();
     const float neg_step = sc[0], bc2s = sc[1];
     if (rg == 0 && j < stride) {
@@ -284,15 +358,17 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
                                                           float* __restrict__ g, float* __restrict__ m,
                                                           float* __restrict__ v, Ranges R, Ranges RE,
                                                           ncf_step_ctl* ctl, double lr, double beta1, double beta2,
-                                                          float eps, float* loss_hist, int64_t hist_len, W0Part wp) {
+                                                          float eps, float* loss_hist, int64_t hist_len, W0Part wp,
+                                                          ScCache* scc) {
 #pragma clang fp contract(off)
     __shared__ float sc[2];
     __shared__ f4 part[16][16];
     const int64_t t_step = ctl->snap_t;
     const int64_t b_step = ctl->snap_batch;
+    step_scalars_ahead(scc, t_step, lr, beta1, beta2);
     if ((int)blockIdx.x < nA) {
         tower_reduce_adam_block(slab, lo, stride, rows, tb, tower_len, p, m, v, R, t_step, b_step, lr, beta1, beta2,
-                                eps, loss_hist, hist_len, wp, sc, part);
+                                eps, loss_hist, hist_len, wp, sc, part, scc);
     } else {
         const float w1 = (float)(1.0 - beta1);
         const float b2 = (float)beta2;
@@ -310,8 +386,9 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restric
             vv = *reinterpret_cast<const f4*>(v + i);
             pp = *reinterpret_cast<const f4*>(p + i);
         };
-        if (q < total) load();  // the first element's loads fly while thread 0 computes
-        step_scalars(t_step, lr, beta1, beta2, sc);
+        const ScCache sce = sc_peek(scc, t_step);
+        if (q < total) load();  // the first element's loads fly while thread 0 resolves the scalars
+        sc_resolve(sce, t_step, lr, beta1, beta2, sc);
         __syncthreads();
         const float neg_step = sc[0], bc2s = sc[1];
         while (q < total) {
@@ -481,24 +558,26 @@ __global__ __launch_bounds__(256) void lazy_adam_kernel(const float* __restrict_
                                                         int nA, int64_t tb, int64_t tower_len, Ranges R,
                                                         ncf_step_ctl* ctl, double lr, double beta1, double beta2,
                                                         float eps, float* loss_hist, int64_t hist_len, W0Part wp,
-                                                        LazyArgs a) {
+                                                        LazyArgs a, ScCache* scc) {
 #pragma clang fp contract(off)
     __shared__ float sc[2];
     __shared__ f4 part[16][16];
     __shared__ float2 win[LZ_WIN];
     const int64_t t_step = ctl->snap_t;
     const int64_t b_step = ctl->snap_batch;
+    step_scalars_ahead(scc, t_step, lr, beta1, beta2);
     if ((int)blockIdx.x < nA) {
         tower_reduce_adam_block(slab, lo, stride, rows, tb, tower_len, a.p, a.m, a.v, R, t_step, b_step, lr, beta1,
-                                beta2, eps, loss_hist, hist_len, wp, sc, part,
+                                beta2, eps, loss_hist, hist_len, wp, sc, part, scc,
                                 a.packed != nullptr ? a.packed + a.pk_tail : nullptr);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             a.ring[2 * (t_step % a.ring_n)] = sc[0];
             a.ring[2 * (t_step % a.ring_n) + 1] = sc[1];
         }
     } else {
+        const ScCache sce = sc_peek(scc, t_step);
         stage_ring(a, t_step, win);
-        step_scalars(t_step, lr, beta1, beta2, sc);
+        sc_resolve(sce, t_step, lr, beta1, beta2, sc);
         __syncthreads();
         const int64_t b = ((b_step % a.nb) + a.nb) % a.nb;
         const int64_t wpb = blockDim.x >> 6;
@@ -1800,7 +1879,8 @@ int ncf_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
     if (grid > 4096) grid = 4096;
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(adam_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
-                       exp_avg_sq, R, ctl, lr, beta1, beta2, (float)eps, loss_slot, loss_hist, hist_len);
+                       exp_avg_sq, R, ctl, lr, beta1, beta2, (float)eps, loss_slot, loss_hist, hist_len,
+                       sc_cache_for(ctl));
     return launch_status();
 }
 
@@ -1841,7 +1921,7 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
     hipLaunchKernelGGL(reduce_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
                        static_cast<const float*>(workspace), lo, stride, rows, nA, lay->tower_begin, lay->tower_len,
                        params, grads, exp_avg, exp_avg_sq, R, RE, ctl, lr, beta1, beta2, (float)eps, loss_hist,
-                       hist_len, w0_part(lay, workspace));
+                       hist_len, w0_part(lay, workspace), sc_cache_for(ctl));
     return launch_status();
 }
 
@@ -1982,7 +2062,8 @@ int ncf_lazy_adam_step(const ncf_layout* lay, const void* workspace, float* para
     const int64_t nB = step_blocks(a, t);
     hipLaunchKernelGGL(lazy_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
                        static_cast<const float*>(workspace), lo, stride, rows, nA, lay->tower_begin, lay->tower_len, R,
-                       ctl, lr, beta1, beta2, (float)eps, loss_hist, hist_len, w0_part(lay, workspace), a);
+                       ctl, lr, beta1, beta2, (float)eps, loss_hist, hist_len, w0_part(lay, workspace), a,
+                       sc_cache_for(ctl));
     return launch_status();
 }
 
@@ -2057,7 +2138,7 @@ int ncf_lazy_adam_step_packed(const ncf_layout* lay, float* params, float* exp_a
     const int64_t nB = step_blocks(a, t);
     hipLaunchKernelGGL(lazy_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
                        (const float*)nullptr, lo, stride, 0, nA, lay->tower_begin, lay->tower_len, R, ctl, lr, beta1,
-                       beta2, (float)eps, loss_hist, hist_len, W0Part{nullptr, 0, 0, 0, 0}, a);
+                       beta2, (float)eps, loss_hist, hist_len, W0Part{nullptr, 0, 0, 0, 0}, a, sc_cache_for(ctl));
     return launch_status();
 }
 

@@ -185,3 +185,38 @@ def test_lazy_adam_bitwise_equals_dense_over_two_epochs():
             flush_and_compare(f"step {t}")
     flush_and_compare("end")
     assert int(last.min()) == int(last.max()) == 2 * nb
+
+
+def test_step_scalar_cache_follows_its_inputs():
+    """The optimizer launches take step t's (-lr/bc1, sqrt(bc2)) from a per-control-
+    block cache that step t - 1's launch filled (ncf_ops.hip ScCache).  Steps out of
+    order, repeated, and with lr / beta changes between them must give bitwise what a
+    fresh control block (no usable entry: the double pows) gives."""
+    import ncf_amd._lib as L
+    lib = L.hip()
+    dev = torch.device("cuda", 0)
+    st = L.stream_ptr(dev)
+    n = 4096
+    g = torch.Generator(device="cpu").manual_seed(5)
+    p0 = torch.randn(n, generator=g).to(dev)
+    grads = [(torch.randn(n, generator=g) * 0.01).to(dev) for _ in range(12)]
+    ranges = (ctypes.c_int64 * 2)(0, n)
+    seq = [(1, 1e-3, 0.999), (2, 1e-3, 0.999), (3, 1e-3, 0.999), (4, 2e-3, 0.999), (5, 2e-3, 0.99),
+           (6, 2e-3, 0.99), (6, 2e-3, 0.99), (3, 2e-3, 0.99), (4, 2e-3, 0.99), (7, 1e-3, 0.999),
+           (8, 1e-3, 0.999), (9, 1e-3, 0.999)]
+    bufs = {k: [p0.clone(), torch.zeros(n, device=dev), torch.zeros(n, device=dev)] for k in ("cached", "fresh")}
+    ctl = torch.zeros(6, dtype=torch.int64, device=dev)
+    fresh = []  # kept alive: every fresh control block a new pointer, so a new cache slot
+    for i, (t, lr, b2) in enumerate(seq):
+        for k in ("cached", "fresh"):
+            if k == "fresh":
+                fresh.append(torch.zeros(6, dtype=torch.int64, device=dev))
+            c = ctl if k == "cached" else fresh[-1]
+            c[1] = t
+            gr = grads[i].clone()
+            p, m, v = bufs[k]
+            L.check(lib.ncf_adam_step(p.data_ptr(), gr.data_ptr(), m.data_ptr(), v.data_ptr(), ranges, 1,
+                                      c.data_ptr(), lr, 0.9, b2, 1e-8, -1, None, 0, st), "adam")
+            torch.cuda.synchronize()
+        for a, b in zip(bufs["cached"], bufs["fresh"]):
+            assert torch.equal(a, b), f"step {i} (t={t}, lr={lr}, beta2={b2})"
