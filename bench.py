@@ -364,16 +364,25 @@ def setup_engine(cfg, ds, train, world, rank, dev, group, global_batch, seed=0):
 
 def run_steps(eng, n_steps, use_graph):
     """n_steps optimizer steps; a new epoch (fresh negatives and permutation)
-    starts at every epoch boundary inside the timed region."""
+    starts at every epoch boundary inside the timed region.  The boundary's host
+    work (the pipeline join, the reference's RNG draws, the stream switch) is done
+    as soon as an epoch's steps are enqueued, while the device still runs them, so
+    the device never waits on it; a timed region of E whole epochs holds E such
+    boundaries (the last one for the epoch after it), the warm-up's last boundary
+    prepared the first.  The draws happen in the reference's order either way."""
     done = 0
     while done < n_steps:
         pos = eng.batches_done % eng.num_batches
-        if pos == 0 and eng.batches_done > 0:
+        if pos == 0 and eng.batches_done > 0 and not getattr(eng, "boundary_ready", False):
             eng.next_epoch()
+        eng.boundary_ready = False
         k = min(n_steps - done, eng.num_batches - pos)
         eng.run(k, use_graph=use_graph)
         eng.batches_done += k
         done += k
+        if eng.batches_done % eng.num_batches == 0:
+            eng.next_epoch()
+            eng.boundary_ready = True
 
 
 def e2e_fit(cfg, ds, dev, epochs):
