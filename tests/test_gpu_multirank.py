@@ -77,12 +77,13 @@ def _free_port():
 @pytest.mark.parametrize("mt,f,nl,use_graph,dp_mode", [("NeuMF-end", 16, 3, True, "zero1"),
                                                        ("NeuMF-end", 16, 3, False, "zero1"),
                                                        ("NeuMF-end", 16, 3, True, "allreduce"),
-                                                       ("NeuMF-end", 16, 3, True, None),  # default: touched
+                                                       ("NeuMF-end", 16, 3, True, None),  # default: auto
                                                        ("NeuMF-end", 16, 3, True, "touched"),
                                                        ("NeuMF-end", 16, 3, False, "touched"),
                                                        ("GMF", 16, 3, True, "touched"),
                                                        ("MLP", 8, 2, True, "touched"),
                                                        ("NeuMF-end", 32, 3, True, "touched"),
+                                                       ("NeuMF-end", 16, 3, True, "auto"),
                                                        ("NeuMF-end", 16, 3, False, "allreduce"),
                                                        ("NeuMF-end", 16, 3, True, "sparse"),
                                                        ("NeuMF-end", 16, 3, False, "sparse"),

@@ -267,3 +267,22 @@ def test_prepare_workspace_small_batches():
     nb = (n + 65535) // 65536
     assert big >= n * 8 + nb * items * 4
     assert L.hip().ncf_prepare_epoch_workspace(20_000_000, 256, 26744) <= 256
+
+
+def test_auto_dp_mode_by_global_batch():
+    """dp_mode "auto" (world > 1 default): the packed touched-row exchange only where
+    it is well under the flat gradient -- C3's 65,536-row batch touches every ml-1m
+    row (all-reduce), C4's ml-20m tables are ~0.56 of it (touched)."""
+    import ncf_amd._lib as L
+    from ncf_amd.engine import TrainEngine, _active_ranges
+    from ncf_amd.models import NCF
+    assert TrainEngine.default_dp_mode(10 ** 6, touched_ok=True) == "auto"
+    assert TrainEngine.default_dp_mode(10 ** 6) == "allreduce"
+    assert TrainEngine.default_dp_mode(10 ** 8) == "zero1"
+    want = {(6041, 3707): "allreduce", (138494, 26745): "touched"}
+    for (U, I), mode in want.items():
+        lay = L.layout(U, I, 16, 3, "NeuMF-end")
+        rng = _active_ranges(NCF(U, I, 16, 3, 0.0, "NeuMF-end"), lay)
+        ranges = (ctypes.c_int64 * (2 * len(rng)))(*[x for r in rng for x in r])
+        got, pf = TrainEngine.auto_dp_mode(lay, ranges, len(rng), 65536)
+        assert got == mode, (U, I, pf, int(lay.total))
