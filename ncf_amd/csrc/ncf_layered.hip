@@ -93,6 +93,22 @@ __device__ __forceinline__ void zero_share(float* p, int64_t n4) {
     for (int64_t i = id; i < n4; i += nt) reinterpret_cast<f4*>(p)[i] = f4{0.f, 0.f, 0.f, 0.f};
 }
 
+// XCD-aware tile order for the 2-D GEMM grids (MI355X dispatches consecutive
+// workgroups round-robin over its 8 XCDs, each with its own L2): the launch's
+// workgroups, in dispatch order, are relabelled so that each group of workgroups
+// sharing an XCD walks a contiguous run of (row tile, column tile) pairs, column tile
+// fastest -- the column tiles of one row tile read the same A rows back to back from
+// one L2 instead of from HBM once per tile.  A bijection (the guide's T1 form for
+// grids not a multiple of 8), so a speed choice only.
+__device__ __forceinline__ void xcd_tile(int& tm, int& tn) {
+    const int64_t nwg = (int64_t)gridDim.x * gridDim.y;
+    const int64_t orig = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const int64_t q = nwg / 8, r = nwg % 8, x = orig % 8;
+    const int64_t w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / 8;
+    tm = (int)(w / gridDim.y);
+    tn = (int)(w % gridDim.y);
+}
+
 __device__ __forceinline__ void row_ids(const LyrArgs& a, const Sel& s, int64_t m, int& u, int& it) {
     if (m < s.nloc) {
         const uint64_t r = a.rows[s.base + m];
@@ -251,8 +267,10 @@ __global__ __launch_bounds__(GNT) void lyr_fwd_kernel(LyrArgs a, int k, const fl
     const ncf_layout& lay = a.lay;
     const int DM = lay.factor_num << (lay.num_layers - 1);
     const int K = (2 * DM) >> k, N = K / 2;
-    const int64_t m0 = (int64_t)blockIdx.x * GBM;
-    const int n0 = blockIdx.y * GBN;
+    int tm, tn;
+    xcd_tile(tm, tn);
+    const int64_t m0 = (int64_t)tm * GBM;
+    const int n0 = tn * GBN;
     const float* prm = a.params;
     const float* W = prm + lay.w[k];
     const float* bias = prm + lay.b[k];
@@ -336,8 +354,10 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, con
     const ncf_layout& lay = a.lay;
     const int DM = lay.factor_num << (lay.num_layers - 1);
     const int N = (2 * DM) >> k, J = N / 2;  // this layer: in = N, out = J
-    const int64_t m0 = (int64_t)blockIdx.x * GBM;
-    const int n0 = blockIdx.y * GBN;
+    int tm, tn;
+    xcd_tile(tm, tn);
+    const int64_t m0 = (int64_t)tm * GBM;
+    const int n0 = tn * GBN;
     const float* W = a.params + lay.w[k];
     if (FIRST && threadIdx.x < GBM) {
         int u, it;
@@ -557,7 +577,14 @@ __device__ __forceinline__ void bwd_w_body(const LyrArgs& a, int k, const float*
 template <bool FIRST, bool DROP, bool VEC>
 __global__ __launch_bounds__(GNT) void lyr_bwd_w_kernel(LyrArgs a, int k, const float* __restrict__ D,
                                                         const float* __restrict__ Ain, int64_t R, int64_t chunk) {
-    bwd_w_body<FIRST, DROP, VEC>(a, k, D, Ain, R, chunk, blockIdx.x, blockIdx.y, blockIdx.z);
+    // XCD-aware order (xcd_tile): the (j, column) tiles of one row chunk share an XCD,
+    // so its D and A rows are read from one L2
+    const int64_t per = (int64_t)gridDim.x * gridDim.y, nwg = per * gridDim.z;
+    const int64_t orig = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const int64_t q = nwg / 8, r = nwg % 8, x = orig % 8;
+    const int64_t w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / 8;
+    const int bz = (int)(w / per), rem = (int)(w % per);
+    bwd_w_body<FIRST, DROP, VEC>(a, k, D, Ain, R, chunk, rem % gridDim.x, rem / gridDim.x, bz);
 }
 
 // The weight gradients of several layers k >= 1 in one launch (the step chain leaves
