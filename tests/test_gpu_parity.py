@@ -39,6 +39,23 @@ def _models(mt, f, L, U=50, I=80, seed=1, dropout=0.0):
     return ref, m.to(DEV)
 
 
+def _close_grad_rows(got, exp, name, terms, max_rows):
+    """_close_grad for an embedding table at large batches, except for at most
+    `max_rows` rows: a row whose layer pre-activation sits within fp32 rounding of 0
+    takes the other side of a ReLU in one of the two computations (as the fp32 oracle
+    itself does against a float64 one -- scripts/diag_fact_rows.py at NCF(64,4),
+    65,536 rows: 3 user rows off on each side, disjoint), so its whole gradient row
+    differs by that row's contribution -- in a weight gradient, the flipped unit's
+    output row."""
+    scale = max(float(np.abs(exp).max()), 1e-30)
+    atol = (1e-6 if terms is None else max(1e-6, 2e-8 * float(np.sqrt(terms)))) * scale
+    bad = np.abs(got - exp) > atol + 1e-4 * np.abs(exp)
+    rows = np.unique(np.nonzero(bad.reshape(got.shape[0], -1))[0])
+    assert len(rows) <= max_rows, f"{name}: {len(rows)} rows beyond tolerance"
+    keep = np.setdiff1d(np.arange(got.shape[0]), rows)
+    _close_grad(got[keep], exp[keep], name, terms=terms)
+
+
 def _close_grad(got, exp, name, terms=None):
     """rtol 1e-4, atol 1e-6 of the largest gradient -- or, for embedding tables whose
     rows sum `terms` per-row contributions in float-atomic (arrival) order, an atol
@@ -180,7 +197,15 @@ def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3, flags=0, order=False):
                 # factored layer 0: dW0 = sum_u G_u^T Um[u] (+ items), G_u summed by float
                 # atomics in arrival order -- the embedding tables' rounding model
                 hot = max(int(np.bincount(items).max()), int(np.bincount(users).max()))
-                _close_grad(got, grads_ref[name].numpy(), name, terms=hot)
+                if B >= 65536:
+                    _close_grad_rows(got, grads_ref[name].numpy(), name, hot, max_rows=8)
+                else:
+                    _close_grad(got, grads_ref[name].numpy(), name, terms=hot)
+                continue
+            if B >= 65536:  # a bias: its flipped units' entries
+                e = grads_ref[name].numpy()
+                _close_grad_rows(got.reshape(len(got), -1), e.reshape(len(e), -1), name,
+                                 hot if "embed" in name else None, max_rows=8)
                 continue
             _close_grad(got, grads_ref[name].numpy(), name, terms=hot if "embed" in name else None)
         else:  # unused in this model type (reference grad None): nothing may be written
@@ -222,7 +247,9 @@ def test_one_step_fact_boundary(U, I, fact):
                                         ("NeuMF-end", 4, 3, 8192), ("MLP", 4, 2, 8192),
                                         ("NeuMF-end", 128, 1, 8192),
                                         # dm 512 / 256: expansion by GEMMs (lyr_fact_dx / dw0), W0 via the slab
-                                        ("NeuMF-end", 64, 4, 8192), ("MLP", 32, 4, 8192)])
+                                        ("NeuMF-end", 64, 4, 8192), ("MLP", 32, 4, 8192),
+                                        # 128-row block tiles of the per-layer GEMMs (R >= 65,536)
+                                        ("NeuMF-end", 64, 4, 65536)])
 def test_one_step_layered_factored_layer0(mt, f, Lyr, B):
     """Layered path with the factored layer 0 (ABI 10: table projections through W0,
     per-row gather, D0 row sums expanded by fact_expand_kernel; dm = 128 for
