@@ -480,6 +480,20 @@ def _barrier(group, dev):
             dist.barrier(group=group)
 
 
+def snapshot_state(eng):
+    """Copies of the engine's trained state (parameters, Adam moments, control block,
+    loss history, deferred-Adam row steps)."""
+    names = ("flat", "exp_avg", "exp_avg_sq", "ctl", "loss_hist", "_last")
+    return {k: getattr(eng, k).clone() for k in names if getattr(eng, k, None) is not None}
+
+
+def restore_state(eng, snap):
+    """Back to snapshot_state's copies, in place (captured graphs keep their pointers)."""
+    for k, v in snap.items():
+        getattr(eng, k).copy_(v)
+    torch.cuda.synchronize(eng.device)
+
+
 def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup, use_graph, whole_epochs=True):
     """Warm-up, then whole fresh epochs timed (>= `steps` optimizer steps, rounded up
     to whole epochs of `global_batch`-row global batches: every epoch in the timed
@@ -508,6 +522,9 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
     fresh = pipe.stats["epochs"] - e0
     losses = eng.epoch_losses()
     final_loss = float(losses[(eng.state_step() - 1) % nb])
+    # the trained state as the timed epochs left it: the quality figures are taken from
+    # it, after the frozen run and the kernel timings below (restore_state)
+    snap = snapshot_state(eng)
     # the same steps on the current epoch stream, reused (the step kernel wraps to the
     # epoch's first batch): the device + exchange rate beside `value`
     _barrier(group, dev)
@@ -526,7 +543,7 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
     if bm:
         host["boundary_join"] = float(np.mean([x[0] for x in bm]))
         host["boundary_rest"] = float(np.mean([x[1] for x in bm]))
-    return {"eng": eng, "model": model, "pipe": pipe, "value": epochs * n_rows / dt, "dt": dt, "steps": k,
+    return {"eng": eng, "model": model, "pipe": pipe, "snap": snap, "value": epochs * n_rows / dt, "dt": dt, "steps": k,
             "epochs": epochs, "fresh_epochs": fresh, "rows_per_epoch": n_rows, "batches_per_epoch": nb,
             "final_loss": final_loss, "frozen_value": k * n_rows / nb / dtf, "frozen_ms_per_step": dtf / k * 1e3,
             "epoch_host_ms": host}
@@ -702,6 +719,7 @@ def main():
 
     # ---- quality: HR@10 / NDCG@10 on the leave-one-out test set ---------------
     hr10 = ndcg10 = None
+    restore_state(eng, m["snap"])  # quality of the state the timed epochs trained, nothing after
     if not args.skip_eval and rank == 0:
         from ncf_amd.metrics import evaluate_arrays
         tu = np.repeat(ds["test_users"], 100)
