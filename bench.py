@@ -362,14 +362,30 @@ def setup_engine(cfg, ds, train, world, rank, dev, group, global_batch, seed=0):
     return eng, model, pipe
 
 
+# Where the boundary's host work goes (NCF_BENCH_BOUNDARY=early|top|auto, default auto):
+# early for epochs of at most EARLY_MAX_STEPS steps, else at the top of the next epoch.
+# Measured on the box (profiles/r03_evidence/ab_boundary.json, same session A/B):
+# C3 (76 steps per epoch) 57-62 us/step early against 71-75 top -- the host is not
+# ahead of a 4.5 ms epoch at its start; C2 (4,855) 24.2-25.0 early against 22.3 top,
+# C5 (19,418) 14.7 against 14.0 -- a host running whole long epochs ahead slows the
+# small steps (the frozen rate is the same in both).
+BOUNDARY = os.environ.get("NCF_BENCH_BOUNDARY", "auto")
+EARLY_MAX_STEPS = 1024
+
+
+def _early_boundary(eng):
+    return BOUNDARY == "early" or (BOUNDARY == "auto" and eng.num_batches <= EARLY_MAX_STEPS)
+
+
 def run_steps(eng, n_steps, use_graph):
     """n_steps optimizer steps; a new epoch (fresh negatives and permutation)
     starts at every epoch boundary inside the timed region.  The boundary's host
     work (the pipeline join, the reference's RNG draws, the stream switch) is done
-    as soon as an epoch's steps are enqueued, while the device still runs them, so
-    the device never waits on it; a timed region of E whole epochs holds E such
+    as soon as an epoch's steps are enqueued, while the device still runs them, for
+    short epochs (_early_boundary); a timed region of E whole epochs holds E such
     boundaries (the last one for the epoch after it), the warm-up's last boundary
-    prepared the first.  The draws happen in the reference's order either way."""
+    prepared the first.  Long epochs take it at the top of the next epoch.  The
+    draws happen in the reference's order either way."""
     done = 0
     while done < n_steps:
         pos = eng.batches_done % eng.num_batches
@@ -380,7 +396,7 @@ def run_steps(eng, n_steps, use_graph):
         eng.run(k, use_graph=use_graph)
         eng.batches_done += k
         done += k
-        if eng.batches_done % eng.num_batches == 0:
+        if eng.batches_done % eng.num_batches == 0 and _early_boundary(eng):
             eng.next_epoch()
             eng.boundary_ready = True
 
