@@ -107,10 +107,11 @@ class HostSampler:
 
 
 def sampler_threads():
-    """Threads of a host sampler pool: NCF_SAMPLER_THREADS, else min(8, half the CPUs
+    """Threads of a host sampler pool: NCF_SAMPLER_THREADS, else min(12, half the CPUs
     this process may run on) -- a GPU box grants 16 CPUs per GPU, and the rest are
     the training loop's (graph replays, the epoch pipeline's staging, the HIP runtime):
-    the pool only has to finish an epoch's draws while the previous epoch trains."""
+    the pool only has to finish an epoch's draws while the previous epoch trains
+    (ml-20m on the box: 42 ms per epoch at 8 threads, 27 ms at 12)."""
     import os
     v = os.environ.get("NCF_SAMPLER_THREADS")
     if v:
@@ -119,7 +120,7 @@ def sampler_threads():
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(8, n // 2))
+    return max(1, min(12, n // 2))
 
 
 def _membership_from(train_mat, features):
