@@ -253,6 +253,268 @@ __device__ __forceinline__ void gemm_block_v(int64_t kbeg, int64_t kend, GA ga4,
     ep(acc, wm, wn, l);
 }
 
+// ---------------------------------------------------------------------------
+// fp32 GEMM on the bf16 matrix cores (three-plane split, six products).
+//
+// gfx950 runs v_mfma_f32_16x16x4_f32 at 1/16 of the bf16 rate and has no xf32.
+// Every fp32 operand element is split exactly into three bf16 planes by
+// truncation, x = h + m + l (h the top 8 significant bits, m the next 8, l the
+// last 8; each remainder is exact in fp32, so is the sum), and
+//   x * y ~= h h' + (h m' + m h') + (h l' + m m' + l h')
+// drops only m l', l m', l l' (each <= 2^-24 |x y|) -- about one fp32 rounding
+// per product, accumulated in fp32 by v_mfma_f32_16x16x32_bf16 (exact bf16 x bf16
+// products).  Per K = 32: 6 bf16 MFMAs of 16 cycles against 8 f32 MFMAs of 32.
+//
+// Same contract as gemm_block_v (64 x 64 block tile, 4 waves of 32 x 32, the same
+// loaders, store hook and accumulator layout -- C/D of the bf16 16x16x32 MFMA is
+// the f32 16x16x4 map), K in steps of 32 through double-buffered LDS.  The LDS
+// holds operands fragment-major: per 16-row (column) tile and plane, lane l's
+// 16 bytes (8 bf16 along k) at l * 16, so each MFMA operand is one conflict-free
+// ds_read_b128.  Loaders:
+//   KC operand   thread t: row (t & 15) + 16 (t >> 6), k 8 ((t >> 4) & 3) .. + 7
+//                (two f4 loads) -> one 16-byte fragment slot per plane
+//   M/N-contig.  thread t: columns 4 (t & 15) .. + 3 at k 2 (t >> 4) and + 1 (two
+//                f4 loads; the store hook sees the same columns per thread as
+//                gemm_block_v) -> k pairs packed, one dword per column and plane
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int XBK = 32;
+
+__device__ __forceinline__ uint32_t fbits(float x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
+// (x0, x1) -> three packed bf16 pairs (x0 in the low half): h, m, l with x = h + m + l
+__device__ __forceinline__ void split3(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
+    const uint32_t u0 = fbits(x0), u1 = fbits(x1);
+    h = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+    const float r0 = x0 - bitsf(u0 & 0xffff0000u), r1 = x1 - bitsf(u1 & 0xffff0000u);
+    const uint32_t v0 = fbits(r0), v1 = fbits(r1);
+    m = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
+    const float s0 = r0 - bitsf(v0 & 0xffff0000u), s1 = r1 - bitsf(v1 & 0xffff0000u);
+    l = __builtin_amdgcn_perm(fbits(s1), fbits(s0), 0x07060302u);
+}
+
+// LDS image of one operand and buffer: [tile 0..3][plane 0..2][lane 0..63] x 16 B
+struct X6Img {
+    uint4 f[4][3][64];
+};
+
+template <bool KC, class G>
+__device__ __forceinline__ void x6_load(G g, int64_t k0, int t, f4& r0, f4& r1) {
+    if constexpr (KC) {
+        const int mn = (t & 15) + 16 * (t >> 6), k = 8 * ((t >> 4) & 3);
+        r0 = g(mn, k0 + k);
+        r1 = g(mn, k0 + k + 4);
+    } else {
+        const int mn = 4 * (t & 15), k = 2 * (t >> 4);
+        r0 = g(mn, k0 + k);
+        r1 = g(mn, k0 + k + 1);
+    }
+}
+// B-operand loaders take (k, mn): adapt to the (mn, k) form above
+template <class G>
+struct X6Swap {
+    G g;
+    __device__ __forceinline__ f4 operator()(int mn, int64_t k) const { return g(k, mn); }
+};
+
+template <bool KC>
+__device__ __forceinline__ void x6_store(X6Img& img, int t, const f4& r0, const f4& r1) {
+    if constexpr (KC) {
+        const int mn = (t & 15) + 16 * (t >> 6), kq = (t >> 4) & 3;
+        uint4 h, m, l;
+        split3(r0.x, r0.y, h.x, m.x, l.x);
+        split3(r0.z, r0.w, h.y, m.y, l.y);
+        split3(r1.x, r1.y, h.z, m.z, l.z);
+        split3(r1.z, r1.w, h.w, m.w, l.w);
+        const int tile = mn >> 4, lane = (mn & 15) + 16 * kq;
+        img.f[tile][0][lane] = h;
+        img.f[tile][1][lane] = m;
+        img.f[tile][2][lane] = l;
+    } else {
+        const int n4 = t & 15, kp = t >> 4;  // k = 2 kp, 2 kp + 1 of this K step
+        const int kg = kp >> 2, dw = kp & 3;  // fragment lane group, dword within the 16 bytes
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int mn = 4 * n4 + i;
+            uint32_t h, m, l;
+            split3(lane_get(r0, i), lane_get(r1, i), h, m, l);
+            constexpr int PLANE = 64 * 4;  // dwords per plane image
+            uint32_t* base = reinterpret_cast<uint32_t*>(&img.f[mn >> 4][0][(mn & 15) + 16 * kg]) + dw;
+            base[0] = h;
+            base[PLANE] = m;
+            base[2 * PLANE] = l;
+        }
+    }
+}
+
+template <bool AKC, bool BKC, class GA, class GB, class EP, class SA = NoHook>
+__device__ __forceinline__ void gemm_block_x6(int64_t kbeg, int64_t kend, GA ga4, GB gb4, EP ep, SA sa = SA{}) {
+    __shared__ X6Img Ai[2], Bi[2];
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+    const X6Swap<GB> gbs{gb4};
+    f4 a0, a1, b0, b1;
+    auto load = [&](int64_t k0) {
+        x6_load<AKC>(ga4, k0, t, a0, a1);
+        x6_load<BKC>(gbs, k0, t, b0, b1);
+    };
+    auto store = [&](int buf) {
+        sa(a0);
+        sa(a1);
+        x6_store<AKC>(Ai[buf], t, a0, a1);
+        x6_store<BKC>(Bi[buf], t, b0, b1);
+    };
+    f4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    load(kbeg);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t k0 = kbeg; k0 < kend; k0 += XBK) {
+        const bool more = k0 + XBK < kend;
+        if (more) load(k0 + XBK);
+        bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                fa[i][p] = __builtin_bit_cast(bf16x8, Ai[buf].f[wm / 16 + i][p][l]);
+                fb[i][p] = __builtin_bit_cast(bf16x8, Bi[buf].f[wn / 16 + i][p][l]);
+            }
+        // smallest terms first: (l h', m m', h l'), (m h', h m'), h h'
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f4 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+            }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    ep(acc, wm, wn, l);
+}
+
+// Split in registers instead: the LDS holds the fp32 tiles ([mn][k], 32 k per row,
+// 4-float chunks XOR-swizzled by (r ^ r >> 3) & 7: conflict-free ds_read_b128 operand
+// reads and 16-byte stores, 2-way dword stores), 32 KB per block; each wave reads its
+// fragments (two ds_read_b128 per 16-row tile) and splits them before its MFMAs.
+__device__ __forceinline__ int x6s_addr(int r, int k) { return r * XBK + 4 * ((k >> 2) ^ ((r ^ (r >> 3)) & 7)) + (k & 3); }
+
+template <bool KC, class G>
+__device__ __forceinline__ void x6s_load(G g, int64_t k0, int t, f4 (&v)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int q = t + 256 * h;
+        v[h] = KC ? g(q >> 3, k0 + 4 * (q & 7)) : g(4 * (q & 15), k0 + (q >> 4));
+    }
+}
+template <bool KC>
+__device__ __forceinline__ void x6s_store(float* S, int t, const f4 (&v)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int q = t + 256 * h;
+        if constexpr (KC) {
+            *reinterpret_cast<f4*>(S + x6s_addr(q >> 3, 4 * (q & 7))) = v[h];
+        } else {
+            const int k = q >> 4, mn = 4 * (q & 15);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) S[x6s_addr(mn + i, k)] = lane_get(v[h], i);
+        }
+    }
+}
+// lane l's 8 k of row r (k 8 (l >> 4) .. + 7) -> the three bf16 planes of its fragment
+__device__ __forceinline__ void x6s_frag(const float* S, int r, int l, bf16x8 (&f)[3]) {
+    const int k = 8 * (l >> 4);
+    const f4 x = *reinterpret_cast<const f4*>(S + x6s_addr(r, k));
+    const f4 y = *reinterpret_cast<const f4*>(S + x6s_addr(r, k + 4));
+    uint4 h, m, lo;
+    split3(x.x, x.y, h.x, m.x, lo.x);
+    split3(x.z, x.w, h.y, m.y, lo.y);
+    split3(y.x, y.y, h.z, m.z, lo.z);
+    split3(y.z, y.w, h.w, m.w, lo.w);
+    f[0] = __builtin_bit_cast(bf16x8, h);
+    f[1] = __builtin_bit_cast(bf16x8, m);
+    f[2] = __builtin_bit_cast(bf16x8, lo);
+}
+
+template <bool AKC, bool BKC, class GA, class GB, class EP, class SA = NoHook>
+__device__ __forceinline__ void gemm_block_x6s(int64_t kbeg, int64_t kend, GA ga4, GB gb4, EP ep, SA sa = SA{}) {
+    __shared__ __attribute__((aligned(16))) float As[2][64 * XBK];
+    __shared__ __attribute__((aligned(16))) float Bs[2][64 * XBK];
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+    const X6Swap<GB> gbs{gb4};
+    f4 ra[2], rb[2];
+    auto load = [&](int64_t k0) {
+        x6s_load<AKC>(ga4, k0, t, ra);
+        x6s_load<BKC>(gbs, k0, t, rb);
+    };
+    auto store = [&](int buf) {
+        sa(ra[0]);
+        sa(ra[1]);
+        x6s_store<AKC>(As[buf], t, ra);
+        x6s_store<BKC>(Bs[buf], t, rb);
+    };
+    f4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    load(kbeg);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t k0 = kbeg; k0 < kend; k0 += XBK) {
+        const bool more = k0 + XBK < kend;
+        if (more) load(k0 + XBK);
+        bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            x6s_frag(As[buf], wm + 16 * i + (l & 15), l, fa[i]);
+            x6s_frag(Bs[buf], wn + 16 * i + (l & 15), l, fb[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f4 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+            }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    ep(acc, wm, wn, l);
+}
+
+// The GEMM core of the layered kernels' 16-byte loader path: the bf16 split core
+// (split in registers), or the A/B library variants -DNCF_GEMM_F32 (the f32-MFMA
+// core) and -DNCF_GEMM_X6P (split once per block into bf16 plane images).
+template <bool AKC, bool BKC, class GA, class GB, class EP, class SA = NoHook>
+__device__ __forceinline__ void gemm_block_vx(int64_t kbeg, int64_t kend, GA ga4, GB gb4, EP ep, SA sa = SA{}) {
+#if defined(NCF_GEMM_F32)
+    gemm_block_v<AKC, BKC>(kbeg, kend, ga4, gb4, ep, sa);
+#elif defined(NCF_GEMM_X6P)
+    gemm_block_x6<AKC, BKC>(kbeg, kend, ga4, gb4, ep, sa);
+#else
+    gemm_block_x6s<AKC, BKC>(kbeg, kend, ga4, gb4, ep, sa);
+#endif
+}
+
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 __device__ __forceinline__ f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
 
@@ -334,7 +596,7 @@ __global__ __launch_bounds__(GNT) void lyr_fwd_kernel(LyrArgs a, int k, const fl
             const int nn = n0 + n;
             return (nn < N && c < K) ? ld4(W + (int64_t)nn * K + c) : zero4();
         };
-        gemm_block_v<true, true>(0, K, ga4, gb4, ep);
+        gemm_block_vx<true, true>(0, K, ga4, gb4, ep);
     } else {
         gemm_block<true, true>(m0, n0, 0, K, ga, gb, ep);
     }
@@ -410,6 +672,9 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, con
             const int nn = n0 + n;
             return (j < J && nn < N) ? ld4(W + j * N + nn) : zero4();
         };
+        // K = J <= 256 here (2-8 K steps of 32): the masked epilogue dominates and the
+        // f32 core's occupancy (8 waves / SIMD against 3) wins -- stress 88.8 against
+        // 95.4 us per launch with the split core (profiles/r03x6_*)
         gemm_block_v<true, false>(0, J, ga4, gb4, ep);
     } else {
         gemm_block<true, false>(m0, n0, 0, J, ga, gb, ep);
@@ -519,7 +784,7 @@ __device__ __forceinline__ void bwd_w_body(const LyrArgs& a, int k, const float*
                     }
                     return v;
                 };
-                gemm_block_v<false, false>(q0, q1, ga4, gb4, ep, sa4);
+                gemm_block_vx<false, false>(q0, q1, ga4, gb4, ep, sa4);
             } else {
                 gemm_block<false, false>(j0, c0, q0, q1, ga2, gb, ep, sa1);
             }
@@ -547,7 +812,7 @@ __device__ __forceinline__ void bwd_w_body(const LyrArgs& a, int k, const float*
                 }
                 return v;
             };
-            gemm_block_v<false, false>(r0, r1, ga4, gb4, ep, sa4);
+            gemm_block_vx<false, false>(r0, r1, ga4, gb4, ep, sa4);
         } else {
             gemm_block<false, false>(j0, c0, r0, r1, ga, gb, ep, sa1);
         }
@@ -663,7 +928,7 @@ __global__ __launch_bounds__(GNT) void lyr_proj_kernel(ncf_layout lay, const flo
         const int nn = n0 + n;
         return (nn < DM && c < DM) ? ld4(W + (int64_t)nn * 2 * DM + c) : zero4();
     };
-    gemm_block_v<true, true>(0, DM, ga4, gb4, ep);  // factored path: dm in {8, ..., 128}
+    gemm_block_vx<true, true>(0, DM, ga4, gb4, ep);  // factored path: dm in {8, ..., 128}
 }
 
 // H_1[m][n] = ReLU(P[u_m][n] + P[U + i_m][n] + b_0[n]), four outputs per thread
@@ -710,7 +975,7 @@ __global__ __launch_bounds__(GNT) void lyr_fact_dx_kernel(ncf_layout lay, const 
         const int nn = n0 + n;
         return (k < DM && nn < DM) ? ld4(W + k * 2 * DM + nn) : zero4();
     };
-    gemm_block_v<true, false>(0, DM, ga4, gb4, ep);
+    gemm_block_vx<true, false>(0, DM, ga4, gb4, ep);
 }
 
 __global__ __launch_bounds__(GNT) void lyr_fact_dw0_kernel(LyrArgs a, int zu, int64_t chunk) {
@@ -749,7 +1014,7 @@ __global__ __launch_bounds__(GNT) void lyr_fact_dw0_kernel(LyrArgs a, int zu, in
         const int c = c0 + cr;
         return (m < r1 && c < DM) ? ld4(X + m * DM + c) : zero4();
     };
-    gemm_block_v<false, false>(r0, r1, ga4, gb4, ep);
+    gemm_block_vx<false, false>(r0, r1, ga4, gb4, ep);
 }
 
 __global__ __launch_bounds__(GNT) void lyr_fwd0_fact_kernel(LyrArgs a, const float* __restrict__ P,
