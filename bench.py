@@ -659,13 +659,21 @@ def main():
         return harness_main(args, world, rank)
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    dev = torch.device("cuda", local)
+    # rehearsal of the N > 1 flow on a one-GPU box (not a measurement): every rank on
+    # cuda:0 (NCF_BENCH_SAME_DEVICE=1) over gloo (NCF_BENCH_BACKEND=gloo; RCCL refuses
+    # two ranks on one device)
+    rehearsal = os.environ.get("NCF_BENCH_SAME_DEVICE") == "1"
+    dev = torch.device("cuda", 0 if rehearsal else local)
     torch.cuda.set_device(dev)
     group = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("NCF_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
         group = dist.group.WORLD
 
     shape, f, nl, global_batch = CONFIGS[args.config]
@@ -719,7 +727,9 @@ def main():
         busy, busy_src = newest_profile(args.config, names) if world == 1 else (None, None)
     else:
         names, traffic, traffic_src, busy, busy_src = [], None, None, None, None
-        kname = "layered path: all kernels of ncf_train_step (fwd/predict/bwd GEMMs)"
+        kname = ("layered path: all kernels of ncf_train_step (fwd/predict/bwd GEMMs); the fp32 GEMMs with "
+                 "16-byte loads run as exact three-plane bf16 splits on v_mfma_f32_16x16x32_bf16 (six bf16 "
+                 "products per fp32 product; peak kept at the fp32 MFMA figure)")
 
     # ---- weak scaling (extra field): global batch x N, per-GPU batch fixed -----
     weak = None
@@ -808,6 +818,9 @@ def main():
             "cpu_baseline": cpu,
             "setup_s": {"data": round(t_data, 2)},
         }
+        if rehearsal:
+            out["rehearsal"] = (f"{world} ranks on one device over {os.environ.get('NCF_BENCH_BACKEND', 'nccl')}: "
+                                "a check of the N > 1 flow, not a measurement")
         print(json.dumps(out), flush=True)
     if world > 1:
         _barrier(group, dev)
