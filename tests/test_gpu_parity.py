@@ -461,6 +461,34 @@ def test_hr_ndcg_vs_golden(golden, bs, k):
     np.testing.assert_allclose(nd.cpu().numpy(), g[f"bs{bs}_k{k}_NDCG"], rtol=1e-6)
 
 
+def test_metrics_unequal_and_large_loader_batches():
+    """metrics() on loaders the ranking kernel does not take -- a batch_sampler of
+    unequal batches, and 2,000-row batches -- equals the reference's per-batch loop
+    (metrics.py:4-25) run on the same model's per-batch forward."""
+    from ncf_amd.metrics import _metrics_cpu, metrics
+    from ncf_amd.models import NCF
+    torch.manual_seed(5)
+    gpu = NCF(300, 500, 8, 2, 0.0, "NeuMF-end").to(DEV)
+
+    class PerBatch(torch.nn.Module):  # the reference loop's model(user, item), on the device
+        def forward(self, u, i):
+            return gpu(u.to(DEV), i.to(DEV)).cpu()
+    cpu = PerBatch()
+    rng = np.random.default_rng(2)
+    n = 6000
+    ds = torch.utils.data.TensorDataset(torch.as_tensor(rng.integers(0, 300, n)), torch.as_tensor(rng.integers(0, 500, n)),
+                                        torch.zeros(n, dtype=torch.int64))
+    cuts = np.cumsum([0] + [int(x) for x in rng.integers(20, 140, 200)])
+    cuts = cuts[cuts < n].tolist() + [n]
+    ragged = [list(range(a, b)) for a, b in zip(cuts, cuts[1:])]
+    for loader in (torch.utils.data.DataLoader(ds, batch_sampler=ragged),
+                   torch.utils.data.DataLoader(ds, batch_size=2000, shuffle=False)):
+        hr, nd = metrics(gpu, loader, 10)
+        hr_ref, nd_ref = _metrics_cpu(cpu, loader, 10)
+        assert hr == hr_ref
+        np.testing.assert_allclose(nd, nd_ref, rtol=1e-12)
+
+
 def test_hr_ndcg_short_batch_raises(golden):
     import ncf_amd._lib as L
     g = golden("G6_metrics")

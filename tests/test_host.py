@@ -286,3 +286,19 @@ def test_auto_dp_mode_by_global_batch():
         ranges = (ctypes.c_int64 * (2 * len(rng)))(*[x for r in rng for x in r])
         got, pf = TrainEngine.auto_dp_mode(lay, ranges, len(rng), 65536)
         assert got == mode, (U, I, pf, int(lay.total))
+
+
+@pytest.mark.parametrize("bs,k", [(100, 10), (100, 1), (100, 5), (25, 10)])
+def test_hr_ndcg_topk_ranking_matches_golden(golden, bs, k):
+    """The per-batch torch.topk ranking metrics() uses for loaders ncf_hr_ndcg does not
+    take (batches above 1024 rows, unequal batches) against the reference's own
+    metrics() output (G6), on CPU tensors."""
+    from ncf_amd.metrics import _hr_ndcg_topk
+    g = golden("G6_metrics")
+    logits = torch.as_tensor(g["logits"])
+    items = torch.as_tensor(g["test_pairs"][:, 1], dtype=torch.int32)
+    n = items.numel()
+    nb = (n + bs - 1) // bs
+    hr, nd = _hr_ndcg_topk(logits, items, [bs] * (nb - 1) + [n - (nb - 1) * bs], k)
+    assert hr.tolist() == g[f"bs{bs}_k{k}_HR"].tolist()
+    np.testing.assert_allclose(nd.numpy(), g[f"bs{bs}_k{k}_NDCG"], rtol=0, atol=0)
