@@ -258,57 +258,39 @@ __device__ __forceinline__ void gemm_block_v(int64_t kbeg, int64_t kend, GA ga4,
 //
 // gfx950 runs v_mfma_f32_16x16x4_f32 at 1/16 of the bf16 rate and has no xf32.
 // Every fp32 operand element is split exactly into three bf16 planes by
-// truncation, x = h + m + l (h the top 8 significant bits, m the next 8, l the
-// last 8; each remainder is exact in fp32, so is the sum), and
+// round-to-nearest, x = h + m + l (h = bf16(x), m = bf16(x - h), l = x - h - m; each
+// remainder is exact in fp32 and the last fits bf16, so the sum is exact), and
 //   x * y ~= h h' + (h m' + m h') + (h l' + m m' + l h')
-// drops only m l', l m', l l' (each <= 2^-24 |x y|) -- about one fp32 rounding
-// per product, accumulated in fp32 by v_mfma_f32_16x16x32_bf16 (exact bf16 x bf16
-// products).  Per K = 32: 6 bf16 MFMAs of 16 cycles against 8 f32 MFMAs of 32.
+// drops only m l', l m', l l': |m| <= 2^-8 |x|, |l| <= 2^-16 |x|, so each is
+// <= 2^-24 |x y| and, the residuals being signed, unbiased -- about one fp32
+// rounding per product (a truncating split leaves 8x larger, same-sign terms:
+// max 4.7e-7 against 5.9e-8 relative over 2M random pairs).
+// Accumulated in fp32 by v_mfma_f32_16x16x32_bf16 (exact bf16 x bf16 products).
+// Per K = 32: 6 bf16 MFMAs of 16 cycles against 8 f32 MFMAs of 32.
 //
-// Same contract as gemm_block_v (64 x 64 block tile, 4 waves of 32 x 32, the same
-// loaders, store hook and accumulator layout -- C/D of the bf16 16x16x32 MFMA is
-// the f32 16x16x4 map), K in steps of 32 through double-buffered LDS.  The LDS
-// holds operands fragment-major: per 16-row (column) tile and plane, lane l's
-// 16 bytes (8 bf16 along k) at l * 16, so each MFMA operand is one conflict-free
-// ds_read_b128.  Loaders:
-//   KC operand   thread t: row (t & 15) + 16 (t >> 6), k 8 ((t >> 4) & 3) .. + 7
-//                (two f4 loads) -> one 16-byte fragment slot per plane
-//   M/N-contig.  thread t: columns 4 (t & 15) .. + 3 at k 2 (t >> 4) and + 1 (two
-//                f4 loads; the store hook sees the same columns per thread as
-//                gemm_block_v) -> k pairs packed, one dword per column and plane
+// gemm_block_x6s keeps gemm_block_v's contract (64 x 64 block tile, 4 waves of 32 x 32,
+// the same loaders, store hook and accumulator layout -- C/D of the bf16 16x16x32
+// MFMA is the f32 16x16x4 map), with K in steps of 32 through double-buffered LDS.
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int XBK = 32;
 
-__device__ __forceinline__ uint32_t fbits(float x) { return __builtin_bit_cast(uint32_t, x); }
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
+// (a, b) -> packed bf16 pair, round to nearest even (v_cvt_pk_bf16_f32), a in the low half
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    const f2_t v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
 // (x0, x1) -> three packed bf16 pairs (x0 in the low half): h, m, l with x = h + m + l
 __device__ __forceinline__ void split3(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
-    const uint32_t u0 = fbits(x0), u1 = fbits(x1);
-    h = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
-    const float r0 = x0 - bitsf(u0 & 0xffff0000u), r1 = x1 - bitsf(u1 & 0xffff0000u);
-    const uint32_t v0 = fbits(r0), v1 = fbits(r1);
-    m = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
-    const float s0 = r0 - bitsf(v0 & 0xffff0000u), s1 = r1 - bitsf(v1 & 0xffff0000u);
-    l = __builtin_amdgcn_perm(fbits(s1), fbits(s0), 0x07060302u);
+    h = pk_bf16(x0, x1);
+    const float r0 = x0 - bitsf(h << 16), r1 = x1 - bitsf(h & 0xffff0000u);
+    m = pk_bf16(r0, r1);
+    const float s0 = r0 - bitsf(m << 16), s1 = r1 - bitsf(m & 0xffff0000u);
+    l = pk_bf16(s0, s1);
 }
 
-// LDS image of one operand and buffer: [tile 0..3][plane 0..2][lane 0..63] x 16 B
-struct X6Img {
-    uint4 f[4][3][64];
-};
-
-template <bool KC, class G>
-__device__ __forceinline__ void x6_load(G g, int64_t k0, int t, f4& r0, f4& r1) {
-    if constexpr (KC) {
-        const int mn = (t & 15) + 16 * (t >> 6), k = 8 * ((t >> 4) & 3);
-        r0 = g(mn, k0 + k);
-        r1 = g(mn, k0 + k + 4);
-    } else {
-        const int mn = 4 * (t & 15), k = 2 * (t >> 4);
-        r0 = g(mn, k0 + k);
-        r1 = g(mn, k0 + k + 1);
-    }
-}
 // B-operand loaders take (k, mn): adapt to the (mn, k) form above
 template <class G>
 struct X6Swap {
@@ -316,94 +298,7 @@ struct X6Swap {
     __device__ __forceinline__ f4 operator()(int mn, int64_t k) const { return g(k, mn); }
 };
 
-template <bool KC>
-__device__ __forceinline__ void x6_store(X6Img& img, int t, const f4& r0, const f4& r1) {
-    if constexpr (KC) {
-        const int mn = (t & 15) + 16 * (t >> 6), kq = (t >> 4) & 3;
-        uint4 h, m, l;
-        split3(r0.x, r0.y, h.x, m.x, l.x);
-        split3(r0.z, r0.w, h.y, m.y, l.y);
-        split3(r1.x, r1.y, h.z, m.z, l.z);
-        split3(r1.z, r1.w, h.w, m.w, l.w);
-        const int tile = mn >> 4, lane = (mn & 15) + 16 * kq;
-        img.f[tile][0][lane] = h;
-        img.f[tile][1][lane] = m;
-        img.f[tile][2][lane] = l;
-    } else {
-        const int n4 = t & 15, kp = t >> 4;  // k = 2 kp, 2 kp + 1 of this K step
-        const int kg = kp >> 2, dw = kp & 3;  // fragment lane group, dword within the 16 bytes
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int mn = 4 * n4 + i;
-            uint32_t h, m, l;
-            split3(lane_get(r0, i), lane_get(r1, i), h, m, l);
-            constexpr int PLANE = 64 * 4;  // dwords per plane image
-            uint32_t* base = reinterpret_cast<uint32_t*>(&img.f[mn >> 4][0][(mn & 15) + 16 * kg]) + dw;
-            base[0] = h;
-            base[PLANE] = m;
-            base[2 * PLANE] = l;
-        }
-    }
-}
-
-template <bool AKC, bool BKC, class GA, class GB, class EP, class SA = NoHook>
-__device__ __forceinline__ void gemm_block_x6(int64_t kbeg, int64_t kend, GA ga4, GB gb4, EP ep, SA sa = SA{}) {
-    __shared__ X6Img Ai[2], Bi[2];
-    const int t = threadIdx.x, l = t & 63, w = t >> 6;
-    const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
-    const X6Swap<GB> gbs{gb4};
-    f4 a0, a1, b0, b1;
-    auto load = [&](int64_t k0) {
-        x6_load<AKC>(ga4, k0, t, a0, a1);
-        x6_load<BKC>(gbs, k0, t, b0, b1);
-    };
-    auto store = [&](int buf) {
-        sa(a0);
-        sa(a1);
-        x6_store<AKC>(Ai[buf], t, a0, a1);
-        x6_store<BKC>(Bi[buf], t, b0, b1);
-    };
-    f4 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    load(kbeg);
-    store(0);
-    __syncthreads();
-    int buf = 0;
-    for (int64_t k0 = kbeg; k0 < kend; k0 += XBK) {
-        const bool more = k0 + XBK < kend;
-        if (more) load(k0 + XBK);
-        bf16x8 fa[2][3], fb[2][3];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                fa[i][p] = __builtin_bit_cast(bf16x8, Ai[buf].f[wm / 16 + i][p][l]);
-                fb[i][p] = __builtin_bit_cast(bf16x8, Bi[buf].f[wn / 16 + i][p][l]);
-            }
-        // smallest terms first: (l h', m m', h l'), (m h', h m'), h h'
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                f4 c = acc[i][j];
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
-            }
-        if (more) store(buf ^ 1);
-        __syncthreads();
-        buf ^= 1;
-    }
-    ep(acc, wm, wn, l);
-}
-
-// Split in registers instead: the LDS holds the fp32 tiles ([mn][k], 32 k per row,
+// The split happens in registers: the LDS holds the fp32 tiles ([mn][k], 32 k per row,
 // 4-float chunks XOR-swizzled by (r ^ r >> 3) & 7: conflict-free ds_read_b128 operand
 // reads and 16-byte stores, 2-way dword stores), 32 KB per block; each wave reads its
 // fragments (two ds_read_b128 per 16-row tile) and splits them before its MFMAs.
@@ -501,15 +396,14 @@ __device__ __forceinline__ void gemm_block_x6s(int64_t kbeg, int64_t kend, GA ga
     ep(acc, wm, wn, l);
 }
 
-// The GEMM core of the layered kernels' 16-byte loader path: the bf16 split core
-// (split in registers), or the A/B library variants -DNCF_GEMM_F32 (the f32-MFMA
-// core) and -DNCF_GEMM_X6P (split once per block into bf16 plane images).
+// The GEMM core of the layered kernels' 16-byte loader path: the bf16 split core, or
+// (-DNCF_GEMM_F32, the A/B library variant) the f32-MFMA core.  (A variant that split
+// once per block into three bf16 plane images in LDS -- 48 KB per block, 3 blocks per
+// CU -- measured slower: stress 1304 against 1093 us per step.)
 template <bool AKC, bool BKC, class GA, class GB, class EP, class SA = NoHook>
 __device__ __forceinline__ void gemm_block_vx(int64_t kbeg, int64_t kend, GA ga4, GB gb4, EP ep, SA sa = SA{}) {
 #if defined(NCF_GEMM_F32)
     gemm_block_v<AKC, BKC>(kbeg, kend, ga4, gb4, ep, sa);
-#elif defined(NCF_GEMM_X6P)
-    gemm_block_x6<AKC, BKC>(kbeg, kend, ga4, gb4, ep, sa);
 #else
     gemm_block_x6s<AKC, BKC>(kbeg, kend, ga4, gb4, ep, sa);
 #endif
