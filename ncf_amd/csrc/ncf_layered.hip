@@ -568,7 +568,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, con
         };
         // K = J <= 256 here (2-8 K steps of 32): the masked epilogue dominates and the
         // f32 core's occupancy (8 waves / SIMD against 3) wins -- stress 88.8 against
-        // 95.4 us per launch with the split core (profiles/r03x6_*)
+        // 95.4 us per launch with the split core (profiles/r03x6/stress_kernel_stats_*.csv)
         gemm_block_v<true, false>(0, J, ga4, gb4, ep);
     } else {
         gemm_block<true, false>(m0, n0, 0, J, ga, gb, ep);
