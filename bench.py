@@ -520,7 +520,11 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
     eng, model, pipe = setup_engine(cfg, ds, train, world, rank, dev, group, global_batch)
     nb = eng.num_batches
     n_rows = eng.n_total
-    warm = max(1, -(-max(1, warmup) // nb)) * nb if whole_epochs else max(1, warmup)
+    # warm-up: whole epochs, at least two -- on a fresh box the first process's first
+    # epochs pay one-off host costs (the sampler pool's first passes, first-touch of
+    # pinned staging buffers): C3 at the driver's command measured 1.06G with one
+    # warm-up epoch there against 1.145-1.148G in the next processes on the same box
+    warm = max(2, -(-max(1, warmup) // nb)) * nb if whole_epochs else max(1, warmup)
     eng.batches_done = 0
     run_steps(eng, warm, use_graph)
     torch.cuda.synchronize(dev)
