@@ -370,6 +370,7 @@ def setup_engine(cfg, ds, train, world, rank, dev, group, global_batch, seed=0):
 # C5 (19,418) 14.7 against 14.0 -- a host running whole long epochs ahead slows the
 # small steps (the frozen rate is the same in both).
 BOUNDARY = os.environ.get("NCF_BENCH_BOUNDARY", "auto")
+WARM_S = float(os.environ.get("NCF_BENCH_WARM_S", "0.5"))
 EARLY_MAX_STEPS = 1024
 
 
@@ -520,14 +521,21 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
     eng, model, pipe = setup_engine(cfg, ds, train, world, rank, dev, group, global_batch)
     nb = eng.num_batches
     n_rows = eng.n_total
-    # warm-up: whole epochs, at least two -- on a fresh box the first process's first
-    # epochs pay one-off host costs (the sampler pool's first passes, first-touch of
-    # pinned staging buffers): C3 at the driver's command measured 1.06G with one
-    # warm-up epoch there against 1.145-1.148G in the next processes on the same box
-    warm = max(2, -(-max(1, warmup) // nb)) * nb if whole_epochs else max(1, warmup)
+    # warm-up: whole epochs, at least `warmup` steps and, with whole epochs, at least
+    # WARM_S seconds -- the first process on a fresh box ran its first timed C3 epoch
+    # at 61 us/step after one or two warm-up epochs (~10 ms) against 57 in the next
+    # processes on the same box, with the same host boundary times (a device-side
+    # ramp; the frozen rate right after it was 56.7)
+    warm = max(1, -(-max(1, warmup) // nb)) * nb if whole_epochs else max(1, warmup)
     eng.batches_done = 0
+    t_w = time.perf_counter()
     run_steps(eng, warm, use_graph)
     torch.cuda.synchronize(dev)
+    while whole_epochs and time.perf_counter() - t_w < WARM_S:
+        run_steps(eng, nb, use_graph)
+        warm += nb
+        torch.cuda.synchronize(dev)
+    warm_s = time.perf_counter() - t_w
     epochs = max(1, -(-steps // nb)) if whole_epochs else steps / nb
     k = int(round(epochs * nb))
     _barrier(group, dev)
@@ -565,6 +573,8 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
         host["boundary_rest"] = float(np.mean([x[1] for x in bm]))
     return {"eng": eng, "model": model, "pipe": pipe, "snap": snap, "value": epochs * n_rows / dt, "dt": dt, "steps": k,
             "epochs": epochs, "fresh_epochs": fresh, "rows_per_epoch": n_rows, "batches_per_epoch": nb,
+            "warmup_run": {"steps": warm, "seconds": round(warm_s, 3),
+                           "note": f"untimed: whole epochs, >= --warmup steps and >= {WARM_S} s (device ramp on a fresh box)"},
             "final_loss": final_loss, "frozen_value": k * n_rows / nb / dtf, "frozen_ms_per_step": dtf / k * 1e3,
             "epoch_host_ms": host}
 
@@ -775,6 +785,7 @@ def main():
             "n_gpus": world,
             "steps": k,
             "warmup": args.warmup,
+            "warmup_run": m["warmup_run"],
             "ms_per_step": dt / k * 1e3,
             "higher_is_better": True,
             "scaling": "strong",
