@@ -531,7 +531,9 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
     t_w = time.perf_counter()
     run_steps(eng, warm, use_graph)
     torch.cuda.synchronize(dev)
-    while whole_epochs and time.perf_counter() - t_w < WARM_S:
+    # every rank must run the same number of steps (each step is a collective at N > 1):
+    # another epoch while any rank is short of WARM_S
+    while whole_epochs and _max_over_ranks(float(time.perf_counter() - t_w < WARM_S), group, dev) > 0:
         run_steps(eng, nb, use_graph)
         warm += nb
         torch.cuda.synchronize(dev)
