@@ -835,6 +835,14 @@ def main():
             "cpu_baseline": cpu,
             "setup_s": {"data": round(t_data, 2)},
         }
+        if path != L.PATH_FUSED and f % 4 == 0:
+            # the layered GEMMs run on v_mfma_f32_16x16x32_bf16 (six bf16 products per fp32
+            # product): the ceiling of those instructions in fp32-equivalent flops is the
+            # dense bf16 peak / 6
+            out["roofline"]["bf16_split_ceiling"] = {
+                "peak": 2500.0 / 6, "unit": "TFLOP/s (fp32-equivalent)", "frac": executed_tf / (2500.0 / 6),
+                "note": "the same executed flops against the bf16-split GEMM core's own ceiling (2.5 PF dense bf16 / 6); "
+                        "`frac` above is against the fp32 MFMA peak"}
         if rehearsal:
             out["rehearsal"] = (f"{world} ranks on one device over {os.environ.get('NCF_BENCH_BACKEND', 'nccl')}: "
                                 "a check of the N > 1 flow, not a measurement")
