@@ -532,12 +532,21 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
     run_steps(eng, warm, use_graph)
     torch.cuda.synchronize(dev)
     # every rank must run the same number of steps (each step is a collective at N > 1):
-    # another epoch while any rank is short of WARM_S
+    # another epoch while any rank is short of WARM_S.  Those extra epochs only warm the
+    # device: the trained state goes back to the one the requested warm-up left (the
+    # quality figures stay those of a few epochs of training, as in the reference's runs)
+    snap0 = None
+    extra = 0
     while whole_epochs and _max_over_ranks(float(time.perf_counter() - t_w < WARM_S), group, dev) > 0:
+        if snap0 is None:
+            snap0 = snapshot_state(eng)
         run_steps(eng, nb, use_graph)
-        warm += nb
+        extra += nb
         torch.cuda.synchronize(dev)
     warm_s = time.perf_counter() - t_w
+    if snap0 is not None:
+        restore_state(eng, snap0)
+        eng.batches_done -= extra  # the control block's batch / step went back with the state
     epochs = max(1, -(-steps // nb)) if whole_epochs else steps / nb
     k = int(round(epochs * nb))
     _barrier(group, dev)
@@ -575,8 +584,9 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
         host["boundary_rest"] = float(np.mean([x[1] for x in bm]))
     return {"eng": eng, "model": model, "pipe": pipe, "snap": snap, "value": epochs * n_rows / dt, "dt": dt, "steps": k,
             "epochs": epochs, "fresh_epochs": fresh, "rows_per_epoch": n_rows, "batches_per_epoch": nb,
-            "warmup_run": {"steps": warm, "seconds": round(warm_s, 3),
-                           "note": f"untimed: whole epochs, >= --warmup steps and >= {WARM_S} s (device ramp on a fresh box)"},
+            "warmup_run": {"steps": warm + extra, "seconds": round(warm_s, 3), "trained_steps_kept": warm,
+                           "note": f"untimed: whole epochs, >= --warmup steps and >= {WARM_S} s (device ramp on a fresh box); "
+                                   "the trained state of the steps past --warmup is discarded"},
             "final_loss": final_loss, "frozen_value": k * n_rows / nb / dtf, "frozen_ms_per_step": dtf / k * 1e3,
             "epoch_host_ms": host}
 
