@@ -27,6 +27,16 @@
 #include <mutex>
 #include <vector>
 
+// Function multiversioning (an AVX-512 / AVX2 clone picked at load time).
+// NCF_SANITIZE (the ASan / TSan builds of tests/test_sanitizers.py): one version --
+// the clones' ifunc resolver runs during relocation, before a sanitizer runtime is
+// initialised, and an instrumented resolver faults there.
+#ifdef NCF_SANITIZE
+#define NCF_TARGET_CLONES(...)
+#else
+#define NCF_TARGET_CLONES(...) __attribute__((target_clones(__VA_ARGS__)))
+#endif
+
 namespace mtj {
 
 constexpr int N = 624, M = 397;
@@ -240,7 +250,7 @@ inline void jump_direct(const uint32_t* win, const Poly& g, uint32_t* out) {
 }
 
 // acc (circular, first word at s) ^= t (linear)
-__attribute__((target_clones("avx512f", "avx2", "default"))) inline void xor_rotated(uint32_t* acc, int s,
+NCF_TARGET_CLONES("avx512f", "avx2", "default") inline void xor_rotated(uint32_t* acc, int s,
                                                                                     const uint32_t* t) {
     const int n1 = N - s;
     for (int j = 0; j < n1; ++j) acc[s + j] ^= t[j];

@@ -191,23 +191,44 @@ __device__ __forceinline__ void step_scalars_ahead(ScCache* cache, int64_t t_ste
 }
 
 // The step-scalar cache entry pair of a control block (see ScCache): one slot per
-// ctl pointer seen, for the life of the process; null (always recompute) past
-// SC_SLOTS control blocks.
-static ScCache* sc_cache_for(const void* ctl) {
+// (device, ctl pointer) seen, for the life of the process; null (always recompute)
+// past SC_SLOTS control blocks on a device.  g_sc_cache has one copy per device, so
+// its address is looked up per device -- the device of the launch's stream -- with
+// that device current for the lookup.
+static ScCache* sc_cache_for(const void* ctl, void* stream) {
+    struct DevSlots {
+        ScCache* base = nullptr;
+        bool failed = false;
+        std::unordered_map<const void*, int> slots;
+    };
     static std::mutex mu;
-    static std::unordered_map<const void*, int> slots;
-    static ScCache* base = nullptr;
+    static std::unordered_map<int, DevSlots> devs;
+    int dev = -1;
+    if (hipStreamGetDevice((hipStream_t)stream, &dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> lk(mu);
-    if (base == nullptr && hipGetSymbolAddress((void**)&base, HIP_SYMBOL(g_sc_cache)) != hipSuccess) {
-        base = nullptr;
-        return nullptr;
+    DevSlots& d = devs[dev];
+    if (d.failed) return nullptr;
+    if (d.base == nullptr) {
+        int cur = -1;
+        if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+        if (cur != dev && hipSetDevice(dev) != hipSuccess) {
+            d.failed = true;
+            return nullptr;
+        }
+        const hipError_t e = hipGetSymbolAddress((void**)&d.base, HIP_SYMBOL(g_sc_cache));
+        if (cur != dev) (void)hipSetDevice(cur);
+        if (e != hipSuccess) {
+            d.base = nullptr;
+            d.failed = true;
+            return nullptr;
+        }
     }
-    auto it = slots.find(ctl);
-    if (it != slots.end()) return base + 2 * it->second;
-    if ((int)slots.size() >= SC_SLOTS) return nullptr;
-    const int k = (int)slots.size();
-    slots.emplace(ctl, k);
-    return base + 2 * k;
+    auto it = d.slots.find(ctl);
+    if (it != d.slots.end()) return d.base + 2 * it->second;
+    if ((int)d.slots.size() >= SC_SLOTS) return nullptr;
+    const int k = (int)d.slots.size();
+    d.slots.emplace(ctl, k);
+    return d.base + 2 * k;
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
@@ -1880,7 +1901,7 @@ int ncf_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(adam_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
                        exp_avg_sq, R, ctl, lr, beta1, beta2, (float)eps, loss_slot, loss_hist, hist_len,
-                       sc_cache_for(ctl));
+                       sc_cache_for(ctl, stream));
     return launch_status();
 }
 
@@ -1921,7 +1942,7 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
     hipLaunchKernelGGL(reduce_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
                        static_cast<const float*>(workspace), lo, stride, rows, nA, lay->tower_begin, lay->tower_len,
                        params, grads, exp_avg, exp_avg_sq, R, RE, ctl, lr, beta1, beta2, (float)eps, loss_hist,
-                       hist_len, w0_part(lay, workspace), sc_cache_for(ctl));
+                       hist_len, w0_part(lay, workspace), sc_cache_for(ctl, stream));
     return launch_status();
 }
 
@@ -2063,7 +2084,7 @@ int ncf_lazy_adam_step(const ncf_layout* lay, const void* workspace, float* para
     hipLaunchKernelGGL(lazy_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
                        static_cast<const float*>(workspace), lo, stride, rows, nA, lay->tower_begin, lay->tower_len, R,
                        ctl, lr, beta1, beta2, (float)eps, loss_hist, hist_len, w0_part(lay, workspace), a,
-                       sc_cache_for(ctl));
+                       sc_cache_for(ctl, stream));
     return launch_status();
 }
 
@@ -2138,7 +2159,7 @@ int ncf_lazy_adam_step_packed(const ncf_layout* lay, float* params, float* exp_a
     const int64_t nB = step_blocks(a, t);
     hipLaunchKernelGGL(lazy_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
                        (const float*)nullptr, lo, stride, 0, nA, lay->tower_begin, lay->tower_len, R, ctl, lr, beta1,
-                       beta2, (float)eps, loss_hist, hist_len, W0Part{nullptr, 0, 0, 0, 0}, a, sc_cache_for(ctl));
+                       beta2, (float)eps, loss_hist, hist_len, W0Part{nullptr, 0, 0, 0, 0}, a, sc_cache_for(ctl, stream));
     return launch_status();
 }
 

@@ -107,11 +107,14 @@ class HostSampler:
 
 
 def sampler_threads():
-    """Threads of a host sampler pool: NCF_SAMPLER_THREADS, else min(12, half the CPUs
-    this process may run on) -- a GPU box grants 16 CPUs per GPU, and the rest are
-    the training loop's (graph replays, the epoch pipeline's staging, the HIP runtime):
-    the pool only has to finish an epoch's draws while the previous epoch trains
-    (ml-20m on the box: 42 ms per epoch at 8 threads, 27 ms at 12)."""
+    """Threads of a host sampler pool: NCF_SAMPLER_THREADS, else min(12, half this
+    rank's share of the CPUs the process may run on) -- a GPU box grants 16 CPUs per
+    GPU, and the rest are the training loop's (graph replays, the epoch pipeline's
+    staging, the HIP runtime): the pool only has to finish an epoch's draws while the
+    previous epoch trains (ml-20m on the box: 42 ms per epoch at 8 threads, 27 ms at
+    12).  The share is the CPUs divided by LOCAL_WORLD_SIZE (set by
+    torch.distributed.run and by bench.py's own spawn): the pools spin-wait inside a
+    pass, so N local ranks must not each size theirs for the whole machine."""
     import os
     v = os.environ.get("NCF_SAMPLER_THREADS")
     if v:
@@ -120,7 +123,8 @@ def sampler_threads():
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(12, n // 2))
+    lws = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
+    return max(1, min(12, (n // lws) // 2))
 
 
 def _membership_from(train_mat, features):

@@ -99,14 +99,28 @@ class TrainEngine:
 
     @classmethod
     def auto_dp_mode(cls, lay, ranges, nranges, batch_size):
-        """("touched" | "allreduce", packed floats) for dp_mode "auto" at this global batch."""
+        """("touched" | "allreduce" | "zero1", packed floats) for dp_mode "auto" at this
+        global batch: touched where the packed buffer is small enough, else the
+        size rule of default_dp_mode without deferred Adam (all-reduce up to
+        ALLREDUCE_MAX_FLOATS, zero1 above: the optimizer state stays sharded)."""
         pf = int(L.hip().ncf_touched_packed_floats(ctypes.byref(lay), ranges, nranges, int(batch_size)))
-        return ("touched" if 0 < pf <= cls.TOUCHED_MAX_FRACTION * int(lay.total) else "allreduce"), pf
+        if 0 < pf <= cls.TOUCHED_MAX_FRACTION * int(lay.total):
+            return "touched", pf
+        return cls.default_dp_mode(int(lay.total), touched_ok=False), pf
 
     def _resolve_auto(self, batch_size):
         self.dp_mode, pf = self.auto_dp_mode(self.lay, self._ranges, self._nranges, batch_size)
         if self.dp_mode == "touched":
             self._packed = torch.zeros(pf, dtype=torch.float32, device=self.device)
+        elif self.dp_mode == "zero1":
+            # the flat buffers were padded to world x shard floats at construction
+            # (__init__): keep this rank's slice of the optimizer state
+            self._init_shards()
+            if self.optimizer == "adam":
+                r, S = self.rank, self.shard
+                self.exp_avg = self.exp_avg[r * S:(r + 1) * S].clone()
+                self.exp_avg_sq = self.exp_avg_sq[r * S:(r + 1) * S].clone()
+            self._drop_graphs()
 
     def __init__(self, model, lr=1e-3, optimizer="adam", betas=(0.9, 0.999), eps=1e-8,
                  world_size=1, rank=0, process_group=None, max_batches=1 << 16, dp_mode=None, distill=None):
@@ -129,13 +143,14 @@ class TrainEngine:
         if dp_mode in ("touched", "auto") and not touched_ok:
             raise ValueError("dp_mode 'touched' needs Adam, factor_num % 4 == 0 and tables of <= 2^19 rows")
         self.dp_mode = dp_mode
-        if dp_mode in ("zero1", "sparse"):
-            # flat buffers padded to world x shard floats; rank r owns [r*S, (r+1)*S)
-            self.shard = D.shard_floats(int(lay.total), self.world_size)
-            n = self.shard * self.world_size
-        else:
-            self.shard = None
-            n = int(lay.total)
+        # flat buffers padded to world x shard floats where the exchange shards them
+        # (rank r owns [r*S, (r+1)*S)); "auto" pads too when its fallback would be zero1
+        shards = dp_mode in ("zero1", "sparse") or (
+            dp_mode == "auto" and self.default_dp_mode(int(lay.total)) == "zero1")
+        self.shard = None
+        n = int(lay.total)
+        if shards:
+            n = D.shard_floats(int(lay.total), self.world_size) * self.world_size
         self.flat, lay0 = ops.ensure_flat(model, n)
         # the engine's own copy: ncf_layout_tune shapes it for the batch size
         self.lay = type(lay0).from_buffer_copy(lay0)
@@ -148,7 +163,7 @@ class TrainEngine:
         n = self.flat.numel()
         self.grads = torch.zeros(n, dtype=torch.float32, device=dev)
         self.optimizer = optimizer
-        n_opt = self.shard if dp_mode in ("zero1", "sparse") else n
+        n_opt = D.shard_floats(int(lay.total), self.world_size) if dp_mode in ("zero1", "sparse") else n
         if optimizer == "adam":
             self.exp_avg = torch.zeros(n_opt, dtype=torch.float32, device=dev)
             self.exp_avg_sq = torch.zeros(n_opt, dtype=torch.float32, device=dev)
@@ -163,29 +178,7 @@ class TrainEngine:
         self._loss_slot = int(self.lay.loss_slot)
         self._opt_ptrs = (self.flat.data_ptr(), self.grads.data_ptr())
         if dp_mode in ("zero1", "sparse"):
-            S, r = self.shard, self.rank
-            self.gshard = torch.zeros(S if dp_mode == "zero1" else 0, dtype=torch.float32, device=dev)
-            # an empty [0, 0) range when no active parameter falls in the shard: the
-            # launch still records the loss if this rank owns the loss slot
-            srng = D.shard_ranges(rng, self.world_size, r, S) or [[0, 0]]
-            self._sranges = (ctypes.c_int64 * (2 * len(srng)))(*[x for q in srng for x in q])
-            self._nsranges = len(srng)
-            self.loss_owner = self._loss_slot // S
-            self._loss_slot = self._loss_slot - r * S
-            self._opt_ptrs = (self.flat.data_ptr() + 4 * r * S, self.gshard.data_ptr())
-            if dp_mode == "sparse":  # the owner's summed shard gradient sits in the local buffer
-                self._opt_ptrs = (self.flat.data_ptr() + 4 * r * S, self.grads.data_ptr() + 4 * r * S)
-                lay = self.lay
-                f, dm = model.factor_num, model.factor_num << (model.num_layers - 1)
-                act = ops.active_mask(model)[:4]
-                if distill is not None and distill.active_extra is not None:
-                    act = [a or b for a, b in zip(act, distill.active_extra[:4])]
-                self._sparse_tables = [(int(off), w, nrows, side) for (off, w, nrows, side), a in zip(
-                    [(lay.ug, f, model.user_num, 0), (lay.ig, f, model.item_num, 1),
-                     (lay.um, dm, model.user_num, 0), (lay.im, dm, model.item_num, 1)], act) if a]
-                self._sparse_tail = (int(lay.tower_begin), int(lay.total))
-                self.sparse_bytes_sent = 0
-            self._ag_scratch = None
+            self._init_shards()
         self.loss_hist = torch.zeros(max_batches, dtype=torch.float32, device=dev)
         self.rows = None
         self.n_total = 0
@@ -212,6 +205,38 @@ class TrainEngine:
             self._packed = torch.zeros(int(L.hip().ncf_touched_packed_floats(ctypes.byref(self.lay), self._ranges,
                                                                              self._nranges, 1)),
                                        dtype=torch.float32, device=dev)  # resized per batch size
+
+    def _init_shards(self):
+        """zero1 / sparse: this rank's shard of the flat buffers, its active ranges,
+        the loss slot's owner and the optimizer's pointers."""
+        model, dm_ = self.model, self.dp_mode
+        S = self.shard = D.shard_floats(int(self.lay.total), self.world_size)
+        r = self.rank
+        assert self.flat.numel() >= S * self.world_size
+        rng = [[self._ranges[2 * k], self._ranges[2 * k + 1]] for k in range(self._nranges)]
+        self.gshard = torch.zeros(S if dm_ == "zero1" else 0, dtype=torch.float32, device=self.device)
+        # an empty [0, 0) range when no active parameter falls in the shard: the
+        # launch still records the loss if this rank owns the loss slot
+        srng = D.shard_ranges(rng, self.world_size, r, S) or [[0, 0]]
+        self._sranges = (ctypes.c_int64 * (2 * len(srng)))(*[x for q in srng for x in q])
+        self._nsranges = len(srng)
+        slot = int(self.lay.loss_slot)
+        self.loss_owner = slot // S
+        self._loss_slot = slot - r * S
+        self._opt_ptrs = (self.flat.data_ptr() + 4 * r * S, self.gshard.data_ptr())
+        if dm_ == "sparse":  # the owner's summed shard gradient sits in the local buffer
+            self._opt_ptrs = (self.flat.data_ptr() + 4 * r * S, self.grads.data_ptr() + 4 * r * S)
+            lay = self.lay
+            f, dm = model.factor_num, model.factor_num << (model.num_layers - 1)
+            act = ops.active_mask(model)[:4]
+            if self.distill is not None and self.distill.active_extra is not None:
+                act = [a or b for a, b in zip(act, self.distill.active_extra[:4])]
+            self._sparse_tables = [(int(off), w, nrows, side) for (off, w, nrows, side), a in zip(
+                [(lay.ug, f, model.user_num, 0), (lay.ig, f, model.item_num, 1),
+                 (lay.um, dm, model.user_num, 0), (lay.im, dm, model.item_num, 1)], act) if a]
+            self._sparse_tail = (int(lay.tower_begin), int(lay.total))
+            self.sparse_bytes_sent = 0
+        self._ag_scratch = None
 
     # ------------------------------------------------------------------ data
     def set_epoch_stream(self, rows, batch_size, checked=False):

@@ -156,7 +156,12 @@ class Trainer:
     def _report_pending(self, pending, save_fn):
         epoch, ev0, ev1, out, snap, t0 = pending
         ev1.synchronize()
-        wall = time.time() - t0  # like the reference: from the epoch's start to its metrics
+        # like the reference: from the epoch's start to its metrics -- the moment the
+        # device finished the epoch's metrics pass (ev1), mapped onto the host clock
+        # through the anchor event of fit(), not the later moment this readback runs
+        # (after epoch e + 1 was enqueued)
+        anchor, host_anchor = self._clock
+        wall = host_anchor + anchor.elapsed_time(ev1) / 1e3 - t0
         avg_loss = float(np.mean(out["loss"].numpy().astype(np.float64)))
         hr = float(np.mean(out["hr"].numpy().astype(np.float64)))
         ndcg = float(np.mean(out["nd"].numpy().astype(np.float64)))
@@ -168,9 +173,11 @@ class Trainer:
         save_fn, the parameters to a device snapshot), epoch e + 1 is enqueued, and
         only then is epoch e read back, printed and checkpointed -- the same values,
         the same generator draws in the same order, no idle device between epochs.
-        Time= (history "time") is wall-clock from the epoch's start to its metrics
-        being read back, as train_neumf.py:100,130 measures it; history
-        "device_time" is the epoch's device time (steps + evaluation)."""
+        Time= (history "time") is wall-clock from the epoch's start to the end of its
+        metrics pass, as train_neumf.py:100,130 measures it (the device's completion
+        of the pass, mapped onto the host clock by an anchor event, so epoch e's time
+        does not include epoch e + 1's host work); history "device_time" is the
+        epoch's device time (steps + evaluation)."""
         self._best = [0, 0, 0]  # hr, ndcg, epoch
         if self.world_size > 1:  # the loss readback is a collective there: in line
             for epoch in range(int(epochs)):
@@ -187,6 +194,10 @@ class Trainer:
                 self._report(epoch, avg_loss, hr, ndcg, time.time() - t0, save_fn, None)
         else:
             pending = None
+            anchor = torch.cuda.Event(enable_timing=True)
+            anchor.record()
+            anchor.synchronize()
+            self._clock = (anchor, time.time())
             for epoch in range(int(epochs)):
                 self.model.train()
                 t0 = time.time()

@@ -1,0 +1,206 @@
+"""Multi-rank parity at the reference's full shapes ("C3 (1 vs 2/4/8
+GPUs)", first steps at <= 1e-5 relative; scripts/train_neumf.py:55,86,90,106-118).
+
+World 2 and 4 ranks are spawned processes sharing cuda:0 over gloo (the one-GPU test
+box cannot hold one RCCL rank per process; gloo moves the same device buffers through
+the host, so everything but the transport is the bench's N > 1 path):
+
+  * C3 -- NCF(16,3) NeuMF-end, the ml-1m-shaped data set, global batch 65,536, the
+    default exchange (dp_mode "auto", which resolves to "allreduce" here: a 65,536-row
+    ml-1m batch touches every row), one whole fresh epoch through Trainer.fit (the
+    epoch pipeline: fresh negatives and permutation, the fused factored step on each
+    rank's 32,768 / 16,384-row shard, hipGraph replay);
+  * C4 -- NCF(16,3) at the ml-20m id space (138,494 x 26,745), global batch 65,536,
+    world 2, 20 steps on the engine (dp_mode "auto" -> "touched": the touched rows
+    packed with the tower gradient, one all-reduce, replicated deferred Adam).
+
+Checks: ranks bitwise equal to each other (losses and every parameter); every step's
+loss within rtol 1e-5 of the single-rank engine on the same stream; the losses
+against the oracle (oracle/ncf_oracle.py, the reference loop restated on torch CPU
+ops + torch.optim.Adam with the same negatives and permutation): C3 the first 20
+steps at rtol 1e-5; C4 the first 10 at 1e-5 and 20 at 1e-4 (the single-rank C4 run
+itself parts from the fp32 oracle to ~3.6e-5 from step ~12, test_gpu_fullsize.py);
+parameters within rtol 1e-4 / atol 1e-6 of the single-rank run (summation order of
+the shard sums)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle import ncf_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+B = 65536
+
+
+def _data(shape):
+    from ncf_amd import synthetic
+    from ncf_amd.data import NCFData
+    ds = synthetic.make_dataset(shape, seed=0)
+    I = ds["item_num"]
+    train = NCFData(np.stack([ds["train_users"], ds["train_items"]], 1), I, None, 4, True)
+    tu = np.repeat(ds["test_users"], 100)
+    ti = np.concatenate([ds["test_items"][:, None], ds["test_negatives"]], 1).reshape(-1)
+    test = NCFData(np.stack([tu, ti], 1), I, None, 0, False)
+    return ds, train, test
+
+
+def _flat(model):
+    return torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu().numpy()
+
+
+def _c3_run(world, rank, group):
+    """Trainer.fit(1) at C3 (train_neumf.py:98-131), seeds 0 as the scripts set them."""
+    from torch.utils.data import DataLoader
+    from ncf_amd.models import NCF
+    from ncf_amd.trainer import Trainer
+    ds, train, test = _data("ml-1m")
+    np.random.seed(0)
+    torch.manual_seed(0)
+    model = NCF(ds["user_num"], ds["item_num"], 16, 3, 0.0, "NeuMF-end").to(DEV)
+    tr = Trainer(model, train, DataLoader(test, batch_size=100, shuffle=False), batch_size=B, lr=1e-3, top_k=10,
+                 verbose=False, world_size=world, rank=rank, process_group=group)
+    tr.fit(1)
+    torch.cuda.synchronize()
+    eng = tr.engine
+    losses = eng.epoch_losses()[:eng.num_batches].astype(np.float64).copy()
+    return _flat(model), losses, eng.dp_mode
+
+
+def _c4_stream(train, item_num, dev):
+    """One epoch stream as the host path of Trainer._epoch_stream builds it:
+    ng_sample (NumPy global stream), the DataLoader's permutation (torch global
+    generator), packed rows grouped by item per global batch."""
+    from ncf_amd import ops
+    from ncf_amd.data import epoch_permutation
+    train.ng_sample()
+    u, i, y = train.arrays()
+    perm = epoch_permutation(len(u)).to(dev)
+    rows = torch.from_numpy(ops.pack_rows_host(u, i, y)).to(dev)
+    return ops.EpochPrep(torch.device(dev))(rows, perm, B, int(item_num))
+
+
+C4_STEPS = 20
+
+
+def _c4_run(world, rank, group):
+    from ncf_amd.engine import TrainEngine
+    from ncf_amd.models import NCF
+    ds, train, _ = _data("ml-20m")
+    np.random.seed(0)
+    torch.manual_seed(0)
+    model = NCF(ds["user_num"], ds["item_num"], 16, 3, 0.0, "NeuMF-end").to(DEV)
+    eng = TrainEngine(model, lr=1e-3, world_size=world, rank=rank, process_group=group)
+    stream = _c4_stream(train, ds["item_num"], DEV)
+    eng.set_epoch_stream(stream, B, checked=True)
+    eng.run(C4_STEPS)
+    torch.cuda.synchronize()
+    losses = eng.epoch_losses()[:C4_STEPS].astype(np.float64).copy()
+    return _flat(model), losses, eng.dp_mode
+
+
+RUNS = {"c3": _c3_run, "c4": _c4_run}
+
+
+def _worker(rank, world, port, name, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    # the ranks share the box's CPUs: one sampler pool each, sized for the group
+    os.environ.setdefault("LOCAL_WORLD_SIZE", str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        res = RUNS[name](world, rank, dist.group.WORLD)
+    except Exception:  # report instead of leaving the other ranks waiting in a collective
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+        os._exit(1)
+    q.put((rank, res, None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(name, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, out, err = q.get(timeout=600)
+            if out is None:
+                raise AssertionError(f"rank {r} failed:\n{err}")
+            res[r] = out
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    return res
+
+
+_single = {}
+
+
+def _single_rank(name):
+    if name not in _single:
+        _single[name] = RUNS[name](1, 0, None)
+    return _single[name]
+
+
+def _oracle_losses(name, steps):
+    """The reference loop's first `steps` losses from the same seeds (oracle)."""
+    ds, _, _ = _data("ml-20m" if name == "c4" else "ml-1m")
+    U, I = ds["user_num"], ds["item_num"]
+    pu, pi = ds["train_users"], ds["train_items"]
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    torch.manual_seed(0)
+    ref = O.OracleNCF(U, I, 16, 3, 0.0, "NeuMF-end")
+    neg = O.ng_sample(pu, pi, I, 4, 0)
+    users = np.concatenate([pu, np.repeat(pu, 4)]).astype(np.int64)
+    items = np.concatenate([pi, neg]).astype(np.int64)
+    labels = np.concatenate([np.ones(len(pu), np.int64), np.zeros(len(neg), np.int64)])
+    perm = O.epoch_order(len(users))
+    sl = [perm[b * B:(b + 1) * B] for b in range(steps)]
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    return np.asarray(O.train_steps(ref, opt, [users[s] for s in sl], [items[s] for s in sl],
+                                    [labels[s] for s in sl]), dtype=np.float64)
+
+
+@pytest.mark.parametrize("name,world", [("c3", 2), ("c3", 4), ("c4", 2)])
+def test_full_shape_ranks_match_single_rank_and_oracle(name, world):
+    res = _spawn(name, world)
+    flat0, loss0, mode0 = res[0]
+    for r in range(1, world):
+        assert np.array_equal(res[r][1], loss0), f"rank {r} losses differ from rank 0"
+        assert np.array_equal(res[r][0], flat0), f"rank {r} parameters differ from rank 0"
+        assert res[r][2] == mode0
+    assert mode0 == {"c3": "allreduce", "c4": "touched"}[name], mode0
+    flat1, loss1, mode1 = _single_rank(name)
+    assert mode1 == "single"
+    nb = {"c3": 76, "c4": C4_STEPS}[name]
+    assert len(loss0) == len(loss1) == nb
+    np.testing.assert_allclose(loss0, loss1, rtol=1e-5, err_msg=f"{name} world {world}: per-step loss vs 1 rank")
+    np.testing.assert_allclose(flat0, flat1, rtol=1e-4, atol=1e-6, err_msg=f"{name} world {world}: params vs 1 rank")
+    ref = _oracle_losses(name, 20)
+    if name == "c3":
+        np.testing.assert_allclose(loss0[:20], ref, rtol=1e-5, err_msg="c3: first 20 losses vs oracle")
+    else:
+        np.testing.assert_allclose(loss0[:10], ref[:10], rtol=1e-5, err_msg="c4: first 10 losses vs oracle")
+        np.testing.assert_allclose(loss0[:20], ref, rtol=1e-4, err_msg="c4: first 20 losses vs oracle")

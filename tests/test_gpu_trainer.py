@@ -10,6 +10,7 @@ import os
 import re
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -51,8 +52,14 @@ def test_trainer_matches_reference_script(golden, ml100k_dir):
     loader = data.DataLoader(test_ds, batch_size=100, shuffle=False, num_workers=0)
     model = NCF(U, I, 8, 3, 0.0, "NeuMF-end").to("cuda:0")
     tr = Trainer(model, train_ds, loader, batch_size=256, lr=1e-3, top_k=10)
+    t0 = time.time()
     res = tr.fit(2)
+    wall = time.time() - t0
     assert res["parameters"] == 107841
+    # Time= of each epoch runs from its start to the end of its metrics pass: the
+    # epochs follow each other, so the times do not overlap and sum to at most fit()
+    assert all(h["time"] > 0 for h in tr.history)
+    assert sum(h["time"] for h in tr.history) <= wall, (tr.history, wall)
     for h, (e, l, hr, nd) in zip(tr.history, ref):
         assert h["epoch"] == e
         assert abs(h["loss"] - l) <= 1e-3 * l + 1e-4, (tr.history, ref)
