@@ -246,16 +246,20 @@ def _oracle_steps(cfg, U, I, batch, seconds, threads, users=None, items=None, la
             "ms_per_step": el / steps * 1e3}
 
 
+SWEEP_THREADS = (8, 16, 32, 64, 128)
+
+
 def cpu_baseline(cfg, seconds, script_epoch=True):
     """BASELINE.md section 3 on the host cores (run in a child process that never
     touches the GPU): the oracle -- the reference model restated on stock PyTorch CPU
     ops + torch.optim.Adam, `kind` "port" -- timed
-      * step-only on the config's epoch stream at os.cpu_count() threads and at 16;
-      * step-only at C2 and C4 shapes (random ids) at 16 threads;
+      * step-only on the config's epoch stream at each of SWEEP_THREADS torch threads
+        (the best is `value`, its count `cores`) and at os.cpu_count() threads;
+      * step-only at C2 and C4 shapes (random ids) at the best count;
       * a script-equivalent epoch (train_neumf.py:98-131): ng_sample (the oracle's
         C restatement), the stock DataLoader(shuffle=True, num_workers=4) over a
         per-sample dataset, zero_grad/forward/BCE/backward/Adam per batch, and the
-        metrics() pass (forward over the test candidates + HR/NDCG), at 16 threads."""
+        metrics() pass (forward over the test candidates + HR/NDCG), at the best count."""
     from oracle import ncf_oracle as O
     shape, f, L, batch = CONFIGS[cfg]
     ds, _ = make_train_data(cfg)
@@ -271,20 +275,27 @@ def cpu_baseline(cfg, seconds, script_epoch=True):
     perm = O.epoch_order(len(users), torch.Generator().manual_seed(0))
     su, si, sy = users[perm], items[perm], labels[perm]
     threads_all = facts["nproc"]
-    out = {"unit": "interactions/s", "kind": "port", "cores": 16,
+    # thread sweep: the best count is `value` (and `cores`); a sweep point takes
+    # ~seconds / 2 of steps after one warm-up step
+    sweep = {}
+    for t in SWEEP_THREADS:
+        sweep[t] = _oracle_steps(cfg, U, I, batch, seconds / 2, t, su, si, sy)
+    best = max(sweep, key=lambda t: sweep[t]["value"])
+    out = {"unit": "interactions/s", "kind": "port", "cores": best,
            "sample": f"{cfg.upper()} step-only: {batch}-row Adam steps of the oracle NCF({U},{I},{f},{L}) on the "
-                     f"shuffled epoch stream, ~{seconds:.0f} s each at 16 threads (value) and at os.cpu_count() "
-                     f"threads; C2/C4-shape step-only and one script-equivalent epoch beside it",
+                     f"shuffled epoch stream, ~{seconds / 2:.0f} s at each of {list(SWEEP_THREADS)} torch threads "
+                     f"(value: the best, {best}) and at os.cpu_count() threads; C2/C4-shape step-only and one "
+                     f"script-equivalent epoch at the best count beside it",
            **facts}
-    r16 = _oracle_steps(cfg, U, I, batch, seconds, 16, su, si, sy)
-    out["value"] = r16["value"]
-    out["step_only_16_threads"] = r16
-    out["step_only_all_threads"] = _oracle_steps(cfg, U, I, batch, seconds, threads_all, su, si, sy)
-    out["c2_step_only_16_threads"] = _oracle_steps("c2", 6041, 3707, 1024, seconds / 3, 16)
-    out["c4_step_only_16_threads"] = _oracle_steps("c4", 138494, 26745, 65536, seconds / 3, 16)
+    out["value"] = sweep[best]["value"]
+    out["threads_best"] = best
+    out["thread_sweep"] = {str(t): r for t, r in sweep.items()}
+    out["step_only_all_threads"] = _oracle_steps(cfg, U, I, batch, seconds / 2, threads_all, su, si, sy)
+    out["c2_step_only"] = _oracle_steps("c2", 6041, 3707, 1024, seconds / 3, best)
+    out["c4_step_only"] = _oracle_steps("c4", 138494, 26745, 65536, seconds / 3, best)
     if script_epoch:
         from torch.utils.data import DataLoader
-        torch.set_num_threads(16)
+        torch.set_num_threads(best)
         torch.manual_seed(0)
         m = O.OracleNCF(U, I, f, L, 0.0, MODEL.get(cfg, "NeuMF-end"))
         opt = torch.optim.Adam(m.parameters(), lr=1e-3)
@@ -309,7 +320,7 @@ def cpu_baseline(cfg, seconds, script_epoch=True):
         t1 = time.perf_counter()
         out["script_epoch"] = {"seconds": t1 - t0, "interactions_per_s": len(users) / (t1 - t0),
                                "ng_sample_s": t_loop - t0, "train_loop_s": t_eval - t_loop, "metrics_s": t1 - t_eval,
-                               "batches": nb, "HR@10": float(np.mean(HR)), "threads": 16, "num_workers": 4}
+                               "batches": nb, "HR@10": float(np.mean(HR)), "threads": best, "num_workers": 4}
     out["ng_sample_s"] = t_sample
     return out
 
