@@ -76,6 +76,10 @@ typedef struct ncf_layout {
 #define NCF_LAYOUT_LAYERED 0x2      /* training steps on the layered path even where a fused kernel exists */
 #define NCF_LAYOUT_WG_SHIFT 8       /* bits 8..19: workgroups of the fused step (0 = ncf_slab_rows()) */
 #define NCF_LAYOUT_WG_MASK 0xfff
+#define NCF_LAYOUT_WG4 0x4          /* fused step on 4-wave workgroups (64-row tiles): small per-rank batches */
+#define NCF_LAYOUT_FACT_DEFER_DX 0x8 /* factored layer 0: the step forms only the dW0 partials and leaves the
+                                        per-entity sums G in grads' Um / Im rows (ncf_adam_step_fact expands them
+                                        per shard after the reduce-scatter); set by the caller, kept by tune */
 
 /* Device-resident step control block (16-byte aligned, 6 x int64).  Lets a
  * captured hipGraph replay consecutive batches with no host involvement. */
@@ -280,6 +284,23 @@ int ncf_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq
                   int64_t hist_len, void *stream);
 
 /*
+ * Sharded Adam of the factored path (data-parallel dp_mode "zero1" with
+ * NCF_LAYOUT_FACT_DEFER_DX; replaces optimizer.step(), train_neumf.py:90,115, on
+ * this rank's shard).  gshard holds the reduce-scattered flat gradient shard
+ * [shard_begin, shard_begin + n): in its Um / Im rows the summed per-entity D0 sums
+ * G (the step deferred their expansion), elsewhere the gradient itself.  The kernel
+ * forms dUm / dIm of its rows as G W0[:, half] (W0 read from params_full) and runs
+ * Adam on the active ranges (shard-relative) of params (= params_full + shard_begin);
+ * gshard is not cleared.  Fused path, factored layer 0 with dm <= 64 and
+ * shard_begin a multiple of 64: NCF_E_UNSUPPORTED otherwise.  Loss bookkeeping as
+ * ncf_adam_step (loss_slot shard-relative, or loss_hist NULL on the other ranks).
+ */
+int ncf_adam_step_fact(const ncf_layout *lay, const float *params_full, float *params, const float *gshard,
+                       float *exp_avg, float *exp_avg_sq, const int64_t *ranges, int nranges, int64_t shard_begin,
+                       ncf_step_ctl *ctl, double lr, double beta1, double beta2, double eps, int64_t loss_slot,
+                       float *loss_hist, int64_t hist_len, void *stream);
+
+/*
  * ncf_reduce_slab + ncf_adam_step in one launch (single-process training: no
  * gradient exchange between the two).  The tower/predict gradient is summed from
  * the slab in the same fixed order and applied by Adam in the same block, without
@@ -444,6 +465,10 @@ int ncf_hr_ndcg(const float *logits, const int32_t *items, int64_t n, int batch,
  * (1 = skip embedding scatter-add, 2 = skip weight-gradient MFMAs).  Results are
  * wrong while any switch is set; 0 restores the production kernel. */
 int ncf_debug_set_diag(int flags);
+/* Launch geometry of the fused step for later ncf_layout_tune calls: 0 = chosen by
+ * the batch size (4-wave workgroups for small per-rank batches), 4 or 8 = forced
+ * where that kernel exists (A/B measurements, tests).  NCF_E_ARG otherwise. */
+int ncf_debug_set_geometry(int waves);
 
 /* Diagnostics only: device buffer of ncf_slab_rows() x 64 uint64 that the next
  * ncf_train_step launches fill with per-workgroup s_memtime phase stamps

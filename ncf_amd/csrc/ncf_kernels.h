@@ -10,9 +10,12 @@ constexpr int TILE_ROWS = NWAVES * 16;
 constexpr int SLAB_ROWS = 256;  // one workgroup per CU on MI355X
 constexpr int LDS_LIMIT_BYTES = 160 * 1024;
 
-template <int F_, int L_, int MODE_>
+// NW_: waves per workgroup of the fused step (16 rows each per tile): NWAVES, or 4
+// for small per-rank batches (twice the workgroups, one wave per SIMD).
+template <int F_, int L_, int MODE_, int NW_ = NWAVES>
 struct Shape {
     static constexpr int F = F_, L = L_, MODE = MODE_;
+    static constexpr int NWV = NW_, NTH = NW_ * WAVE, TR = NW_ * 16;
     static constexpr bool GMF = MODE != NCF_MODEL_MLP;
     static constexpr bool MLP = MODE != NCF_MODEL_GMF;
     static constexpr int DM = F << (L - 1);
@@ -47,17 +50,17 @@ struct Shape {
     // partials per output) and the entries of their sum over the waves per thread.
     __host__ __device__ static constexpr int rwk(int k) { return S(k + 1) * S(k) + 4 * S(k + 1); }
     __host__ __device__ static constexpr int nek(int k) {
-        return (MLP && k >= 1) ? (S(k + 1) * S(k) + S(k + 1) + NWAVES * 64 - 1) / (NWAVES * 64) : 0;
+        return (MLP && k >= 1) ? (S(k + 1) * S(k) + S(k + 1) + NTH - 1) / NTH : 0;
     }
     // su[2], si[2], labels[2] (double-buffered tile indices), zgmf, dz, teacher
     // logits[2], then 128 floats of biases (each layer's padded to 16*MT) and 128 of
     // predict weights
-    static constexpr int MISC = 12 * TILE_ROWS;
+    static constexpr int MISC = 12 * TR;
     // Two halves per wave whose roles (layer-0 staging / scatter scratch) alternate
     // with tile parity: the next tile's staging never overwrites rows a slow wave
     // still reads, so there is no tile-end barrier (if the LDS budget allows).
     static constexpr int HALF0 = ST0 > SCR ? ST0 : SCR;
-    static constexpr bool ALT0_FITS = (W_TOTAL + MISC + NWAVES * 2 * HALF0) * 4 <= LDS_LIMIT_BYTES;
+    static constexpr bool ALT0_FITS = (W_TOTAL + MISC + NWV * 2 * HALF0) * 4 <= LDS_LIMIT_BYTES;
 #ifdef NCF_KEEP_END_BARRIER  // experiment switch: one region + tile-end barrier
     static constexpr bool ALT0 = false;
 #else
@@ -105,12 +108,18 @@ constexpr int DIAG_NO_ITEM_SCATTER = 16;  // diag build only: skip the Im segmen
 constexpr int DIAG_NO_GMF_SCATTER = 32;   // diag build only: skip the Ug / Ig atomics
 constexpr int DIAG_PREP_DIRECT = 4;  // ncf_prepare_epoch: global-atomic histogram variant (still correct)
 
+// Launch geometries of the fused step: GEO_8 = NWAVES-wave workgroups (128-row
+// tiles), GEO_4 = 4-wave workgroups (64-row tiles; NCF_LAYOUT_WG4).
+enum { GEO_8 = 0, GEO_4 = 1, NGEO = 2 };
+__host__ __device__ constexpr int geo_waves(int g) { return g == GEO_4 ? 4 : NWAVES; }
+
 struct KernelEntry {
     int mode, F, L;
-    const void* train;
-    const void* fwd;
-    const void* train_fact;  // factored layer 0 (MLP shapes; see ncf_train.hip), else nullptr
-    int w_total, misc, stage8;  // LDS floats
+    const void* train[NGEO];       // per geometry; nullptr where it has no instantiation
+    const void* fwd;               // GEO_8
+    const void* train_fact[NGEO];  // factored layer 0 (MLP shapes; see ncf_train.hip), else nullptr
+    int w_total;                   // LDS floats
+    int misc[NGEO], stage[NGEO];   // LDS floats per geometry
 };
 
 const KernelEntry* kernel_table(int* n);

@@ -273,6 +273,72 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
     record_loss(ctl, g, loss_slot, loss_hist, hist_len);
 }
 
+// Sharded Adam of the factored path (dp_mode "zero1" with NCF_LAYOUT_FACT_DEFER_DX):
+// the reduce-scattered gradient shard holds, in the Um / Im rows, the summed
+// per-entity D0 sums G (the train step expanded only the dW0 partials), so the
+// gradient of element (row, col) of table X is formed here, by the rank that owns
+// it, as  dX[row][col] = sum_j G[row][j] W0[j][koff + col]  (koff = 0 for Um, DM
+// for Im; the re-association of fact_expand_kernel's dX = G W0half) -- then Adam.
+// The shard is 64-float aligned and DM divides 64, so a G row never straddles two
+// shards.  g is not cleared (the next reduce-scatter overwrites the shard).
+struct FactShard {
+    const float* prm;      // full flat parameters (W0 rows)
+    int64_t um, im, nu, ni;  // table offsets and float counts (U * DM, I * DM)
+    int64_t w0, base;      // W0 offset; flat index of shard element 0
+    int dm;
+};
+
+__global__ __launch_bounds__(256) void adam_fact_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v, Ranges R,
+                                                        FactShard F, const ncf_step_ctl* ctl, double lr, double beta1,
+                                                        double beta2, float eps, int64_t loss_slot, float* loss_hist,
+                                                        int64_t hist_len, ScCache* scc) {
+#pragma clang fp contract(off)
+    __shared__ float sc[2];
+    const int64_t t_step = ctl->adam_t;
+    step_scalars(scc, t_step, lr, beta1, beta2, sc);
+    step_scalars_ahead(scc, t_step, lr, beta1, beta2);
+    __syncthreads();
+    const float neg_step = sc[0], bc2s = sc[1];
+    const float w1 = (float)(1.0 - beta1);
+    const float b2 = (float)beta2;
+    const float omb2 = (float)(1.0 - beta2);
+    const int64_t total = R.prefix[R.n];
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
+        int which;
+        const int64_t i = range_locate(R, q, &which);
+        const int64_t fi = F.base + i;
+        f4 gg;
+        const bool isu = fi >= F.um && fi < F.um + F.nu, isi = fi >= F.im && fi < F.im + F.ni;
+        if (isu || isi) {
+            const int64_t rel = fi - (isu ? F.um : F.im);
+            const int64_t row = rel / F.dm;
+            const int col = (int)(rel - row * F.dm);
+            const float* G = g + (i - col);  // the row's first float (same shard)
+            const float* W = F.prm + F.w0 + (isu ? 0 : F.dm) + col;
+            gg = f4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < F.dm; ++j) {
+                const float gj = G[j];
+                const f4 w = *reinterpret_cast<const f4*>(W + (int64_t)j * 2 * F.dm);
+                gg.x = fmaf(gj, w.x, gg.x);
+                gg.y = fmaf(gj, w.y, gg.y);
+                gg.z = fmaf(gj, w.z, gg.z);
+                gg.w = fmaf(gj, w.w, gg.w);
+            }
+        } else {
+            gg = *reinterpret_cast<const f4*>(g + i);
+        }
+        f4 mm = *reinterpret_cast<const f4*>(m + i);
+        f4 vv = *reinterpret_cast<const f4*>(v + i);
+        f4 pp = *reinterpret_cast<const f4*>(p + i);
+        adam_f4(pp, mm, vv, gg, w1, b2, omb2, bc2s, eps, neg_step);
+        *reinterpret_cast<f4*>(m + i) = mm;
+        *reinterpret_cast<f4*>(v + i) = vv;
+        *reinterpret_cast<f4*>(p + i) = pp;
+    }
+    record_loss(ctl, g, loss_slot, loss_hist, hist_len);
+}
+
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* __restrict__ g, Ranges R,
                                                   const ncf_step_ctl* ctl, float lr, int64_t loss_slot, float* loss_hist,
                                                   int64_t hist_len) {
@@ -1173,9 +1239,9 @@ static const KernelEntry* find_entry(int mode, int F, int L) {
     return nullptr;
 }
 
-static int64_t train_lds_floats(const KernelEntry* e, const ncf_layout* lay) {
+static int64_t train_lds_floats(const KernelEntry* e, const ncf_layout* lay, int geo = GEO_8) {
     const int64_t img = lay->tower_len + 1;
-    return e->w_total + e->misc + (e->stage8 > img ? e->stage8 : img);
+    return e->w_total + e->misc[geo] + (e->stage[geo] > img ? e->stage[geo] : img);
 }
 
 static Ranges make_ranges(const int64_t* ranges, int nranges, int* err) {
@@ -1200,6 +1266,10 @@ static Ranges make_ranges(const int64_t* ranges, int nranges, int* err) {
 
 static int g_diag = 0;
 static unsigned long long* g_stamps = nullptr;
+// ncf_debug_set_geometry: 0 = ncf_layout_tune decides, 4 / NWAVES = forced (A/B, tests)
+static int g_geo_waves = 0;
+// ncf_layout_tune: 4-wave workgroups up to this many rows per rank
+constexpr int64_t WG4_MAX_ROWS = 16384;
 
 static int launch_status() { return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH; }
 
@@ -1382,7 +1452,8 @@ struct FxShape {
 template <int DM>
 __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout lay, const float* __restrict__ prm,
                                                                      float* __restrict__ grads,
-                                                                     float* __restrict__ partials, int nbu) {
+                                                                     float* __restrict__ partials, int nbu,
+                                                                     int dw0_only) {
     using X_ = FxShape<DM>;
     constexpr int CH = X_::CH, ST = X_::ST, NT = X_::NT, Q4 = X_::Q4, TPW = X_::TPW, cpb = X_::CPB;
     extern __shared__ __attribute__((aligned(16))) float fsm[];
@@ -1460,6 +1531,9 @@ __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout l
             a0.x += a1.x; a0.y += a1.y; a0.z += a1.z; a0.w += a1.w;
             accw[q] = a0;
         }
+        // NCF_LAYOUT_FACT_DEFER_DX: G stays; the owner of each row expands it after the
+        // reduce-scatter (ncf_adam_step_fact)
+        if (dw0_only) continue;
         // dX = G W0h, tiles (rt, nt): A[i = row][k = j] = G[row][j],  B[k = j][n = k'] = W0h[j][k']
         for (int tt = w; tt < (CH / 16) * NT; tt += FX_WAVES) {
             const int rt = tt / NT, nt = tt - rt * NT;
@@ -1535,9 +1609,17 @@ static bool fact_mode(const ncf_layout* lay) {
     const int dm = fact_dm(lay);
     const bool lds_dm = dm == 8 || dm == 16 || dm == 32 || dm == 64 || dm == 128;  // fact_expand_kernel<DM>
     const KernelEntry* e = train_fused(lay);
-    if (e) return lds_dm && e->train_fact != nullptr;
+    if (e) return lds_dm && e->train_fact[GEO_8] != nullptr;
     // layered path: wider dm (256, 512) expanded with GEMMs (ncf_layered.hip lyr_fact_dx / dw0)
     return (lds_dm || dm == 256 || dm == FACT_MAX_DM) && lay->factor_num <= LYR_MAX_FACTOR;
+}
+
+// Launch geometry of the fused training step: 4-wave workgroups where
+// ncf_layout_tune asked for them (NCF_LAYOUT_WG4) and the kernel exists.
+static int train_geo(const KernelEntry* e, const ncf_layout* lay) {
+    if (!(lay->flags & NCF_LAYOUT_WG4)) return GEO_8;
+    const void* fn = fact_mode(lay) ? e->train_fact[GEO_4] : e->train[GEO_4];
+    return fn != nullptr ? GEO_4 : GEO_8;
 }
 
 // Workgroups of the fused step = rows of the slab the reductions read.
@@ -1608,8 +1690,9 @@ static int launch_fact_expand(const ncf_layout* lay, const float* params, float*
     ncf_layout l = *lay;
     int nbu;
     int nblk = fact_blocks(lay, &nbu);
+    int dw0_only = (lay->flags & NCF_LAYOUT_FACT_DEFER_DX) ? 1 : 0;
     if (ensure_lds(fe, lds) != NCF_OK) return NCF_E_LAUNCH;
-    void* ae[] = {&l, (void*)&params, (void*)&grads, (void*)&partials, &nbu};
+    void* ae[] = {&l, (void*)&params, (void*)&grads, (void*)&partials, &nbu, &dw0_only};
     if (hipLaunchKernel(fe, dim3((unsigned)nblk), dim3(FX_WAVES * 64), ae, (size_t)lds, st) != hipSuccess)
         return NCF_E_LAUNCH;
     return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
@@ -1649,11 +1732,25 @@ int64_t ncf_fact_partials_bytes(const ncf_layout* lay) {
 
 int ncf_layout_tune(ncf_layout* lay, int64_t rows) {
     if (!lay || rows <= 0) return NCF_E_ARG;
-    int32_t f = lay->flags & ~(NCF_LAYOUT_PER_ROW_L0 | (NCF_LAYOUT_WG_MASK << NCF_LAYOUT_WG_SHIFT));
-    const int64_t tiles = (rows + TILE_ROWS - 1) / TILE_ROWS;
-    if (tiles < SLAB_ROWS) f |= (int32_t)tiles << NCF_LAYOUT_WG_SHIFT;
+    int32_t f = lay->flags & ~(NCF_LAYOUT_PER_ROW_L0 | NCF_LAYOUT_WG4 | (NCF_LAYOUT_WG_MASK << NCF_LAYOUT_WG_SHIFT));
     if (2 * rows < (int64_t)lay->user_num + lay->item_num) f |= NCF_LAYOUT_PER_ROW_L0;
+    // small per-rank batches: 4-wave workgroups on 64-row tiles (twice the workgroups
+    // of the 128-row tiling, one wave per SIMD, half the waves per barrier and sum)
+    const bool wg4 = g_geo_waves == 4 || (g_geo_waves == 0 && rows <= WG4_MAX_ROWS);
+    if (wg4) f |= NCF_LAYOUT_WG4;
     lay->flags = f;
+    const KernelEntry* e = train_fused(lay);
+    if (wg4 && (!e || train_geo(e, lay) != GEO_4)) f &= ~NCF_LAYOUT_WG4;  // no 4-wave kernel for this shape
+    const int tr = 16 * ((f & NCF_LAYOUT_WG4) ? geo_waves(GEO_4) : geo_waves(GEO_8));
+    const int64_t tiles = (rows + tr - 1) / tr;
+    if (tiles < SLAB_ROWS) f |= (int32_t)tiles << NCF_LAYOUT_WG_SHIFT;
+    lay->flags = f;
+    return NCF_OK;
+}
+
+int ncf_debug_set_geometry(int waves) {
+    if (waves != 0 && waves != 4 && waves != NWAVES) return NCF_E_ARG;
+    g_geo_waves = waves;
     return NCF_OK;
 }
 
@@ -1744,9 +1841,10 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
         if (rc != NCF_OK || la.fact_part_floats < 0) return rc;
         return launch_fact_expand(lay, params, grads, fact_partials(lay, workspace), (hipStream_t)stream);
     }
-    const int64_t lds = train_lds_floats(e, lay) * 4;
+    const int geo = train_geo(e, lay);
+    const int64_t lds = train_lds_floats(e, lay, geo) * 4;
     if (lds > LDS_LIMIT_BYTES) return NCF_E_UNSUPPORTED;
-    const void* fn = fact_mode(lay) ? e->train_fact : e->train;
+    const void* fn = fact_mode(lay) ? e->train_fact[geo] : e->train[geo];
     if (ensure_lds(fn, lds) != NCF_OK) return NCF_E_LAUNCH;
     TrainArgs a;
     memset(&a, 0, sizeof(a));
@@ -1769,8 +1867,8 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
     a.slab = slab;
     a.logits_out = logits_out;
     void* args[] = {&a};
-    if (hipLaunchKernel(fn, dim3(slab_rows_of(lay)), dim3(NTHREADS), args, (size_t)lds, (hipStream_t)stream) !=
-        hipSuccess)
+    if (hipLaunchKernel(fn, dim3(slab_rows_of(lay)), dim3(geo_waves(geo) * WAVE), args, (size_t)lds,
+                        (hipStream_t)stream) != hipSuccess)
         return NCF_E_LAUNCH;
     const int rc = launch_status();
     if (rc != NCF_OK || !fact_mode(lay)) return rc;
@@ -1855,7 +1953,7 @@ int ncf_forward(const ncf_layout* lay, const float* params, const uint64_t* rows
         la.fact_part_floats = -1;
         return lyr_run(la, static_cast<float*>(workspace), n, false, (hipStream_t)stream);
     }
-    const int64_t lds = (int64_t)(e->w_total + e->misc) * 4;
+    const int64_t lds = (int64_t)(e->w_total + e->misc[GEO_8]) * 4;
     if (lds > LDS_LIMIT_BYTES) return NCF_E_UNSUPPORTED;
     if (ensure_lds(e->fwd, lds) != NCF_OK) return NCF_E_LAUNCH;
     TrainArgs a;
@@ -1901,6 +1999,35 @@ int ncf_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(adam_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
                        exp_avg_sq, R, ctl, lr, beta1, beta2, (float)eps, loss_slot, loss_hist, hist_len,
+                       sc_cache_for(ctl, stream));
+    return launch_status();
+}
+
+int ncf_adam_step_fact(const ncf_layout* lay, const float* params_full, float* params, const float* gshard,
+                       float* exp_avg, float* exp_avg_sq, const int64_t* ranges, int nranges, int64_t shard_begin,
+                       ncf_step_ctl* ctl, double lr, double beta1, double beta2, double eps, int64_t loss_slot,
+                       float* loss_hist, int64_t hist_len, void* stream) {
+    if (!lay || !params_full || !params || !gshard || !exp_avg || !exp_avg_sq || !ranges || !ctl) return NCF_E_ARG;
+    const int dm = fact_dm(lay);
+    if (!fact_mode(lay) || dm > 64 || (shard_begin & 63)) return NCF_E_UNSUPPORTED;
+    int err = 0;
+    Ranges R = make_ranges(ranges, nranges, &err);
+    if (err) return NCF_E_ARG;
+    FactShard F;
+    F.prm = params_full;
+    F.um = lay->um;
+    F.im = lay->im;
+    F.nu = (int64_t)lay->user_num * dm;
+    F.ni = (int64_t)lay->item_num * dm;
+    F.w0 = lay->w[0];
+    F.base = shard_begin;
+    F.dm = dm;
+    const int64_t total = R.prefix[R.n];
+    int64_t grid = (total + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(adam_fact_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, params, gshard, exp_avg,
+                       exp_avg_sq, R, F, ctl, lr, beta1, beta2, (float)eps, loss_slot, loss_hist, hist_len,
                        sc_cache_for(ctl, stream));
     return launch_status();
 }

@@ -88,26 +88,28 @@ __device__ __forceinline__ void set_r(f4& v, int r, float x) {
 // fact_expand_kernel (ncf_ops.hip) turns those sums into dUm, dIm, dW0 with
 // (U + I) / 16 tile GEMMs instead of B / 16.  Every wave then touches only its own
 // rows of LDS after the weight prologue, so tiles need no workgroup barrier.
-template <int F, int L, int MODE, bool FWD_ONLY, bool FACT>
-__global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
-    using S_ = Shape<F, L, MODE>;
+template <int F, int L, int MODE, bool FWD_ONLY, bool FACT, int NW>
+__global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
+    using S_ = Shape<F, L, MODE, NW>;
+    // workgroup geometry: NW waves, 16 rows each, per tile (NW = 8, or 4 for small batches)
+    constexpr int NWV = S_::NWV, NTH = S_::NTH, TRW = S_::TR;
     static_assert(!FACT || S_::MLP, "factored layer 0 needs the MLP tower");
-    static_assert(!S_::MLP || S_::KT(0) <= NWAVES, "layer-0 wgrad: one 16-column block per wave");
+    static_assert(!S_::MLP || FACT || FWD_ONLY || S_::KT(0) <= NWV, "layer-0 wgrad: one 16-column block per wave");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* sW = smem;
-    int* su2 = reinterpret_cast<int*>(smem + S_::W_TOTAL);  // [2][TILE_ROWS] user ids (-1 = padding row)
-    int* si2 = su2 + 2 * TILE_ROWS;                         // [2][TILE_ROWS] item ids
-    float* slab2 = reinterpret_cast<float*>(si2 + 2 * TILE_ROWS);  // [2][TILE_ROWS] labels / dlogits
-    float* szg = slab2 + 2 * TILE_ROWS;  // GMF part of the logit, per tile row
-    float* sdz = szg + TILE_ROWS;        // dlogit, per tile row
-    float* stl2 = sdz + TILE_ROWS;       // [2][TILE_ROWS] NCF_DZ_KD: teacher logits
-    float* sB = stl2 + 2 * TILE_ROWS;    // biases, layer k at boff(k), zero-padded
+    int* su2 = reinterpret_cast<int*>(smem + S_::W_TOTAL);  // [2][TRW] user ids (-1 = padding row)
+    int* si2 = su2 + 2 * TRW;                         // [2][TRW] item ids
+    float* slab2 = reinterpret_cast<float*>(si2 + 2 * TRW);  // [2][TRW] labels / dlogits
+    float* szg = slab2 + 2 * TRW;  // GMF part of the logit, per tile row
+    float* sdz = szg + TRW;        // dlogit, per tile row
+    float* stl2 = sdz + TRW;       // [2][TRW] NCF_DZ_KD: teacher logits
+    float* sB = stl2 + 2 * TRW;    // biases, layer k at boff(k), zero-padded
     float* sWP = sB + 128;               // predict weights, zero-padded
     float* sstage = sWP + 128;           // union: per-wave staging | epilogue images
 
     const int tid = threadIdx.x;
     const int w = tid >> 6;
-    const bool wv_hi = __builtin_amdgcn_readfirstlane(w) >= NWAVES / 2;  // wave-uniform (scalar branch)
+    const bool wv_hi = __builtin_amdgcn_readfirstlane(w) >= NWV / 2;  // wave-uniform (scalar branch)
     const int l0 = tid & 63;
     const int c0 = l0 & 15;
     const int g0 = l0 >> 4;
@@ -116,22 +118,22 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 
     // Tower weight / bias loads first: they depend on nothing, so they fly while
     // the control block and the row indices make their round trips.
-    constexpr int PERMAX = S_::MLP ? (16 * S_::MT(0) * (S_::S(0) / 4) + NTHREADS - 1) / NTHREADS : 1;
+    constexpr int PERMAX = S_::MLP ? (16 * S_::MT(0) * (S_::S(0) / 4) + NTH - 1) / NTH : 1;
     f4 wreg[L][PERMAX];
     float breg[L];
     if constexpr (S_::MLP) {
         static_for<L>([&](auto kk) {
             constexpr int k = decltype(kk)::value;
             constexpr int rows = 16 * S_::MT(k), cols4 = S_::S(k) / 4, outs = S_::S(k + 1);
-            constexpr int PER = (rows * cols4 + NTHREADS - 1) / NTHREADS;
+            constexpr int PER = (rows * cols4 + NTH - 1) / NTH;
             const f4* Wg = reinterpret_cast<const f4*>(prm + lay.w[k]);
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
-                const int e = tid + q * NTHREADS;
+                const int e = tid + q * NTH;
                 const int o = e / cols4;
                 wreg[k][q] = (e < rows * cols4 && o < outs) ? Wg[e] : f4{0.f, 0.f, 0.f, 0.f};
             }
-            breg[k] = tid < outs ? prm[lay.b[k] + tid] : 0.f;  // 16 * MT(k) <= 128 < NTHREADS
+            breg[k] = tid < outs ? prm[lay.b[k] + tid] : 0.f;  // 16 * MT(k) <= 128 < NTH
         });
     }
 
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
             a.ctl->snap_t = a.ctl->adam_t + 1;
         }
     }
-    const int64_t ntiles = (nloc + TILE_ROWS - 1) / TILE_ROWS;
+    const int64_t ntiles = (nloc + TRW - 1) / TRW;
     stamp(a, 0);
 
     // Row prefetch: every thread issues the same loads (clamped row), so the
@@ -207,8 +209,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
             }
         }
     };
-    if ((int64_t)blockIdx.x < ntiles) load_idx((int64_t)blockIdx.x * TILE_ROWS);
-    if constexpr (FACT && !FWD_ONLY) load_idx2(((int64_t)blockIdx.x + gridDim.x) * TILE_ROWS);
+    if ((int64_t)blockIdx.x < ntiles) load_idx((int64_t)blockIdx.x * TRW);
+    if constexpr (FACT && !FWD_ONLY) load_idx2(((int64_t)blockIdx.x + gridDim.x) * TRW);
 
     // ---- tower weights, biases, predict weights -> LDS (zero-padded) ---------
     if constexpr (S_::MLP) {
@@ -217,18 +219,18 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         static_for<L>([&](auto kk) {
             constexpr int k = decltype(kk)::value;
             constexpr int rows = 16 * S_::MT(k), cols4 = S_::S(k) / 4;
-            constexpr int PER = (rows * cols4 + NTHREADS - 1) / NTHREADS;
+            constexpr int PER = (rows * cols4 + NTH - 1) / NTH;
             float* Ws = sW + S_::woff(k);
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
-                const int e = tid + q * NTHREADS;
+                const int e = tid + q * NTH;
                 const int o = e / cols4, i4 = e - o * cols4;
                 if (e < rows * cols4) *reinterpret_cast<f4*>(Ws + o * S_::SW(k) + 4 * i4) = wreg[k][q];
             }
             if (tid < 16 * S_::MT(k)) sB[S_::boff(k) + tid] = breg[k];
         });
     }
-    for (int e = tid; e < 128; e += NTHREADS) sWP[e] = e < S_::P ? prm[lay.wp + e] : 0.f;
+    for (int e = tid; e < 128; e += NTH) sWP[e] = e < S_::P ? prm[lay.wp + e] : 0.f;
 
     // ---- per-lane persistent accumulators ----------------------------------
     constexpr int MT0 = S_::MLP ? S_::MT(0) : 1;
@@ -399,11 +401,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
     int titer = 0;
 
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t row0 = tile * TILE_ROWS;
+        const int64_t row0 = tile * TRW;
         const int buf = titer & 1;
-        const int* su = su2 + buf * TILE_ROWS;
-        const int* si = si2 + buf * TILE_ROWS;
-        const float* slab_ = slab2 + buf * TILE_ROWS;
+        const int* su = su2 + buf * TRW;
+        const int* si = si2 + buf * TRW;
+        const float* slab_ = slab2 + buf * TRW;
         const bool has_next = tile + gridDim.x < ntiles;
         const int sb = 2 + 14 * titer;  // stamp base of this tile
         stamp(a, sb + 0);
@@ -417,9 +419,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 
         // (a) next tile's indices
         if constexpr (EARLY) {
-            load_idx2(row0 + 2 * (int64_t)gridDim.x * TILE_ROWS);
+            load_idx2(row0 + 2 * (int64_t)gridDim.x * TRW);
         } else {
-            load_idx(row0 + (int64_t)gridDim.x * TILE_ROWS);
+            load_idx(row0 + (int64_t)gridDim.x * TRW);
             nok = nok && has_next;
         }
 
@@ -473,9 +475,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         }
         stamp(a, sb + 1);
         if constexpr (EARLY) {
-            publish((buf ^ 1) * TILE_ROWS);
+            publish((buf ^ 1) * TRW);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // same-wave LDS hand-off
-            load_mlp(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g);
+            load_mlp(su2 + (buf ^ 1) * TRW, si2 + (buf ^ 1) * TRW, c, g);
         }
 
         // predict
@@ -501,15 +503,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 
         if constexpr (FWD_ONLY) {
             if (g == 0 && valid) a.logits_out[base + row0 + myq] = z;
-            publish((buf ^ 1) * TILE_ROWS);
+            publish((buf ^ 1) * TRW);
             lds_barrier();
-            load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
+            load_emb(su2 + (buf ^ 1) * TRW, si2 + (buf ^ 1) * TRW, c, g, l);
             ++titer;
             continue;
         } else {
             // (d) layer-0 wgrad operand: X0 rows of the whole tile, columns 16*nt + c
             constexpr int DM = S_::DM;
-            float bx[S_::MLP && !FACT ? NWAVES * 4 : 1];
+            float bx[S_::MLP && !FACT ? NWV * 4 : 1];
             const int nt0 = w < KT0 ? w : KT0 - 1;
             if constexpr (S_::MLP && !FACT) {
                 const int fj = 16 * nt0 + c;
@@ -517,7 +519,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                 const int64_t tab = isu ? lay.um + fj : lay.im + (fj - DM);
                 const int* ids = isu ? su : si;
 #pragma unroll
-                for (int ws = 0; ws < NWAVES; ++ws) {
+                for (int ws = 0; ws < NWV; ++ws) {
 #pragma unroll
                     for (int s = 0; s < 4; ++s) {
                         const int id = max(ids[ws * 16 + 4 * g + s], 0);
@@ -539,7 +541,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                     // distillation (base.py:40-50; response term: kd_response)
                     const float y = slab_[myq];
                     float rl;
-                    const float rg = kd_response(z, stl2[buf * TILE_ROWS + myq], a.kd_temp, &rl);
+                    const float rg = kd_response(z, stl2[buf * TRW + myq], a.kd_temp, &rl);
                     dz = (a.kd_wt * (sigmoidf_(z) - y) + a.kd_wr * rg) / gb_f;
                     if (g == 0) lossAcc += a.kd_wt * bce_loss(z, y) + a.kd_wr * rl;
                 } else {
@@ -564,7 +566,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                     if (!DIAG_ON(a, DIAG_NO_GMF_SCATTER)) atomicAdd(a.grads + lay.ug + (int64_t)max(su[q], 0) * F + gf, dgm * igv[j]);
                     gIg[j] = dgm * ugv[j];
                 }
-                if constexpr (EARLY) load_gmf(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, l);
+                if constexpr (EARLY) load_gmf(su2 + (buf ^ 1) * TRW, si2 + (buf ^ 1) * TRW, l);
             }
             stamp(a, sb + 2);
 
@@ -716,7 +718,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
                         for (int mt = 0; mt < S_::MT(0); ++mt)
                             *reinterpret_cast<f4*>(st + c * S_::SD(0) + 16 * mt + 4 * g) = D[0][mt];
-                        publish((buf ^ 1) * TILE_ROWS);
+                        publish((buf ^ 1) * TRW);
                         lds_barrier();
                         stamp(a, sb + 3 + 3 * (L - 1));
                         // bias grad: this wave's 16 rows, lane = output feature
@@ -734,7 +736,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                             for (int mt = 0; mt < MT0; ++mt) {
                                 f4 acc0 = accW0[mt], acc1 = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                                for (int ws = 0; ws < NWAVES; ++ws) {
+                                for (int ws = 0; ws < NWV; ++ws) {
                                     const float* sto = sstage + ws * S_::WAVE_STAGE + RK0;
 #pragma unroll
                                     for (int s = 0; s < 4; ++s) {
@@ -760,7 +762,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                         if (!S_::WGRAD0_LATE || wv_hi) wgrad0();
                         // (h) next tile's embedding fragments: before this tile's
                         // scatter atomics, so the next tile waits on them only
-                        load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
+                        load_emb(su2 + (buf ^ 1) * TRW, si2 + (buf ^ 1) * TRW, c, g, l);
                         const float* Ws = sW + S_::woff(0);
                         // orientation B: C[i = row 4g+r][j = in-feature 16*nt + c]
                         f4 acc[KT0];
@@ -786,7 +788,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                         // drain the atomics too.
                         if (S_::WGRAD0_LATE && !wv_hi) {
 #pragma unroll
-                            for (int i = 0; i < NWAVES * 4; ++i) asm volatile("" ::"v"(bx[i]));
+                            for (int i = 0; i < NWV * 4; ++i) asm volatile("" ::"v"(bx[i]));
                         }
                         stamp(a, sb + 4 + 3 * (L - 1));
                         // item half -> this wave's scratch rows (segment-reduced below);
@@ -851,9 +853,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
             } else {
                 // GMF-only model: item-side GMF rows, then publish next indices
                 item_segments(sstage + w * S_::WAVE_STAGE, a, su, si, wr, l, gIg, gf, gq0);
-                publish((buf ^ 1) * TILE_ROWS);
+                publish((buf ^ 1) * TRW);
                 lds_barrier();
-                load_emb(su2 + (buf ^ 1) * TILE_ROWS, si2 + (buf ^ 1) * TILE_ROWS, c, g, l);
+                load_emb(su2 + (buf ^ 1) * TRW, si2 + (buf ^ 1) * TRW, c, g, l);
             }
             // Tile end: no barrier unless the staging layout needs one (END_BARRIER):
             // the next tile's first cross-wave staging goes to the other region and
@@ -894,7 +896,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
         // the tail rides with the last layer's round where both images fit
         constexpr bool TAIL_MERGED = S_::MLP && L >= 2 && S_::rwk(L - 1) + NT <= S_::WAVE_STAGE;
         constexpr int TOFF = TAIL_MERGED ? S_::rwk(L - 1) : 0;
-        static_assert(TOFF + NT <= S_::WAVE_STAGE && NT <= NTHREADS, "epilogue tail image");
+        static_assert(TOFF + NT <= S_::WAVE_STAGE && NT <= NTH, "epilogue tail image");
         float tw[MTL][4];  // predict-weight partials summed over the wave's rows (lanes c == 0)
         if constexpr (S_::MLP) {
 #pragma unroll
@@ -943,7 +945,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
             if (tid < NT) {
                 float ts = 0.f;
 #pragma unroll
-                for (int ws = 0; ws < NWAVES; ++ws) ts += sstage[ws * S_::WAVE_STAGE + TOFF + tid];
+                for (int ws = 0; ws < NWV; ++ws) ts += sstage[ws * S_::WAVE_STAGE + TOFF + tid];
                 const int64_t pos = tid < S1 ? (lay.b[0] - tb) + tid
                                   : tid < S1 + S_::P ? (lay.wp - tb) + (tid - S1)
                                   : tid == S1 + S_::P ? (lay.bp - tb) : (int64_t)lay.tower_len;
@@ -983,16 +985,16 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
                     lds_barrier();
 #pragma unroll
                     for (int j = 0; j < S_::nek(k); ++j) {
-                        const int e = tid + j * NTHREADS;
+                        const int e = tid + j * NTH;
                         if (e < SO * SK) {
                             float s = 0.f;
 #pragma unroll
-                            for (int ws = 0; ws < NWAVES; ++ws) s += sstage[ws * S_::WAVE_STAGE + e];
+                            for (int ws = 0; ws < NWV; ++ws) s += sstage[ws * S_::WAVE_STAGE + e];
                             out[(lay.w[k] - tb) + e] = s;
                         } else if (e < SO * SK + SO) {
                             float s = 0.f;
 #pragma unroll
-                            for (int ws = 0; ws < NWAVES; ++ws)
+                            for (int ws = 0; ws < NWV; ++ws)
 #pragma unroll
                                 for (int gg = 0; gg < 4; ++gg) s += sstage[ws * S_::WAVE_STAGE + SO * SK + gg * SO + (e - SO * SK)];
                             out[(lay.b[k] - tb) + (e - SO * SK)] = s;
@@ -1038,19 +1040,30 @@ __global__ __launch_bounds__(NTHREADS, 2) void ncf_step_kernel(TrainArgs a) {
 template <int F, int L, int MODE>
 static KernelEntry make_entry() {
     using S_ = Shape<F, L, MODE>;
+    using S4 = Shape<F, L, MODE, 4>;
     KernelEntry e;
     e.mode = MODE;
     e.F = F;
     e.L = L;
-    e.train = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, false>);
-    e.fwd = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, true, false>);
-    if constexpr (S_::MLP)
-        e.train_fact = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, true>);
+    e.train[GEO_8] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, false, NWAVES>);
+    // 4-wave workgroups: the per-row layer-0 wgrad gives each wave one 16-column block
+    // of dW0, so KT(0) <= 4 there; the factored kernel has no such limit
+    if constexpr (!S_::MLP || S_::KT(0) <= 4)
+        e.train[GEO_4] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, false, 4>);
     else
-        e.train_fact = nullptr;
+        e.train[GEO_4] = nullptr;
+    e.fwd = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, true, false, NWAVES>);
+    if constexpr (S_::MLP) {
+        e.train_fact[GEO_8] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, true, NWAVES>);
+        e.train_fact[GEO_4] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, true, 4>);
+    } else {
+        e.train_fact[GEO_8] = e.train_fact[GEO_4] = nullptr;
+    }
     e.w_total = S_::W_TOTAL;
-    e.misc = S_::MISC;
-    e.stage8 = NWAVES * S_::WAVE_STAGE;
+    e.misc[GEO_8] = S_::MISC;
+    e.misc[GEO_4] = S4::MISC;
+    e.stage[GEO_8] = NWAVES * S_::WAVE_STAGE;
+    e.stage[GEO_4] = 4 * S4::WAVE_STAGE;
     return e;
 }
 

@@ -120,6 +120,7 @@ class TrainEngine:
                 r, S = self.rank, self.shard
                 self.exp_avg = self.exp_avg[r * S:(r + 1) * S].clone()
                 self.exp_avg_sq = self.exp_avg_sq[r * S:(r + 1) * S].clone()
+            self._set_fact_shard()
             self._drop_graphs()
 
     def __init__(self, model, lr=1e-3, optimizer="adam", betas=(0.9, 0.999), eps=1e-8,
@@ -171,6 +172,7 @@ class TrainEngine:
             raise ValueError(optimizer)
         self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
         self.ws = None  # ncf_train_step workspace, sized by set_epoch_stream
+        self._fact_shard = False  # zero1: the factored expansion sharded into the optimizer (_set_fact_shard)
         self.ctl = ops.new_ctl(0, dev)
         rng = _active_ranges(model, self.lay, None if distill is None else distill.active_extra)
         self._ranges = (ctypes.c_int64 * (2 * len(rng)))(*[x for r in rng for x in r])
@@ -254,11 +256,17 @@ class TrainEngine:
         if self.batch_size != batch_size or self.ws is None:
             self._drop_graphs()
             per = (int(batch_size) + self.world_size - 1) // self.world_size
-            # launch shape for this batch size: workgroups = its 128-row tiles (up to
-            # one per CU), per-row layer 0 for batches small against the tables
+            # launch shape for this batch size: workgroups = its 128-row tiles (64-row
+            # tiles of 4-wave workgroups for small per-rank batches; up to one per CU),
+            # per-row layer 0 for batches small against the tables.  NCF_WG_WAVES=4|8
+            # forces the workgroup geometry (A/B measurements).
+            wg = os.environ.get("NCF_WG_WAVES")
+            if wg:
+                L.check(L.hip().ncf_debug_set_geometry(int(wg)), "ncf_debug_set_geometry")
             L.check(L.hip().ncf_layout_tune(ctypes.byref(self.lay), per), "ncf_layout_tune")
             if os.environ.get("NCF_FORCE_LAYERED", "0") == "1":  # A/B: the layered path for any shape
                 self.lay.flags |= L.LAYOUT_LAYERED
+            self._set_fact_shard()
             self.ws = ops.new_workspace(self.lay, per, self.device)
         self.batch_size = int(batch_size)
         if self.num_batches > self.loss_hist.numel():
@@ -311,6 +319,25 @@ class TrainEngine:
             # the frozen teacher's logit for every row of the epoch stream (one
             # forward launch per epoch instead of one no_grad forward per step)
             self.distill.teacher_logits(rows)
+
+    def _set_fact_shard(self):
+        """zero1 on the factored fused path (dm <= 64, Adam): the step forms only the
+        dW0 partials (NCF_LAYOUT_FACT_DEFER_DX) and each rank expands the summed G rows
+        of its own shard inside its Adam launch (ncf_adam_step_fact) -- the expansion
+        and the optimizer sharded together, 1/W of each per rank.  NCF_FACT_SHARD=0
+        keeps the full expansion before the reduce-scatter (A/B)."""
+        lay, m = self.lay, self.model
+        self._fact_shard = bool(
+            self.dp_mode == "zero1" and self.optimizer == "adam" and self.distill is None
+            and os.environ.get("NCF_FACT_SHARD", "1") == "1"
+            and not (lay.flags & L.LAYOUT_LAYERED) and lay.dropout == 0.0
+            and L.supported(m.model_type, m.factor_num, m.num_layers) == L.PATH_FUSED
+            and (m.factor_num << (m.num_layers - 1)) <= 64
+            and L.hip().ncf_fact_mode(ctypes.byref(lay)) == 1)
+        if self._fact_shard:
+            lay.flags |= L.LAYOUT_FACT_DEFER_DX
+        else:
+            lay.flags &= ~L.LAYOUT_FACT_DEFER_DX
 
     def _order_buf(self, rows):
         """The user-order buffer that goes with epoch-stream buffer `rows`."""
@@ -464,7 +491,12 @@ class TrainEngine:
             ranges, nr = self._ranges, self._nranges
             hist = self.loss_hist.data_ptr()
         p, g = self._opt_ptrs
-        if self.optimizer == "adam":
+        if self._fact_shard:  # the shard's G rows expanded inside the optimizer launch
+            L.check(lib.ncf_adam_step_fact(ctypes.byref(self.lay), self.flat.data_ptr(), p, g, self.exp_avg.data_ptr(),
+                                           self.exp_avg_sq.data_ptr(), ranges, nr, self.rank * self.shard,
+                                           self.ctl.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps,
+                                           self._loss_slot, hist, hist_len, st), "ncf_adam_step_fact")
+        elif self.optimizer == "adam":
             L.check(lib.ncf_adam_step(p, g, self.exp_avg.data_ptr(),
                                       self.exp_avg_sq.data_ptr(), ranges, nr,
                                       self.ctl.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps,

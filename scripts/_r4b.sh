@@ -1,0 +1,16 @@
+set -u
+cd $GRAFT_REPO_ROOT
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4b_smoke.log 2>&1 || exit 1
+timeout -k 10 800 python -u -m pytest -x -v --timeout 500 --timeout-method thread -p no:cacheprovider \
+  tests/test_gpu_parity.py -k "geometry_vs_oracle or tuned_launch" > gpurun_out/r4b_tests1.log 2>&1 || exit 1
+timeout -k 10 800 python -u -m pytest -x -v --timeout 500 --timeout-method thread -p no:cacheprovider \
+  tests/test_gpu_multirank_fullsize.py tests/test_gpu_multirank.py::test_two_ranks_match_single_rank \
+  tests/test_gpu_trainer.py::test_trainer_matches_reference_script tests/test_gpu_lazy_adam.py > gpurun_out/r4b_tests2.log 2>&1 || exit 1
+for w in 8 4; do
+  NCF_WG_WAVES=$w timeout -k 10 200 python scripts/dp_modes.py c3 8 allreduce,zero1 > gpurun_out/r4b_dp_c3_w$w.json 2>&1 || exit 1
+  NCF_WG_WAVES=$w timeout -k 10 200 python bench.py --config c2 --steps 2000 --warmup 200 --skip-cpu-baseline --e2e-epochs 0 > gpurun_out/r4b_c2_w$w.json 2>&1 || exit 1
+done
+for a in "c2 1024" "c3 8192"; do NCF_WG_WAVES=8 timeout -k 10 120 python scripts/stamps.py $a >> gpurun_out/r4b_stamps.jsonl 2>>gpurun_out/r4b_stamps.err || exit 1; done
+echo DONE

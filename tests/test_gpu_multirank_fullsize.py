@@ -68,6 +68,8 @@ def _c3_run(world, rank, group):
     torch.cuda.synchronize()
     eng = tr.engine
     losses = eng.epoch_losses()[:eng.num_batches].astype(np.float64).copy()
+    if eng.dp_mode == "zero1":
+        assert eng._fact_shard  # the sharded factored expansion ran
     return _flat(model), losses, eng.dp_mode
 
 
@@ -106,9 +108,11 @@ def _c4_run(world, rank, group):
 RUNS = {"c3": _c3_run, "c4": _c4_run}
 
 
-def _worker(rank, world, port, name, q):
+def _worker(rank, world, port, name, q, dp_mode=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    if dp_mode is not None:  # TrainEngine's default exchange for world > 1 (Trainer takes none)
+        os.environ["NCF_DP_MODE"] = dp_mode
     # the ranks share the box's CPUs: one sampler pool each, sized for the group
     os.environ.setdefault("LOCAL_WORLD_SIZE", str(world))
     import torch.distributed as dist
@@ -131,11 +135,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _spawn(name, world):
+def _spawn(name, world, dp_mode=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, q, dp_mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -183,15 +187,19 @@ def _oracle_losses(name, steps):
                                     [labels[s] for s in sl]), dtype=np.float64)
 
 
-@pytest.mark.parametrize("name,world", [("c3", 2), ("c3", 4), ("c4", 2)])
-def test_full_shape_ranks_match_single_rank_and_oracle(name, world):
-    res = _spawn(name, world)
+@pytest.mark.parametrize("name,world,dp_mode", [("c3", 2, None), ("c3", 4, None), ("c4", 2, None),
+                                                 ("c3", 4, "zero1")])
+def test_full_shape_ranks_match_single_rank_and_oracle(name, world, dp_mode):
+    """dp_mode None: the default ("auto"); "zero1" at C3: reduce-scatter, each rank
+    expands the factored layer 0 of its own shard inside its Adam launch
+    (ncf_adam_step_fact), all-gather."""
+    res = _spawn(name, world, dp_mode)
     flat0, loss0, mode0 = res[0]
     for r in range(1, world):
         assert np.array_equal(res[r][1], loss0), f"rank {r} losses differ from rank 0"
         assert np.array_equal(res[r][0], flat0), f"rank {r} parameters differ from rank 0"
         assert res[r][2] == mode0
-    assert mode0 == {"c3": "allreduce", "c4": "touched"}[name], mode0
+    assert mode0 == (dp_mode or {"c3": "allreduce", "c4": "touched"}[name]), mode0
     flat1, loss1, mode1 = _single_rank(name)
     assert mode1 == "single"
     nb = {"c3": 76, "c4": C4_STEPS}[name]

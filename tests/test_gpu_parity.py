@@ -213,6 +213,25 @@ def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3, flags=0, order=False, data
     return lay
 
 
+@pytest.mark.parametrize("waves", [8, 4])
+@pytest.mark.parametrize("mt,f,Lyr,B,U,I", [("NeuMF-end", 8, 3, 1024, 6041, 3707),     # C2 (per-row layer 0)
+                                            ("NeuMF-end", 16, 3, 8192, 6041, 3707),    # C3 at N = 8 (factored)
+                                            ("MLP", 8, 2, 256, 6041, 3707),            # C5 student
+                                            ("GMF", 16, 1, 3000, 6041, 3707),
+                                            ("NeuMF-end", 16, 3, 20000, 138494, 26745)])  # C4 ids, per-row
+def test_one_step_tuned_geometry_vs_oracle(mt, f, Lyr, B, U, I, waves, geometry):
+    """One step on the layout ncf_layout_tune shapes for B rows, with 8- and 4-wave
+    workgroups forced (NCF_LAYOUT_WG4: 64-row tiles; where the shape has no 4-wave
+    kernel -- per-row layer 0 with KT(0) > 4 -- the 8-wave one runs)."""
+    import ncf_amd._lib as L
+    from ncf_amd import ops
+    geometry(waves)
+    _, m = _models(mt, f, Lyr, U=U, I=I, seed=11)
+    lay = type(ops.ensure_flat(m)[1]).from_buffer_copy(ops.ensure_flat(m)[1])
+    L.check(L.hip().ncf_layout_tune(L.ctypes.byref(lay), B), "tune")
+    _one_step(mt, f, Lyr, B, U, I, flags=int(lay.flags))
+
+
 @pytest.mark.parametrize("cfg", list(ONE_STEP))
 def test_one_step_grads_vs_oracle(cfg):
     """Full-size id spaces (ml-1m): logits, loss and every gradient of one step."""
@@ -716,12 +735,24 @@ def test_engine_multitile_trajectory_vs_oracle(mt, f, Lyr):
     _teacher_forced_steps(ref, m, eng, users, items, labels)
 
 
-@pytest.mark.parametrize("B,per_row", [(1024, True), (4096, True), (8192, False), (300, True)])
-def test_engine_tuned_launch_shape_vs_oracle(B, per_row):
-    """ncf_layout_tune: the engine launches ceil(B/128) workgroups (the reductions read
-    that many slab rows) and takes per-row layer 0 when 2B < U + I (config C2:
-    NCF(8,3), bs 1024, ml-1m ids).  Every step teacher-forced from the oracle."""
+@pytest.fixture
+def geometry():
+    """Force the fused step's workgroup geometry (ncf_debug_set_geometry) for the test."""
     import ncf_amd._lib as L
+    yield lambda waves: L.check(L.hip().ncf_debug_set_geometry(waves), "geometry")
+    L.hip().ncf_debug_set_geometry(0)
+
+
+@pytest.mark.parametrize("waves", [0, 8, 4])
+@pytest.mark.parametrize("B,per_row", [(1024, True), (4096, True), (8192, False), (300, True), (20000, False)])
+def test_engine_tuned_launch_shape_vs_oracle(B, per_row, waves, geometry):
+    """ncf_layout_tune: the engine launches ceil(B / (16 x waves)) workgroups (the
+    reductions read that many slab rows) -- 4-wave workgroups up to 16,384 rows by
+    default (waves 0), or forced 8 / 4 -- and takes per-row layer 0 when 2B < U + I
+    (config C2: NCF(8,3), bs 1024, ml-1m ids).  Every step teacher-forced from the
+    oracle."""
+    import ncf_amd._lib as L
+    geometry(waves)
     T = 6
     ref, m, eng = _engine_for("NeuMF-end", 8, 3, 6041, 3707, 17)
     rng = np.random.default_rng(43)
@@ -730,7 +761,10 @@ def test_engine_tuned_launch_shape_vs_oracle(B, per_row):
     labels = (rng.random((T, B)) < 0.2).astype(np.int64)
     _stream(eng, users, items, labels, B)
     assert _fact_mode(eng.lay) == (not per_row)
-    assert (eng.lay.flags >> 8) & 0xFFF == (B + 127) // 128
+    w = waves or (4 if B <= 16384 else 8)
+    assert bool(eng.lay.flags & L.LAYOUT_WG4) == (w == 4)
+    tiles = (B + 16 * w - 1) // (16 * w)
+    assert (eng.lay.flags >> 8) & 0xFFF == (tiles if tiles < 256 else 0)
     ref0 = {k: v.clone() for k, v in ref.state_dict().items()}
     eng.run(T, use_graph=True)
     torch.cuda.synchronize()

@@ -304,3 +304,30 @@ def test_hr_ndcg_topk_ranking_matches_golden(golden, bs, k):
     hr, nd = _hr_ndcg_topk(logits, items, [bs] * (nb - 1) + [n - (nb - 1) * bs], k)
     assert hr.tolist() == g[f"bs{bs}_k{k}_HR"].tolist()
     np.testing.assert_allclose(nd.numpy(), g[f"bs{bs}_k{k}_NDCG"], rtol=0, atol=0)
+
+
+def test_layout_tune_launch_geometry():
+    """ncf_layout_tune (host logic, no GPU): per-rank batches up to 16,384 rows take
+    4-wave workgroups on 64-row tiles where the shape has that kernel (the factored
+    path always; per-row layer 0 when KT(0) <= 4), else 8-wave workgroups on 128-row
+    tiles; the workgroup count is the tile count below 256."""
+    import ncf_amd._lib as L
+    lib = L.hip()
+
+    def tune(U, I, f, nl, rows, waves=0):
+        assert lib.ncf_debug_set_geometry(waves) == 0
+        try:
+            lay = L.layout(U, I, f, nl, "NeuMF-end")
+            assert lib.ncf_layout_tune(ctypes.byref(lay), rows) == 0
+            return bool(lay.flags & L.LAYOUT_WG4), (lay.flags >> L.LAYOUT_WG_SHIFT) & L.LAYOUT_WG_MASK
+        finally:
+            lib.ncf_debug_set_geometry(0)
+
+    assert tune(6041, 3707, 8, 3, 1024) == (True, 16)        # C2: per-row layer 0, KT(0) = 4
+    assert tune(6041, 3707, 16, 3, 8192) == (True, 128)      # C3 at N = 8: factored
+    assert tune(6041, 3707, 16, 3, 65536) == (False, 0)      # C3 at N = 1: 512 tiles -> 256 workgroups
+    assert tune(6041, 3707, 16, 3, 16384) == (True, 0)       # 256 tiles of 64 rows
+    assert tune(138494, 26745, 16, 3, 8192) == (False, 64)   # C4 at N = 8: per-row, KT(0) = 8
+    assert tune(6041, 3707, 8, 3, 1024, waves=8) == (False, 8)
+    assert tune(6041, 3707, 16, 3, 65536, waves=4) == (True, 0)
+    assert lib.ncf_debug_set_geometry(5) != 0
