@@ -32,6 +32,7 @@ script spawns its N ranks itself before any GPU call.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import glob
 import json
 import os
@@ -109,6 +110,43 @@ def gather_scatter_bytes_per_row(f, L):
     dm = f * 2 ** (L - 1)
     rows = 2 * (f + dm) * 4
     return 8 + rows + rows
+
+
+def cache_probe(eng, rows_n, reps=50):
+    """ncf_probe_gather_scatter (include/ncf_hip.h) on the engine's own tables and the
+    first `rows_n` rows of its current epoch stream: the step's gather + float-atomic
+    scatter pattern with no arithmetic, `reps` launches back to back between one HIP
+    event pair on the launch stream per mode.  GB/s in the same algorithmic bytes as
+    roofline_hbm (gather_scatter_bytes_per_row; gather only: the row + reads, scatter
+    only: the row + adds)."""
+    import ncf_amd._lib as L
+    lay = eng.lay
+    if eng.model.model_type != "NeuMF-end" or eng.model.factor_num % 4:
+        return None
+    f, nl = eng.model.factor_num, eng.model.num_layers
+    dev = eng.device
+    st = torch.cuda.current_stream(dev)
+    sp = L.stream_ptr(dev)
+    scratch = torch.zeros_like(eng.grads)
+    sink = torch.empty(L.PROBE_BLOCKS * 256, dtype=torch.float32, device=dev)
+    full = gather_scatter_bytes_per_row(f, nl)
+    half = (full - 8) // 2
+    out = {}
+    for mode, name, per_row in ((1, "gather", 8 + half), (2, "scatter", 8 + half), (3, "gather_scatter", full)):
+        def launch():
+            L.check(L.hip().ncf_probe_gather_scatter(ctypes.byref(lay), eng.flat.data_ptr(), scratch.data_ptr(),
+                                                     sink.data_ptr(), eng.rows.data_ptr(), rows_n, mode, sp), "probe")
+        launch()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            launch()
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / reps
+        out[name] = {"GBps": per_row * rows_n / (ms * 1e-3) / 1e9, "us_per_launch": ms * 1e3}
+    del scratch, sink
+    return out
 
 
 def adam_info(kt, eng, model):
@@ -768,6 +806,25 @@ def main():
                  "16-byte loads run as exact three-plane bf16 splits on v_mfma_f32_16x16x32_bf16 (six bf16 "
                  "products per fp32 product; peak kept at the fp32 MFMA figure)")
 
+    # ---- the gather / scatter rate against a measured cache ceiling: the same
+    # access pattern alone (ncf_probe_gather_scatter) on the same tables and rows
+    roofline_cache = None
+    if path == L.PATH_FUSED and world == 1:
+        probe = cache_probe(eng, rows_per_launch)
+        if probe is not None:
+            ceil = probe["gather_scatter"]["GBps"]
+            tables_mb = 4 * (U + I) * (f + dm) / 1e6
+            state_mb = 4 * 4 * int(eng.lay.total) / 1e6  # params, grads, two Adam moments
+            roofline_cache = {
+                "bound": "cache", "achieved": achieved_gbs, "peak": ceil, "unit": "GB/s", "frac": achieved_gbs / ceil,
+                "probe": probe, "tables_MB": round(tables_mb, 2), "model_state_MB": round(state_mb, 2),
+                "resident": ("L2/MALL (tables fit the 4 MB L2 per XCD and the 256 MB MALL)" if tables_mb <= 4 else
+                             "MALL-assisted (tables and optimizer state fit the 256 MB MALL)" if state_mb <= 256 else
+                             "HBM (model state above the 256 MB MALL)"),
+                "note": "achieved = the step launch group's gather+scatter algorithmic bytes (roofline_hbm) / its "
+                        "time; peak = ncf_probe_gather_scatter: the same gathers and float-atomic adds, same rows "
+                        "and tables, no arithmetic, launches back to back"}
+
     # ---- weak scaling (extra field): global batch x N, per-GPU batch fixed -----
     weak = None
     if world > 1 and not args.no_weak:
@@ -844,6 +901,7 @@ def main():
                              "traffic_GBps": (traffic / (ms * 1e-3) / 1e9) if traffic else None,
                              "note": ("gather+scatter algorithmic bytes of the same launch group" if path == L.PATH_FUSED
                                       else "gather+scatter algorithmic bytes over all layered-path kernels")},
+            "roofline_cache": roofline_cache,
             "kernel_ms": kt,
             "adam": adam_info(kt, eng, model),
             "quality": {"HR@10": hr10, "NDCG@10": ndcg10, "epochs_trained": round(eng.state_step() / eng.num_batches, 2),

@@ -465,6 +465,18 @@ int ncf_hr_ndcg(const float *logits, const int32_t *items, int64_t n, int batch,
  * (1 = skip embedding scatter-add, 2 = skip weight-gradient MFMAs).  Results are
  * wrong while any switch is set; 0 restores the production kernel. */
 int ncf_debug_set_diag(int flags);
+
+/*
+ * Ceiling probe of the embedding access pattern (bench.py `roofline_cache`): for the
+ * n packed rows, the 16-byte pieces of their four embedding rows (Ug[u], Ig[i],
+ * Um[u], Im[i]; models.py:108-112) gathered (mode 1), float-atomically added into
+ * the same rows of grads (mode 2), or both (mode 3) -- the fused step's gather and
+ * scatter with no arithmetic, on tables that sit in L2 / the MALL at ml-1m.  NeuMF
+ * layouts with factor_num % 4 == 0.  sink: NCF_PROBE_BLOCKS * 256 floats (modes 1, 3).
+ */
+#define NCF_PROBE_BLOCKS 2048
+int ncf_probe_gather_scatter(const ncf_layout *lay, const float *params, float *grads, float *sink,
+                             const uint64_t *rows, int64_t n, int mode, void *stream);
 /* Launch geometry of the fused step for later ncf_layout_tune calls: 0 = chosen by
  * the batch size (4-wave workgroups for small per-rank batches), 4 or 8 = forced
  * where that kernel exists (A/B measurements, tests).  NCF_E_ARG otherwise. */

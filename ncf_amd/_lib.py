@@ -34,6 +34,7 @@ PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 LAYOUT_PER_ROW_L0, LAYOUT_WG_SHIFT, LAYOUT_WG_MASK = 0x1, 8, 0xFFF  # ncf_layout.flags (ncf_layout_tune)
 LAYOUT_LAYERED = 0x2  # ncf_layout.flags: training on the layered path even where a fused kernel exists
 LAYOUT_WG4 = 0x4  # ncf_layout.flags: the fused step on 4-wave workgroups (small per-rank batches)
+PROBE_BLOCKS = 2048  # include/ncf_hip.h NCF_PROBE_BLOCKS (ncf_probe_gather_scatter's sink: x 256 floats)
 LAYOUT_FACT_DEFER_DX = 0x8  # ncf_layout.flags: factored step leaves G for ncf_adam_step_fact (sharded zero1)
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
 
@@ -84,6 +85,8 @@ _HIP_PROTOS = {
     "ncf_slab_stride": (c_i64, [ctypes.POINTER(NcfLayout)]),
     "ncf_debug_set_diag": (ctypes.c_int, [ctypes.c_int]),
     "ncf_debug_set_geometry": (ctypes.c_int, [ctypes.c_int]),
+    "ncf_probe_gather_scatter": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_i64,
+                                                ctypes.c_int, c_vp]),
     "ncf_debug_set_stamps": (ctypes.c_int, [c_vp]),
     "ncf_adam_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.c_int, c_vp,
                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,

@@ -12,5 +12,6 @@ for w in 8 4; do
   NCF_WG_WAVES=$w timeout -k 10 200 python scripts/dp_modes.py c3 8 allreduce,zero1 > gpurun_out/r4b_dp_c3_w$w.json 2>&1 || exit 1
   NCF_WG_WAVES=$w timeout -k 10 200 python bench.py --config c2 --steps 2000 --warmup 200 --skip-cpu-baseline --e2e-epochs 0 > gpurun_out/r4b_c2_w$w.json 2>&1 || exit 1
 done
+timeout -k 10 300 python bench.py --steps 20 --skip-cpu-baseline --e2e-epochs 0 > gpurun_out/r4b_c3.json 2>&1 || exit 1
 for a in "c2 1024" "c3 8192"; do NCF_WG_WAVES=8 timeout -k 10 120 python scripts/stamps.py $a >> gpurun_out/r4b_stamps.jsonl 2>>gpurun_out/r4b_stamps.err || exit 1; done
 echo DONE
