@@ -76,7 +76,8 @@ typedef struct ncf_layout {
 #define NCF_LAYOUT_LAYERED 0x2      /* training steps on the layered path even where a fused kernel exists */
 #define NCF_LAYOUT_WG_SHIFT 8       /* bits 8..19: workgroups of the fused step (0 = ncf_slab_rows()) */
 #define NCF_LAYOUT_WG_MASK 0xfff
-#define NCF_LAYOUT_WG4 0x4          /* fused step on 4-wave workgroups (64-row tiles): small per-rank batches */
+#define NCF_LAYOUT_GEO_SHIFT 20     /* bits 20..21: workgroup geometry of the fused step -- 0: 8 waves on */
+#define NCF_LAYOUT_GEO_MASK 0x3     /* 128-row tiles; 1, 2, 3: 4, 2, 1 waves on 64, 32, 16-row tiles */
 #define NCF_LAYOUT_FACT_DEFER_DX 0x8 /* factored layer 0: the step forms only the dW0 partials and leaves the
                                         per-entity sums G in grads' Um / Im rows (ncf_adam_step_fact expands them
                                         per shard after the reduce-scatter); set by the caller, kept by tune */
@@ -477,9 +478,9 @@ int ncf_debug_set_diag(int flags);
 #define NCF_PROBE_BLOCKS 2048
 int ncf_probe_gather_scatter(const ncf_layout *lay, const float *params, float *grads, float *sink,
                              const uint64_t *rows, int64_t n, int mode, void *stream);
-/* Launch geometry of the fused step for later ncf_layout_tune calls: 0 = chosen by
- * the batch size (4-wave workgroups for small per-rank batches), 4 or 8 = forced
- * where that kernel exists (A/B measurements, tests).  NCF_E_ARG otherwise. */
+/* Workgroup geometry of the fused step for later ncf_layout_tune calls: 0 = chosen by
+ * the per-rank batch (narrower workgroups for small batches), 8, 4, 2 or 1 waves =
+ * forced where that kernel exists (A/B measurements, tests).  NCF_E_ARG otherwise. */
 int ncf_debug_set_geometry(int waves);
 
 /* Diagnostics only: device buffer of ncf_slab_rows() x 64 uint64 that the next

@@ -33,7 +33,7 @@ ABI_VERSION = 14  # include/ncf_hip.h NCF_ABI_VERSION
 PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 LAYOUT_PER_ROW_L0, LAYOUT_WG_SHIFT, LAYOUT_WG_MASK = 0x1, 8, 0xFFF  # ncf_layout.flags (ncf_layout_tune)
 LAYOUT_LAYERED = 0x2  # ncf_layout.flags: training on the layered path even where a fused kernel exists
-LAYOUT_WG4 = 0x4  # ncf_layout.flags: the fused step on 4-wave workgroups (small per-rank batches)
+LAYOUT_GEO_SHIFT, LAYOUT_GEO_MASK = 20, 0x3  # ncf_layout.flags: fused-step geometry (0..3: 8, 4, 2, 1 waves)
 PROBE_BLOCKS = 2048  # include/ncf_hip.h NCF_PROBE_BLOCKS (ncf_probe_gather_scatter's sink: x 256 floats)
 LAYOUT_FACT_DEFER_DX = 0x8  # ncf_layout.flags: factored step leaves G for ncf_adam_step_fact (sharded zero1)
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}

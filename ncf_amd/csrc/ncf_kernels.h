@@ -73,6 +73,11 @@ struct Shape {
     static_assert(!MLP || boff(L) <= 128, "bias LDS region");
     static_assert(P <= 128, "predict LDS region");
     static constexpr int KT0 = MLP ? KT(0) : 1;
+    // tower weights staged through registers by each thread in the prologue (16-byte
+    // pieces): the narrow workgroup geometries are built where this stays <= 16
+    __host__ __device__ static constexpr int wper(int k) { return MLP ? (16 * MT(k) * (S(k) / 4) + NTH - 1) / NTH : 0; }
+    __host__ __device__ static constexpr int wreg_total(int k) { return k < 0 ? 0 : wper(k) + wreg_total(k - 1); }
+    static constexpr int WREG = wreg_total(L - 1);
     // Layer-0 wgrad after the embedding scatter (its atomics drain under the wgrad
     // MFMAs) keeps the wgrad operands live through the dgrad: off where that
     // exceeds the register file (NeuMF f=64).
@@ -108,10 +113,11 @@ constexpr int DIAG_NO_ITEM_SCATTER = 16;  // diag build only: skip the Im segmen
 constexpr int DIAG_NO_GMF_SCATTER = 32;   // diag build only: skip the Ug / Ig atomics
 constexpr int DIAG_PREP_DIRECT = 4;  // ncf_prepare_epoch: global-atomic histogram variant (still correct)
 
-// Launch geometries of the fused step: GEO_8 = NWAVES-wave workgroups (128-row
-// tiles), GEO_4 = 4-wave workgroups (64-row tiles; NCF_LAYOUT_WG4).
-enum { GEO_8 = 0, GEO_4 = 1, NGEO = 2 };
-__host__ __device__ constexpr int geo_waves(int g) { return g == GEO_4 ? 4 : NWAVES; }
+// Launch geometries of the fused step (the NCF_LAYOUT_GEO field): GEO_8 = NWAVES-wave
+// workgroups on 128-row tiles, GEO_4 / GEO_2 / GEO_1 = 4 / 2 / 1 waves on 64 / 32 /
+// 16-row tiles for small per-rank batches.
+enum { GEO_8 = 0, GEO_4 = 1, GEO_2 = 2, GEO_1 = 3, NGEO = 4 };
+__host__ __device__ constexpr int geo_waves(int g) { return g == GEO_8 ? NWAVES : (8 >> g); }
 
 struct KernelEntry {
     int mode, F, L;

@@ -1268,8 +1268,11 @@ static int g_diag = 0;
 static unsigned long long* g_stamps = nullptr;
 // ncf_debug_set_geometry: 0 = ncf_layout_tune decides, 4 / NWAVES = forced (A/B, tests)
 static int g_geo_waves = 0;
-// ncf_layout_tune: 4-wave workgroups up to this many rows per rank
-constexpr int64_t WG4_MAX_ROWS = 16384;
+// ncf_layout_tune: the widest workgroup geometry with at least this many tiles
+#ifndef NCF_GEO_MIN_WGS
+#define NCF_GEO_MIN_WGS 256
+#endif
+constexpr int64_t GEO_MIN_WGS = NCF_GEO_MIN_WGS;
 
 static int launch_status() { return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH; }
 
@@ -1615,11 +1618,12 @@ static bool fact_mode(const ncf_layout* lay) {
 }
 
 // Launch geometry of the fused training step: 4-wave workgroups where
-// ncf_layout_tune asked for them (NCF_LAYOUT_WG4) and the kernel exists.
+// ncf_layout_tune asked for them (the NCF_LAYOUT_GEO field) and the kernel exists.
 static int train_geo(const KernelEntry* e, const ncf_layout* lay) {
-    if (!(lay->flags & NCF_LAYOUT_WG4)) return GEO_8;
-    const void* fn = fact_mode(lay) ? e->train_fact[GEO_4] : e->train[GEO_4];
-    return fn != nullptr ? GEO_4 : GEO_8;
+    const int g = (lay->flags >> NCF_LAYOUT_GEO_SHIFT) & NCF_LAYOUT_GEO_MASK;
+    if (g == GEO_8) return GEO_8;
+    const void* fn = fact_mode(lay) ? e->train_fact[g] : e->train[g];
+    return fn != nullptr ? g : GEO_8;
 }
 
 // Workgroups of the fused step = rows of the slab the reductions read.
@@ -1732,16 +1736,33 @@ int64_t ncf_fact_partials_bytes(const ncf_layout* lay) {
 
 int ncf_layout_tune(ncf_layout* lay, int64_t rows) {
     if (!lay || rows <= 0) return NCF_E_ARG;
-    int32_t f = lay->flags & ~(NCF_LAYOUT_PER_ROW_L0 | NCF_LAYOUT_WG4 | (NCF_LAYOUT_WG_MASK << NCF_LAYOUT_WG_SHIFT));
+    int32_t f = lay->flags & ~(NCF_LAYOUT_PER_ROW_L0 | (NCF_LAYOUT_GEO_MASK << NCF_LAYOUT_GEO_SHIFT) |
+                               (NCF_LAYOUT_WG_MASK << NCF_LAYOUT_WG_SHIFT));
     if (2 * rows < (int64_t)lay->user_num + lay->item_num) f |= NCF_LAYOUT_PER_ROW_L0;
-    // small per-rank batches: 4-wave workgroups on 64-row tiles (twice the workgroups
-    // of the 128-row tiling, one wave per SIMD, half the waves per barrier and sum)
-    const bool wg4 = g_geo_waves == 4 || (g_geo_waves == 0 && rows <= WG4_MAX_ROWS);
-    if (wg4) f |= NCF_LAYOUT_WG4;
     lay->flags = f;
+    // geometry: forced (ncf_debug_set_geometry), else the widest workgroups that still
+    // give GEO_MIN_WGS tiles -- small per-rank batches spread over more CUs with fewer
+    // waves per workgroup (shorter barriers and cross-wave sums, one wave per SIMD)
     const KernelEntry* e = train_fused(lay);
-    if (wg4 && (!e || train_geo(e, lay) != GEO_4)) f &= ~NCF_LAYOUT_WG4;  // no 4-wave kernel for this shape
-    const int tr = 16 * ((f & NCF_LAYOUT_WG4) ? geo_waves(GEO_4) : geo_waves(GEO_8));
+    int g = GEO_8;
+    if (e) {
+        auto avail = [&](int gg) {
+            lay->flags = f | (gg << NCF_LAYOUT_GEO_SHIFT);
+            return train_geo(e, lay) == gg;
+        };
+        if (g_geo_waves != 0) {
+            for (int gg = 0; gg < NGEO; ++gg)
+                if (geo_waves(gg) == g_geo_waves && avail(gg)) g = gg;
+        } else {
+            for (int gg = GEO_8; gg < NGEO; ++gg) {
+                if (!avail(gg)) continue;
+                g = gg;
+                if ((rows + 16 * geo_waves(gg) - 1) / (16 * geo_waves(gg)) >= GEO_MIN_WGS) break;
+            }
+        }
+    }
+    f |= g << NCF_LAYOUT_GEO_SHIFT;
+    const int tr = 16 * geo_waves(g);
     const int64_t tiles = (rows + tr - 1) / tr;
     if (tiles < SLAB_ROWS) f |= (int32_t)tiles << NCF_LAYOUT_WG_SHIFT;
     lay->flags = f;
@@ -1749,7 +1770,7 @@ int ncf_layout_tune(ncf_layout* lay, int64_t rows) {
 }
 
 int ncf_debug_set_geometry(int waves) {
-    if (waves != 0 && waves != 4 && waves != NWAVES) return NCF_E_ARG;
+    if (waves != 0 && waves != 1 && waves != 2 && waves != 4 && waves != NWAVES) return NCF_E_ARG;
     g_geo_waves = waves;
     return NCF_OK;
 }

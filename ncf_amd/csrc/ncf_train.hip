@@ -94,7 +94,6 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     // workgroup geometry: NW waves, 16 rows each, per tile (NW = 8, or 4 for small batches)
     constexpr int NWV = S_::NWV, NTH = S_::NTH, TRW = S_::TR;
     static_assert(!FACT || S_::MLP, "factored layer 0 needs the MLP tower");
-    static_assert(!S_::MLP || FACT || FWD_ONLY || S_::KT(0) <= NWV, "layer-0 wgrad: one 16-column block per wave");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* sW = smem;
     int* su2 = reinterpret_cast<int*>(smem + S_::W_TOTAL);  // [2][TRW] user ids (-1 = padding row)
@@ -120,7 +119,8 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     // the control block and the row indices make their round trips.
     constexpr int PERMAX = S_::MLP ? (16 * S_::MT(0) * (S_::S(0) / 4) + NTH - 1) / NTH : 1;
     f4 wreg[L][PERMAX];
-    float breg[L];
+    constexpr int BPER = (128 + NTH - 1) / NTH;  // bias entries per thread (16 * MT(k) <= 128)
+    float breg[L][BPER];
     if constexpr (S_::MLP) {
         static_for<L>([&](auto kk) {
             constexpr int k = decltype(kk)::value;
@@ -133,7 +133,11 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                 const int o = e / cols4;
                 wreg[k][q] = (e < rows * cols4 && o < outs) ? Wg[e] : f4{0.f, 0.f, 0.f, 0.f};
             }
-            breg[k] = tid < outs ? prm[lay.b[k] + tid] : 0.f;  // 16 * MT(k) <= 128 < NTH
+#pragma unroll
+            for (int q = 0; q < BPER; ++q) {
+                const int e = tid + q * NTH;
+                breg[k][q] = e < outs ? prm[lay.b[k] + e] : 0.f;
+            }
         });
     }
 
@@ -227,7 +231,9 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                 const int o = e / cols4, i4 = e - o * cols4;
                 if (e < rows * cols4) *reinterpret_cast<f4*>(Ws + o * S_::SW(k) + 4 * i4) = wreg[k][q];
             }
-            if (tid < 16 * S_::MT(k)) sB[S_::boff(k) + tid] = breg[k];
+#pragma unroll
+            for (int q = 0; q < BPER; ++q)
+                if (tid + q * NTH < 16 * S_::MT(k)) sB[S_::boff(k) + tid + q * NTH] = breg[k][q];
         });
     }
     for (int e = tid; e < 128; e += NTH) sWP[e] = e < S_::P ? prm[lay.wp + e] : 0.f;
@@ -236,7 +242,10 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     constexpr int MT0 = S_::MLP ? S_::MT(0) : 1;
     constexpr int KT0 = S_::KT0;
     constexpr int MTL = S_::MLP ? S_::MT(L - 1) : 1;
-    f4 accW0[MT0];          // dW_0 tiles (mt, nt = w)
+    // per-row layer-0 wgrad: each wave owns the 16-column blocks nt = w + j * NWV of
+    // dW0 (j < CB0; one block at 8 waves, several in narrow workgroups)
+    constexpr int CB0 = S_::MLP && !FACT ? (KT0 + NWV - 1) / NWV : 1;
+    f4 accW0[CB0][MT0];     // dW_0 tiles (mt, nt = w + j * NWV)
     float dbAcc[L];
     f4 dWpT[MTL];
     f4 accK[S_::NKT > 0 ? S_::NKT : 1];    // dW_k tiles of layers k >= 1, this wave's rows
@@ -251,7 +260,9 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         dbAcc[k] = 0.f;
     }
 #pragma unroll
-    for (int t = 0; t < MT0; ++t) accW0[t] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < MT0; ++t)
+#pragma unroll
+        for (int j = 0; j < CB0; ++j) accW0[j][t] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < MTL; ++t) dWpT[t] = f4{0.f, 0.f, 0.f, 0.f};
 
@@ -511,19 +522,22 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         } else {
             // (d) layer-0 wgrad operand: X0 rows of the whole tile, columns 16*nt + c
             constexpr int DM = S_::DM;
-            float bx[S_::MLP && !FACT ? NWV * 4 : 1];
-            const int nt0 = w < KT0 ? w : KT0 - 1;
+            float bx[CB0][S_::MLP && !FACT ? NWV * 4 : 1];
             if constexpr (S_::MLP && !FACT) {
-                const int fj = 16 * nt0 + c;
-                const bool isu = fj < DM;
-                const int64_t tab = isu ? lay.um + fj : lay.im + (fj - DM);
-                const int* ids = isu ? su : si;
 #pragma unroll
-                for (int ws = 0; ws < NWV; ++ws) {
+                for (int j = 0; j < CB0; ++j) {
+                    const int ntj = w + j * NWV < KT0 ? w + j * NWV : KT0 - 1;
+                    const int fj = 16 * ntj + c;
+                    const bool isu = fj < DM;
+                    const int64_t tab = isu ? lay.um + fj : lay.im + (fj - DM);
+                    const int* ids = isu ? su : si;
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        const int id = max(ids[ws * 16 + 4 * g + s], 0);
-                        bx[ws * 4 + s] = prm[tab + (int64_t)id * DM];
+                    for (int ws = 0; ws < NWV; ++ws) {
+#pragma unroll
+                        for (int s = 0; s < 4; ++s) {
+                            const int id = max(ids[ws * 16 + 4 * g + s], 0);
+                            bx[j][ws * 4 + s] = prm[tab + (int64_t)id * DM];
+                        }
                     }
                 }
             }
@@ -729,30 +743,34 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                             dbAcc[0] += s;
                         }
                     auto wgrad0 = [&]() {
-                        if (w < KT0 && !(a.diag & DIAG_NO_WGRAD)) {
+                        if (!(a.diag & DIAG_NO_WGRAD)) {
                             // layer-0 staging region of this tile (see RK below)
                             const int RK0 = S_::ALT0 ? ((titer & 1) ? S_::HALF0 : 0) : 0;
 #pragma unroll
-                            for (int mt = 0; mt < MT0; ++mt) {
-                                f4 acc0 = accW0[mt], acc1 = f4{0.f, 0.f, 0.f, 0.f};
+                            for (int j = 0; j < CB0; ++j) {
+                                if (w + j * NWV >= KT0) break;  // wave-uniform
 #pragma unroll
-                                for (int ws = 0; ws < NWV; ++ws) {
-                                    const float* sto = sstage + ws * S_::WAVE_STAGE + RK0;
+                                for (int mt = 0; mt < MT0; ++mt) {
+                                    f4 acc0 = accW0[j][mt], acc1 = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                                    for (int s = 0; s < 4; ++s) {
-                                        const float av = sto[(4 * g + s) * S_::SD(0) + 16 * mt + c];
-                                        if (ws & 1)
-                                            acc1 = MFMA4(av, bx[ws * 4 + s], acc1);
-                                        else
-                                            acc0 = MFMA4(av, bx[ws * 4 + s], acc0);
+                                    for (int ws = 0; ws < NWV; ++ws) {
+                                        const float* sto = sstage + ws * S_::WAVE_STAGE + RK0;
+#pragma unroll
+                                        for (int s = 0; s < 4; ++s) {
+                                            const float av = sto[(4 * g + s) * S_::SD(0) + 16 * mt + c];
+                                            if (ws & 1)
+                                                acc1 = MFMA4(av, bx[j][ws * 4 + s], acc1);
+                                            else
+                                                acc0 = MFMA4(av, bx[j][ws * 4 + s], acc0);
+                                        }
+                                        if (ws & 1) __builtin_amdgcn_sched_barrier(0);
                                     }
-                                    if (ws & 1) __builtin_amdgcn_sched_barrier(0);
+                                    acc0.x += acc1.x;
+                                    acc0.y += acc1.y;
+                                    acc0.z += acc1.z;
+                                    acc0.w += acc1.w;
+                                    accW0[j][mt] = acc0;
                                 }
-                                acc0.x += acc1.x;
-                                acc0.y += acc1.y;
-                                acc0.z += acc1.z;
-                                acc0.w += acc1.w;
-                                accW0[mt] = acc0;
                             }
                         }
                     };
@@ -788,7 +806,9 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                         // drain the atomics too.
                         if (S_::WGRAD0_LATE && !wv_hi) {
 #pragma unroll
-                            for (int i = 0; i < NWV * 4; ++i) asm volatile("" ::"v"(bx[i]));
+                            for (int i = 0; i < NWV * 4; ++i)
+#pragma unroll
+                                for (int j = 0; j < CB0; ++j) asm volatile("" ::"v"(bx[j][i]));
                         }
                         stamp(a, sb + 4 + 3 * (L - 1));
                         // item half -> this wave's scratch rows (segment-reduced below);
@@ -878,13 +898,16 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         // layer-0 wgrad: this wave's 16-column block, already summed over the rows
         // (FACT: formed after the step by fact_expand_kernel; its slab columns unused)
         if constexpr (S_::MLP && !FACT) {
-            if (w < KT0) {
+#pragma unroll
+            for (int j = 0; j < CB0; ++j) {
+                const int ntj = w + j * NWV;
+                if (ntj >= KT0) break;
 #pragma unroll
                 for (int mt = 0; mt < MT0; ++mt) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int o = 16 * mt + 4 * g + r;
-                        if (o < S_::S(1)) out[(lay.w[0] - tb) + o * S_::S(0) + 16 * w + c] = lane_get(accW0[mt], r);
+                        if (o < S_::S(1)) out[(lay.w[0] - tb) + o * S_::S(0) + 16 * ntj + c] = lane_get(accW0[j][mt], r);
                     }
                 }
             }
@@ -896,7 +919,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         // the tail rides with the last layer's round where both images fit
         constexpr bool TAIL_MERGED = S_::MLP && L >= 2 && S_::rwk(L - 1) + NT <= S_::WAVE_STAGE;
         constexpr int TOFF = TAIL_MERGED ? S_::rwk(L - 1) : 0;
-        static_assert(TOFF + NT <= S_::WAVE_STAGE && NT <= NTH, "epilogue tail image");
+        static_assert(TOFF + NT <= S_::WAVE_STAGE, "epilogue tail image");
         float tw[MTL][4];  // predict-weight partials summed over the wave's rows (lanes c == 0)
         if constexpr (S_::MLP) {
 #pragma unroll
@@ -942,13 +965,13 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
             }
         };
         auto sum_tail = [&]() {
-            if (tid < NT) {
+            for (int e = tid; e < NT; e += NTH) {
                 float ts = 0.f;
 #pragma unroll
-                for (int ws = 0; ws < NWV; ++ws) ts += sstage[ws * S_::WAVE_STAGE + TOFF + tid];
-                const int64_t pos = tid < S1 ? (lay.b[0] - tb) + tid
-                                  : tid < S1 + S_::P ? (lay.wp - tb) + (tid - S1)
-                                  : tid == S1 + S_::P ? (lay.bp - tb) : (int64_t)lay.tower_len;
+                for (int ws = 0; ws < NWV; ++ws) ts += sstage[ws * S_::WAVE_STAGE + TOFF + e];
+                const int64_t pos = e < S1 ? (lay.b[0] - tb) + e
+                                  : e < S1 + S_::P ? (lay.wp - tb) + (e - S1)
+                                  : e == S1 + S_::P ? (lay.bp - tb) : (int64_t)lay.tower_len;
                 out[pos] = ts;
             }
         };
@@ -1037,33 +1060,42 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
 
 // ---------------------------------------------------------------------------
 // host-side dispatch table
+// Narrow workgroups (4 / 2 / 1 waves) for the small shapes: each thread stages a
+// 1/(64 waves) share of the tower weights through registers in the prologue (at most
+// 16 16-byte pieces, WREG), and the per-row layer-0 wgrad gives each wave
+// CB0 = KT(0) / waves column blocks of dW0 in registers, so that kernel is built where
+// dW0 has at most 8 16x16 tiles (the factored kernel and GMF have no such term).
+template <int F, int L, int MODE, int G>
+static void set_geo(KernelEntry& e) {
+    constexpr int NW = geo_waves(G);
+    using SG = Shape<F, L, MODE, NW>;
+    using S8 = Shape<F, L, MODE>;
+    constexpr bool regs_ok = NW == NWAVES || SG::WREG <= 16;  // the prologue's weight registers
+    if constexpr (regs_ok && (!S8::MLP || S8::MT(0) * S8::KT(0) <= 8 || NW == NWAVES))
+        e.train[G] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, false, NW>);
+    else
+        e.train[G] = nullptr;
+    if constexpr (S8::MLP && regs_ok)
+        e.train_fact[G] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, true, NW>);
+    else
+        e.train_fact[G] = nullptr;
+    e.misc[G] = SG::MISC;
+    e.stage[G] = NW * SG::WAVE_STAGE;
+}
+
 template <int F, int L, int MODE>
 static KernelEntry make_entry() {
     using S_ = Shape<F, L, MODE>;
-    using S4 = Shape<F, L, MODE, 4>;
     KernelEntry e;
     e.mode = MODE;
     e.F = F;
     e.L = L;
-    e.train[GEO_8] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, false, NWAVES>);
-    // 4-wave workgroups: the per-row layer-0 wgrad gives each wave one 16-column block
-    // of dW0, so KT(0) <= 4 there; the factored kernel has no such limit
-    if constexpr (!S_::MLP || S_::KT(0) <= 4)
-        e.train[GEO_4] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, false, 4>);
-    else
-        e.train[GEO_4] = nullptr;
+    set_geo<F, L, MODE, GEO_8>(e);
+    set_geo<F, L, MODE, GEO_4>(e);
+    set_geo<F, L, MODE, GEO_2>(e);
+    set_geo<F, L, MODE, GEO_1>(e);
     e.fwd = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, true, false, NWAVES>);
-    if constexpr (S_::MLP) {
-        e.train_fact[GEO_8] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, true, NWAVES>);
-        e.train_fact[GEO_4] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, true, 4>);
-    } else {
-        e.train_fact[GEO_8] = e.train_fact[GEO_4] = nullptr;
-    }
     e.w_total = S_::W_TOTAL;
-    e.misc[GEO_8] = S_::MISC;
-    e.misc[GEO_4] = S4::MISC;
-    e.stage[GEO_8] = NWAVES * S_::WAVE_STAGE;
-    e.stage[GEO_4] = 4 * S4::WAVE_STAGE;
     return e;
 }
 

@@ -213,16 +213,17 @@ def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3, flags=0, order=False, data
     return lay
 
 
-@pytest.mark.parametrize("waves", [8, 4])
+@pytest.mark.parametrize("waves", [8, 4, 2, 1])
 @pytest.mark.parametrize("mt,f,Lyr,B,U,I", [("NeuMF-end", 8, 3, 1024, 6041, 3707),     # C2 (per-row layer 0)
                                             ("NeuMF-end", 16, 3, 8192, 6041, 3707),    # C3 at N = 8 (factored)
                                             ("MLP", 8, 2, 256, 6041, 3707),            # C5 student
                                             ("GMF", 16, 1, 3000, 6041, 3707),
                                             ("NeuMF-end", 16, 3, 20000, 138494, 26745)])  # C4 ids, per-row
 def test_one_step_tuned_geometry_vs_oracle(mt, f, Lyr, B, U, I, waves, geometry):
-    """One step on the layout ncf_layout_tune shapes for B rows, with 8- and 4-wave
-    workgroups forced (NCF_LAYOUT_WG4: 64-row tiles; where the shape has no 4-wave
-    kernel -- per-row layer 0 with KT(0) > 4 -- the 8-wave one runs)."""
+    """One step on the layout ncf_layout_tune shapes for B rows, with 8-, 4-, 2- and
+    1-wave workgroups forced (the NCF_LAYOUT_GEO field: 128 / 64 / 32 / 16-row tiles;
+    where the shape has no narrow kernel -- per-row layer 0 with more than 8 dW0
+    tiles -- the 8-wave one runs)."""
     import ncf_amd._lib as L
     from ncf_amd import ops
     geometry(waves)
@@ -743,14 +744,14 @@ def geometry():
     L.hip().ncf_debug_set_geometry(0)
 
 
-@pytest.mark.parametrize("waves", [0, 8, 4])
+@pytest.mark.parametrize("waves", [0, 8, 4, 2, 1])
 @pytest.mark.parametrize("B,per_row", [(1024, True), (4096, True), (8192, False), (300, True), (20000, False)])
 def test_engine_tuned_launch_shape_vs_oracle(B, per_row, waves, geometry):
     """ncf_layout_tune: the engine launches ceil(B / (16 x waves)) workgroups (the
-    reductions read that many slab rows) -- 4-wave workgroups up to 16,384 rows by
-    default (waves 0), or forced 8 / 4 -- and takes per-row layer 0 when 2B < U + I
-    (config C2: NCF(8,3), bs 1024, ml-1m ids).  Every step teacher-forced from the
-    oracle."""
+    reductions read that many slab rows) -- by default (waves 0) the widest of 8 / 4 /
+    2 / 1-wave workgroups that gives 256 tiles, or forced -- and takes per-row layer 0
+    when 2B < U + I (config C2: NCF(8,3), bs 1024, ml-1m ids).  Every step
+    teacher-forced from the oracle."""
     import ncf_amd._lib as L
     geometry(waves)
     T = 6
@@ -761,8 +762,8 @@ def test_engine_tuned_launch_shape_vs_oracle(B, per_row, waves, geometry):
     labels = (rng.random((T, B)) < 0.2).astype(np.int64)
     _stream(eng, users, items, labels, B)
     assert _fact_mode(eng.lay) == (not per_row)
-    w = waves or (4 if B <= 16384 else 8)
-    assert bool(eng.lay.flags & L.LAYOUT_WG4) == (w == 4)
+    w = waves or next((x for x in (8, 4, 2, 1) if (B + 16 * x - 1) // (16 * x) >= 256), 1)
+    assert (8, 4, 2, 1)[(eng.lay.flags >> L.LAYOUT_GEO_SHIFT) & L.LAYOUT_GEO_MASK] == w
     tiles = (B + 16 * w - 1) // (16 * w)
     assert (eng.lay.flags >> 8) & 0xFFF == (tiles if tiles < 256 else 0)
     ref0 = {k: v.clone() for k, v in ref.state_dict().items()}

@@ -307,10 +307,11 @@ def test_hr_ndcg_topk_ranking_matches_golden(golden, bs, k):
 
 
 def test_layout_tune_launch_geometry():
-    """ncf_layout_tune (host logic, no GPU): per-rank batches up to 16,384 rows take
-    4-wave workgroups on 64-row tiles where the shape has that kernel (the factored
-    path always; per-row layer 0 when KT(0) <= 4), else 8-wave workgroups on 128-row
-    tiles; the workgroup count is the tile count below 256."""
+    """ncf_layout_tune (host logic, no GPU): the fused step's workgroup geometry is the
+    widest of 8 / 4 / 2 / 1 waves (128 / 64 / 32 / 16-row tiles) that still gives 256
+    tiles, among the geometries the shape has (the factored kernel and GMF: all; the
+    per-row layer 0: narrow ones only where dW0 has at most 8 16x16 tiles), else the
+    narrowest; the workgroup count is the tile count below 256."""
     import ncf_amd._lib as L
     lib = L.hip()
 
@@ -319,15 +320,19 @@ def test_layout_tune_launch_geometry():
         try:
             lay = L.layout(U, I, f, nl, "NeuMF-end")
             assert lib.ncf_layout_tune(ctypes.byref(lay), rows) == 0
-            return bool(lay.flags & L.LAYOUT_WG4), (lay.flags >> L.LAYOUT_WG_SHIFT) & L.LAYOUT_WG_MASK
+            g = (lay.flags >> L.LAYOUT_GEO_SHIFT) & L.LAYOUT_GEO_MASK
+            return (8, 4, 2, 1)[g], (lay.flags >> L.LAYOUT_WG_SHIFT) & L.LAYOUT_WG_MASK
         finally:
             lib.ncf_debug_set_geometry(0)
 
-    assert tune(6041, 3707, 8, 3, 1024) == (True, 16)        # C2: per-row layer 0, KT(0) = 4
-    assert tune(6041, 3707, 16, 3, 8192) == (True, 128)      # C3 at N = 8: factored
-    assert tune(6041, 3707, 16, 3, 65536) == (False, 0)      # C3 at N = 1: 512 tiles -> 256 workgroups
-    assert tune(6041, 3707, 16, 3, 16384) == (True, 0)       # 256 tiles of 64 rows
-    assert tune(138494, 26745, 16, 3, 8192) == (False, 64)   # C4 at N = 8: per-row, KT(0) = 8
-    assert tune(6041, 3707, 8, 3, 1024, waves=8) == (False, 8)
-    assert tune(6041, 3707, 16, 3, 65536, waves=4) == (True, 0)
+    assert tune(6041, 3707, 8, 3, 1024) == (1, 64)         # C2: per-row layer 0, dW0 2 x 4 tiles
+    assert tune(6041, 3707, 16, 3, 8192) == (4, 128)       # C3 at N = 8 (factored): no 2-wave kernel (weights
+    assert tune(6041, 3707, 8, 3, 8192) == (2, 0)          # staged in 21 registers); NCF(8,3): 256 tiles of 32
+    assert tune(6041, 3707, 16, 3, 65536) == (8, 0)        # C3 at N = 1: 512 tiles -> 256 workgroups
+    assert tune(6041, 3707, 16, 3, 16384) == (4, 0)        # 256 tiles of 64 rows
+    assert tune(138494, 26745, 16, 3, 8192) == (8, 64)     # C4 at N = 8: per-row, dW0 4 x 8 tiles
+    assert tune(6041, 3707, 8, 3, 1024, waves=8) == (8, 8)
+    assert tune(6041, 3707, 8, 3, 1024, waves=4) == (4, 16)
+    assert tune(6041, 3707, 16, 3, 65536, waves=4) == (4, 0)
+    assert tune(138494, 26745, 16, 3, 8192, waves=1) == (8, 64)  # no 1-wave kernel there
     assert lib.ncf_debug_set_geometry(5) != 0
