@@ -53,9 +53,9 @@ struct Shape {
         return (MLP && k >= 1) ? (S(k + 1) * S(k) + S(k + 1) + NTH - 1) / NTH : 0;
     }
     // su[2], si[2], labels[2] (double-buffered tile indices), zgmf, dz, teacher
-    // logits[2], then 128 floats of biases (each layer's padded to 16*MT) and 128 of
-    // predict weights
-    static constexpr int MISC = 12 * TR;
+    // logits[2] (10 floats per tile row), then 128 floats of biases (each layer's
+    // padded to 16*MT) and 128 of predict weights
+    static constexpr int MISC = 10 * TR + 256;
     // Two halves per wave whose roles (layer-0 staging / scatter scratch) alternate
     // with tile parity: the next tile's staging never overwrites rows a slow wave
     // still reads, so there is no tile-end barrier (if the LDS budget allows).

@@ -105,6 +105,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     float* sB = stl2 + 2 * TRW;    // biases, layer k at boff(k), zero-padded
     float* sWP = sB + 128;               // predict weights, zero-padded
     float* sstage = sWP + 128;           // union: per-wave staging | epilogue images
+    static_assert(10 * TRW + 256 == S_::MISC, "LDS carve-up must match Shape::MISC (the launch's LDS size)");
 
     const int tid = threadIdx.x;
     const int w = tid >> 6;
