@@ -399,7 +399,7 @@ def setup_engine(cfg, ds, train, world, rank, dev, group, global_batch, seed=0):
     np.random.seed(seed)
     torch.manual_seed(seed)
     model, dist = build_model(cfg, U, I, dev)
-    pipe = EpochPipeline(train, dev, global_batch, I, user_num=U, prefetch=True)
+    pipe = EpochPipeline(train, dev, global_batch, I, user_num=U, prefetch=True, canonical=world > 1)
     eng = TrainEngine(model, lr=1e-3, world_size=world, rank=rank, process_group=group,
                       distill=None if dist is None else dist.device_plan())
     eng.stream_buffers = pipe.buffers  # the pipeline alternates two: graphs captured for both up front

@@ -290,13 +290,15 @@ int ncf_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq
  * this rank's shard).  gshard holds the reduce-scattered flat gradient shard
  * [shard_begin, shard_begin + n): in its Um / Im rows the summed per-entity D0 sums
  * G (the step deferred their expansion), elsewhere the gradient itself.  The kernel
- * forms dUm / dIm of its rows as G W0[:, half] (W0 read from params_full) and runs
- * Adam on the active ranges (shard-relative) of params (= params_full + shard_begin);
- * gshard is not cleared.  Fused path, factored layer 0 with dm <= 64 and
- * shard_begin a multiple of 64: NCF_E_UNSUPPORTED otherwise.  Loss bookkeeping as
- * ncf_adam_step (loss_slot shard-relative, or loss_hist NULL on the other ranks).
+ * forms dUm / dIm of its rows as G W0[:, half], W0 being the weights the step ran
+ * with (saved in the step's workspace: the same launch updates W0 when the shard
+ * holds it), and runs Adam on the active ranges (shard-relative) of params (the
+ * flat parameters + shard_begin); gshard is not cleared.  Fused path, factored layer
+ * 0 with dm <= 64 and shard_begin a multiple of 64: NCF_E_UNSUPPORTED otherwise.
+ * Loss bookkeeping as ncf_adam_step (loss_slot shard-relative, or loss_hist NULL on
+ * the other ranks).
  */
-int ncf_adam_step_fact(const ncf_layout *lay, const float *params_full, float *params, const float *gshard,
+int ncf_adam_step_fact(const ncf_layout *lay, const void *workspace, float *params, const float *gshard,
                        float *exp_avg, float *exp_avg_sq, const int64_t *ranges, int nranges, int64_t shard_begin,
                        ncf_step_ctl *ctl, double lr, double beta1, double beta2, double eps, int64_t loss_slot,
                        float *loss_hist, int64_t hist_len, void *stream);
@@ -412,6 +414,18 @@ int64_t ncf_prepare_epoch_workspace(int64_t n, int64_t batch_global, int item_nu
 int ncf_prepare_epoch(const uint64_t *rows, const int64_t *perm, int64_t n, int64_t batch_global,
                       int item_num, uint64_t *rows_out, void *workspace, int64_t workspace_bytes,
                       void *stream);
+
+/*
+ * ncf_prepare_epoch with flags.  NCF_PREP_CANONICAL: the rows of each item inside a
+ * batch come out sorted by (user, label) -- a canonical order that does not depend
+ * on the placement order of the grouping, so every rank of a data-parallel group
+ * that builds the same epoch stream gets the same rows in the same positions (rank r
+ * takes positions [r per, (r + 1) per) of each global batch).  Batches below 4,096
+ * rows are not grouped (the shuffle alone is deterministic).  Same workspace.
+ */
+#define NCF_PREP_CANONICAL 0x1
+int ncf_prepare_epoch2(const uint64_t *rows, const int64_t *perm, int64_t n, int64_t batch_global, int item_num,
+                       int flags, uint64_t *rows_out, void *workspace, int64_t workspace_bytes, void *stream);
 
 /*
  * User order of an epoch stream (since ABI 12): each global batch b of rows[0 .. n)

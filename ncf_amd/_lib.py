@@ -34,6 +34,7 @@ PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 LAYOUT_PER_ROW_L0, LAYOUT_WG_SHIFT, LAYOUT_WG_MASK = 0x1, 8, 0xFFF  # ncf_layout.flags (ncf_layout_tune)
 LAYOUT_LAYERED = 0x2  # ncf_layout.flags: training on the layered path even where a fused kernel exists
 LAYOUT_GEO_SHIFT, LAYOUT_GEO_MASK = 20, 0x3  # ncf_layout.flags: fused-step geometry (0..3: 8, 4, 2, 1 waves)
+PREP_CANONICAL = 0x1  # ncf_prepare_epoch2 flags: canonical row order inside item runs (data parallel)
 PROBE_BLOCKS = 2048  # include/ncf_hip.h NCF_PROBE_BLOCKS (ncf_probe_gather_scatter's sink: x 256 floats)
 LAYOUT_FACT_DEFER_DX = 0x8  # ncf_layout.flags: factored step leaves G for ncf_adam_step_fact (sharded zero1)
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
@@ -103,6 +104,8 @@ _HIP_PROTOS = {
     "ncf_gather_epoch": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "ncf_prepare_epoch_workspace": (c_i64, [c_i64, c_i64, ctypes.c_int]),
     "ncf_prepare_epoch": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, ctypes.c_int, c_vp, c_vp, c_i64, c_vp]),
+    "ncf_prepare_epoch2": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_i64,
+                                          c_vp]),
     "ncf_hr_ndcg": (ctypes.c_int, [c_vp, c_vp, c_i64, ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp]),
     "ncf_fact_mode": (ctypes.c_int, [c_vp]),
     "ncf_reduce_rows": (ctypes.c_int, [c_vp]),

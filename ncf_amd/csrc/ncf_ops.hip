@@ -282,9 +282,9 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
 // The shard is 64-float aligned and DM divides 64, so a G row never straddles two
 // shards.  g is not cleared (the next reduce-scatter overwrites the shard).
 struct FactShard {
-    const float* prm;      // full flat parameters (W0 rows)
+    const float* w0s;      // W0 as the step ran with it ([DM][2 DM], fact_w0_snap)
     int64_t um, im, nu, ni;  // table offsets and float counts (U * DM, I * DM)
-    int64_t w0, base;      // W0 offset; flat index of shard element 0
+    int64_t base;          // flat index of shard element 0
     int dm;
 };
 
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256) void adam_fact_kernel(float* __restrict__ p, c
             const int64_t row = rel / F.dm;
             const int col = (int)(rel - row * F.dm);
             const float* G = g + (i - col);  // the row's first float (same shard)
-            const float* W = F.prm + F.w0 + (isu ? 0 : F.dm) + col;
+            const float* W = F.w0s + (isu ? 0 : F.dm) + col;
             gg = f4{0.f, 0.f, 0.f, 0.f};
             for (int j = 0; j < F.dm; ++j) {
                 const float gj = G[j];
@@ -1027,10 +1027,45 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_parts_kernel(int* __restric
     }
 }
 
+// Canonical order of a batch's grouped rows (ncf_prepare_epoch2, NCF_PREP_CANONICAL):
+// the LDS-atomic placement leaves the rows of one item in arrival order, which
+// differs from run to run; data parallelism needs every rank's stream identical
+// (rank r takes rows [r per, (r + 1) per) of each global batch), so with the flag
+// each part is sorted by (item, user, label) -- a total order on the rows' values,
+// identical duplicates being interchangeable -- which keeps the item grouping.
+__device__ __forceinline__ uint64_t canon_key(uint64_t r) {
+    return (((r >> 32) & 0x7fffffffull) << 33) | ((r & 0xffffffffull) << 1) | (r >> 63);
+}
+// Ascending sort of a[0 .. n) in place by canon_key, one workgroup (any n): the
+// bitonic network in its all-ascending form (each merge stage starts with a flip
+// comparison i <-> i ^ (k - 1), then half-cleaners i <-> i + j), so positions past
+// n act as +infinity and are simply skipped.
+template <int NT, class T>
+__device__ void canon_sort(T* a, int n) {
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    for (int k = 2; k <= n2; k <<= 1) {
+        for (int j = k >> 1; j >= 1; j >>= 1) {
+            for (int q = threadIdx.x; q < (n2 >> 1); q += NT) {
+                const int i = (q / j) * 2 * j + (q % j);
+                const int p = j == (k >> 1) ? (i ^ (k - 1)) : i + j;  // flip, then half-cleaners
+                if (p < n) {
+                    const uint64_t x = a[i], y = a[p];
+                    if (canon_key(x) > canon_key(y)) {
+                        a[i] = y;
+                        a[p] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 __global__ __launch_bounds__(SORT_THREADS) void sort_part_kernel(const uint64_t* __restrict__ shuf,
                                                                  int* __restrict__ hist, const int* __restrict__ parts,
                                                                  int64_t n, int64_t B, int item_num, int P, int64_t nb,
-                                                                 uint64_t* __restrict__ out) {
+                                                                 uint64_t* __restrict__ out, int canon) {
     extern __shared__ uint64_t stg[];                       // [STAGE_ROWS]
     int* loff = reinterpret_cast<int*>(stg + STAGE_ROWS);  // [ITEM_CAP]
     const int tid = threadIdx.x;
@@ -1081,7 +1116,12 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_part_kernel(const uint64_t*
     }
     if (stage) {
         __syncthreads();
+        if (canon) canon_sort<SORT_THREADS>(stg, nrows);
         for (int e = tid; e < nrows; e += SORT_THREADS) ob[e] = stg[e];
+    } else if (canon) {  // the region in place in global memory (a part beyond the LDS stage)
+        __threadfence_block();
+        __syncthreads();
+        canon_sort<SORT_THREADS>(ob, nrows);
     }
 }
 
@@ -1456,7 +1496,7 @@ template <int DM>
 __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout lay, const float* __restrict__ prm,
                                                                      float* __restrict__ grads,
                                                                      float* __restrict__ partials, int nbu,
-                                                                     int dw0_only) {
+                                                                     int dw0_only, float* __restrict__ w0snap) {
     using X_ = FxShape<DM>;
     constexpr int CH = X_::CH, ST = X_::ST, NT = X_::NT, Q4 = X_::Q4, TPW = X_::TPW, cpb = X_::CPB;
     extern __shared__ __attribute__((aligned(16))) float fsm[];
@@ -1478,6 +1518,15 @@ __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout l
         const int e4 = tid + q * FX_WAVES * 64, j = e4 / Q4, k4 = e4 - j * Q4;
         wv[q] = e4 < NW4 ? *reinterpret_cast<const f4*>(prm + lay.w[0] + (int64_t)j * 2 * DM + koff + 4 * k4)
                          : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    // dW0-only mode: the first block of each table saves its W0 half (the weights this
+    // step ran with) for the sharded dX expansion of ncf_adam_step_fact
+    if (dw0_only && w0snap != nullptr && (blockIdx.x == 0 || (int)blockIdx.x == nbu)) {
+#pragma unroll
+        for (int q = 0; q < PW; ++q) {
+            const int e4 = tid + q * FX_WAVES * 64, j = e4 / Q4, k4 = e4 - j * Q4;
+            if (e4 < NW4) *reinterpret_cast<f4*>(w0snap + (int64_t)j * 2 * DM + koff + 4 * k4) = wv[q];
+        }
     }
     f4 accw[TPW];
 #pragma unroll
@@ -1668,6 +1717,17 @@ static float* fact_partials(const ncf_layout* lay, void* workspace) {
 // layered path's lyr_slab_rows.
 static int reduce_rows(const ncf_layout* lay) { return train_fused(lay) ? slab_rows_of(lay) : lyr_slab_rows(lay); }
 
+// NCF_LAYOUT_FACT_DEFER_DX: the W0 the step ran with ([DM][2 DM]), saved by the
+// expansion after the dW0 partials; ncf_adam_step_fact forms dX = G W0 half from it
+// while the same launch updates W0 itself (fused path, dm <= FACT_LDS_DM).
+static int64_t fact_w0_snap_floats(const ncf_layout* lay) {
+    const int64_t DM = fact_dm(lay);
+    return DM <= FACT_LDS_DM ? 2 * DM * DM : 0;
+}
+static float* fact_w0_snap(const ncf_layout* lay, void* workspace) {
+    return fact_partials(lay, workspace) + fact_partials_floats(lay);
+}
+
 static W0Part w0_part(const ncf_layout* lay, const void* workspace) {
     W0Part wp;
     memset(&wp, 0, sizeof(wp));
@@ -1680,7 +1740,7 @@ static W0Part w0_part(const ncf_layout* lay, const void* workspace) {
 }
 
 static int launch_fact_expand(const ncf_layout* lay, const float* params, float* grads, float* partials,
-                              hipStream_t st) {
+                              float* w0snap, hipStream_t st) {
     const int DM = lay->factor_num << (lay->num_layers - 1);
     if (DM > FACT_LDS_DM) return NCF_OK;  // expanded by the layered path itself (lyr_run)
     const void* fe;
@@ -1696,7 +1756,7 @@ static int launch_fact_expand(const ncf_layout* lay, const float* params, float*
     int nblk = fact_blocks(lay, &nbu);
     int dw0_only = (lay->flags & NCF_LAYOUT_FACT_DEFER_DX) ? 1 : 0;
     if (ensure_lds(fe, lds) != NCF_OK) return NCF_E_LAUNCH;
-    void* ae[] = {&l, (void*)&params, (void*)&grads, (void*)&partials, &nbu, &dw0_only};
+    void* ae[] = {&l, (void*)&params, (void*)&grads, (void*)&partials, &nbu, &dw0_only, (void*)&w0snap};
     if (hipLaunchKernel(fe, dim3((unsigned)nblk), dim3(FX_WAVES * 64), ae, (size_t)lds, st) != hipSuccess)
         return NCF_E_LAUNCH;
     return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
@@ -1815,7 +1875,8 @@ int ncf_supported(int mode, int F, int L) {
 int64_t ncf_workspace_bytes(const ncf_layout* lay, int64_t rows) {
     if (!lay || rows < 0) return -1;
     if (train_fused(lay))
-        return ((int64_t)SLAB_ROWS * ncf_slab_stride(lay) + (fact_mode(lay) ? fact_partials_floats(lay) : 0)) * 4;
+        return ((int64_t)SLAB_ROWS * ncf_slab_stride(lay) +
+                (fact_mode(lay) ? fact_partials_floats(lay) + fact_w0_snap_floats(lay) : 0)) * 4;
     return lyr_workspace_floats(lay, rows, true, fact_mode(lay) ? fact_partials_floats(lay) : -1) * 4;
 }
 
@@ -1860,7 +1921,7 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
         la.fact_part_floats = fact_mode(lay) ? fact_partials_floats(lay) : -1;
         const int rc = lyr_run(la, slab, rows_max, true, (hipStream_t)stream);
         if (rc != NCF_OK || la.fact_part_floats < 0) return rc;
-        return launch_fact_expand(lay, params, grads, fact_partials(lay, workspace), (hipStream_t)stream);
+        return launch_fact_expand(lay, params, grads, fact_partials(lay, workspace), nullptr, (hipStream_t)stream);
     }
     const int geo = train_geo(e, lay);
     const int64_t lds = train_lds_floats(e, lay, geo) * 4;
@@ -1894,7 +1955,8 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
     const int rc = launch_status();
     if (rc != NCF_OK || !fact_mode(lay)) return rc;
     // factored layer 0: the per-user / per-item D0 sums -> dUm, dIm, dW0 partials
-    return launch_fact_expand(lay, params, grads, fact_partials(lay, workspace), (hipStream_t)stream);
+    return launch_fact_expand(lay, params, grads, fact_partials(lay, workspace), fact_w0_snap(lay, workspace),
+                              (hipStream_t)stream);
 }
 
 int ncf_train_step(const ncf_layout* lay, const float* params, float* grads, const uint64_t* rows,
@@ -2024,23 +2086,24 @@ int ncf_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
     return launch_status();
 }
 
-int ncf_adam_step_fact(const ncf_layout* lay, const float* params_full, float* params, const float* gshard,
+int ncf_adam_step_fact(const ncf_layout* lay, const void* workspace, float* params, const float* gshard,
                        float* exp_avg, float* exp_avg_sq, const int64_t* ranges, int nranges, int64_t shard_begin,
                        ncf_step_ctl* ctl, double lr, double beta1, double beta2, double eps, int64_t loss_slot,
                        float* loss_hist, int64_t hist_len, void* stream) {
-    if (!lay || !params_full || !params || !gshard || !exp_avg || !exp_avg_sq || !ranges || !ctl) return NCF_E_ARG;
+    if (!lay || !workspace || !params || !gshard || !exp_avg || !exp_avg_sq || !ranges || !ctl) return NCF_E_ARG;
     const int dm = fact_dm(lay);
-    if (!fact_mode(lay) || dm > 64 || (shard_begin & 63)) return NCF_E_UNSUPPORTED;
+    if (!fact_mode(lay) || !train_fused(lay) || dm > 64 || (shard_begin & 63) ||
+        !(lay->flags & NCF_LAYOUT_FACT_DEFER_DX))
+        return NCF_E_UNSUPPORTED;
     int err = 0;
     Ranges R = make_ranges(ranges, nranges, &err);
     if (err) return NCF_E_ARG;
     FactShard F;
-    F.prm = params_full;
+    F.w0s = fact_w0_snap(lay, const_cast<void*>(workspace));
     F.um = lay->um;
     F.im = lay->im;
     F.nu = (int64_t)lay->user_num * dm;
     F.ni = (int64_t)lay->item_num * dm;
-    F.w0 = lay->w[0];
     F.base = shard_begin;
     F.dm = dm;
     const int64_t total = R.prefix[R.n];
@@ -2384,7 +2447,13 @@ int64_t ncf_prepare_epoch_workspace(int64_t n, int64_t batch_global, int item_nu
 
 int ncf_prepare_epoch(const uint64_t* rows, const int64_t* perm, int64_t n, int64_t batch_global, int item_num,
                       uint64_t* rows_out, void* workspace, int64_t workspace_bytes, void* stream) {
+    return ncf_prepare_epoch2(rows, perm, n, batch_global, item_num, 0, rows_out, workspace, workspace_bytes, stream);
+}
+
+int ncf_prepare_epoch2(const uint64_t* rows, const int64_t* perm, int64_t n, int64_t batch_global, int item_num,
+                       int flags, uint64_t* rows_out, void* workspace, int64_t workspace_bytes, void* stream) {
     if (!rows || !perm || !rows_out || !workspace || n < 0 || batch_global <= 0 || item_num <= 0) return NCF_E_ARG;
+    if (flags & ~NCF_PREP_CANONICAL) return NCF_E_ARG;
     if (batch_global > 0x7fffffff) return NCF_E_ARG;
     if (workspace_bytes < ncf_prepare_epoch_workspace(n, batch_global, item_num)) return NCF_E_ARG;
     if (n == 0) return NCF_OK;
@@ -2418,7 +2487,7 @@ int ncf_prepare_epoch(const uint64_t* rows, const int64_t* perm, int64_t n, int6
     if (ensure_lds(reinterpret_cast<const void*>(&sort_part_kernel), SORT_LDS) != NCF_OK) return NCF_E_LAUNCH;
     const int64_t g3 = P >= 8 ? ((nb + 7) / 8) * 8 * P : nb * P;
     hipLaunchKernelGGL(sort_part_kernel, dim3((unsigned)g3), dim3(SORT_THREADS), (size_t)SORT_LDS, st, shuf, hist,
-                       parts, n, batch_global, item_num, P, nb, rows_out);
+                       parts, n, batch_global, item_num, P, nb, rows_out, (flags & NCF_PREP_CANONICAL) ? 1 : 0);
     return launch_status();
 }
 

@@ -492,7 +492,7 @@ class TrainEngine:
             hist = self.loss_hist.data_ptr()
         p, g = self._opt_ptrs
         if self._fact_shard:  # the shard's G rows expanded inside the optimizer launch
-            L.check(lib.ncf_adam_step_fact(ctypes.byref(self.lay), self.flat.data_ptr(), p, g, self.exp_avg.data_ptr(),
+            L.check(lib.ncf_adam_step_fact(ctypes.byref(self.lay), self.ws.data_ptr(), p, g, self.exp_avg.data_ptr(),
                                            self.exp_avg_sq.data_ptr(), ranges, nr, self.rank * self.shard,
                                            self.ctl.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps,
                                            self._loss_slot, hist, hist_len, st), "ncf_adam_step_fact")

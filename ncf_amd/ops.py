@@ -148,12 +148,15 @@ def pack_rows_host(users, items, labels=None):
 
 class EpochPrep:
     """ncf_prepare_epoch with its device workspace kept between epochs (stable
-    pointers, so the output can feed a captured step graph)."""
+    pointers, so the output can feed a captured step graph).  canonical: the rows
+    of one item inside a batch in (user, label) order (NCF_PREP_CANONICAL), so that
+    every data-parallel rank building the stream gets the same positions."""
 
-    def __init__(self, device):
+    def __init__(self, device, canonical=False):
         self.device = torch.device(device)
         self.ws = None
         self.out = None
+        self.canonical = bool(canonical)
 
     def __call__(self, rows, perm, batch_size, item_num, out=None):
         """On the current stream; into `out` (n int64 on the device) if given."""
@@ -169,9 +172,10 @@ class EpochPrep:
             out = self.out
         elif out.numel() != n or out.dtype != torch.int64 or not out.is_contiguous():
             raise ValueError("prepare_epoch out: n contiguous int64")
-        L.check(L.hip().ncf_prepare_epoch(rows.data_ptr(), perm.data_ptr(), n, int(batch_size), int(item_num),
-                                          out.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
-                                          L.stream_ptr(self.device)), "ncf_prepare_epoch")
+        L.check(L.hip().ncf_prepare_epoch2(rows.data_ptr(), perm.data_ptr(), n, int(batch_size), int(item_num),
+                                           L.PREP_CANONICAL if self.canonical else 0, out.data_ptr(),
+                                           self.ws.data_ptr(), self.ws.numel(), L.stream_ptr(self.device)),
+                "ncf_prepare_epoch2")
         return out
 
 

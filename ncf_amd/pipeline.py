@@ -112,7 +112,11 @@ class EpochPipeline:
     """depth: epochs staged ahead (host draws, uploads and device build); slots =
     depth + 1 sets of buffers, one being trained from."""
 
-    def __init__(self, dataset, device, batch_size, item_num, user_num=None, prefetch=True, depth=None):
+    def __init__(self, dataset, device, batch_size, item_num, user_num=None, prefetch=True, depth=None,
+                 canonical=False):
+        """canonical: rows of one item inside a batch in (user, label) order
+        (ncf_prepare_epoch2 NCF_PREP_CANONICAL) -- every rank of a data-parallel group
+        then builds the identical stream (set for world > 1)."""
         self.ds = dataset
         self.device = torch.device(device)
         self.batch_size = int(batch_size)
@@ -141,7 +145,7 @@ class EpochPipeline:
         self.rows = torch.empty(self.n, dtype=torch.int64, device=dev)
         self.perm = torch.empty(self.n, dtype=torch.int64, device=dev)
         self.fy_ws = torch.empty(int(L.hip().ncf_randperm_workspace(self.n)), dtype=torch.uint8, device=dev)
-        self.prep = ops.EpochPrep(dev)
+        self.prep = ops.EpochPrep(dev, canonical=canonical)
         # per slot
         self._out = [torch.empty(self.n, dtype=torch.int64, device=dev) for _ in range(K)]
         self._neg_host = [torch.empty(max(1, self.S), dtype=torch.int32).pin_memory() for _ in range(K)]

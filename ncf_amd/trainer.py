@@ -74,7 +74,7 @@ class Trainer:
             if self._pipe is None:
                 from .pipeline import EpochPipeline
                 self._pipe = EpochPipeline(self.ds, self.device, self.batch_size, int(self.model.item_num),
-                                                 user_num=int(self.model.user_num))
+                                           user_num=int(self.model.user_num), canonical=self.world_size > 1)
                 self.engine.stream_buffers = self._pipe.buffers  # step graphs captured for both
             # fit() evaluates after every epoch (one torch draw): the next epoch's
             # sampler seed is peeked past it
@@ -86,7 +86,7 @@ class Trainer:
         perm = epoch_permutation(n).to(self.device)
         if getattr(self, "_rows", None) is None or self._rows.numel() != n:
             self._rows = torch.empty(n, dtype=torch.int64, device=self.device)
-            self._prep = ops.EpochPrep(self.device)
+            self._prep = ops.EpochPrep(self.device, canonical=self.world_size > 1)
         # packed on the host (one int64 per row), one upload, shuffle+group on the device
         self._rows.copy_(torch.from_numpy(ops.pack_rows_host(u, i, y)))
         return self._prep(self._rows, perm, self.batch_size, int(self.model.item_num))

@@ -568,14 +568,24 @@ PREP_CASES = [(10007, 1000, 37, None), (65536 * 2 + 123, 65536, 3707, None), (50
               (20000, 256, 3707, None), (99999, 33333, 999, 0.05)]
 
 
+def _canon_keys(r):
+    r = r.astype(np.uint64)
+    return (((r >> np.uint64(32)) & np.uint64(0x7FFFFFFF)) << np.uint64(33)) | \
+        ((r & np.uint64(0xFFFFFFFF)) << np.uint64(1)) | (r >> np.uint64(63))
+
+
+@pytest.mark.parametrize("canonical", [False, True])
 @pytest.mark.parametrize("n,bs,n_items,hot", PREP_CASES)
-def test_prepare_epoch_batches_grouped_by_item(n, bs, n_items, hot):
-    """Per batch: same rows as the plain shuffle (DataLoader membership), grouped by item."""
+def test_prepare_epoch_batches_grouped_by_item(n, bs, n_items, hot, canonical):
+    """Per batch: same rows as the plain shuffle (DataLoader membership), grouped by
+    item; canonical (NCF_PREP_CANONICAL, data parallelism): exactly the batch's rows
+    sorted by (item, user, label) -- staged parts and a hot item's part beyond the LDS
+    stage (hot 0.4) alike -- so every rank building the stream gets the same one."""
     from ncf_amd import ops
     rng = np.random.default_rng(n + bs)
     rows = _rand_rows(rng, n, 500, n_items, hot=hot)
     perm = torch.randperm(n, device=DEV)
-    prep = ops.EpochPrep(DEV)
+    prep = ops.EpochPrep(DEV, canonical=canonical)
     out = prep(rows, perm, bs, n_items)
     torch.cuda.synchronize()
     exp = rows[perm].cpu().numpy()
@@ -585,6 +595,9 @@ def test_prepare_epoch_batches_grouped_by_item(n, bs, n_items, hot):
         gi = (got[sl] >> 32) & 0x7FFFFFFF
         if bs >= 4096:  # smaller batches are shuffled only (include/ncf_hip.h)
             assert (np.diff(gi) >= 0).all(), "batch not grouped by item"
+            if canonical:
+                e = exp[sl]
+                assert np.array_equal(got[sl], e[np.argsort(_canon_keys(e), kind="stable")]), "not canonical"
         else:
             assert np.array_equal(got[sl], exp[sl])
         assert np.array_equal(np.sort(exp[sl]), np.sort(got[sl])), "batch membership changed"
