@@ -822,8 +822,9 @@ def main():
                              "MALL-assisted (tables and optimizer state fit the 256 MB MALL)" if state_mb <= 256 else
                              "HBM (model state above the 256 MB MALL)"),
                 "note": "achieved = the step launch group's gather+scatter algorithmic bytes (roofline_hbm) / its "
-                        "time; peak = ncf_probe_gather_scatter: the same gathers and float-atomic adds, same rows "
-                        "and tables, no arithmetic, launches back to back"}
+                        "time; peak = ncf_probe_gather_scatter: the same 16-byte row gathers and row-contiguous "
+                        "float-atomic adds (one per float: the step also sums item runs first), same rows and "
+                        "tables, no arithmetic, launches back to back -- the rate of the access pattern alone"}
 
     # ---- weak scaling (extra field): global batch x N, per-GPU batch fixed -----
     weak = None

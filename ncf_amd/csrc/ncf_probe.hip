@@ -24,39 +24,42 @@ struct ProbeArgs {
     int f, dm, mode;
 };
 
-// One thread per 16-byte piece of a row's four embedding rows: the pieces of a batch
-// row are consecutive threads (E4 = (2f + 2dm) / 4 of them), so each table row is one
-// contiguous run of lanes -- the step kernel's coalescing.
+// Gather: one thread per 16-byte piece of a row's four embedding rows (E4 = (2f +
+// 2dm) / 4 consecutive threads per batch row: each table row one contiguous run of
+// lanes, the step kernel's coalescing).  Scatter: one thread per float, so one atomic
+// wave-instruction adds 64 consecutive floats of a row (the step's row-contiguous
+// atomics; it also sums runs of equal items first, which this probe does not).
 __global__ __launch_bounds__(256) void probe_gs_kernel(ProbeArgs a) {
-    const int e4n = (2 * a.f + 2 * a.dm) / 4;
-    const int64_t total = a.n * e4n;
-    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = q / e4n;
-        const int e = (int)(q - r * e4n) * 4;
+    const int en = 2 * a.f + 2 * a.dm;
+    const int e4n = en / 4;
+    const int64_t nt = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    auto offset = [&](int64_t r, int e) {
         const uint64_t pr = a.rows[r];
         const int64_t u = (int64_t)(uint32_t)pr, it = (int64_t)((pr >> 32) & 0x7fffffffu);
-        int64_t off;
-        if (e < a.f) off = a.ug + u * a.f + e;
-        else if (e < 2 * a.f) off = a.ig + it * a.f + (e - a.f);
-        else if (e < 2 * a.f + a.dm) off = a.um + u * a.dm + (e - 2 * a.f);
-        else off = a.im + it * a.dm + (e - 2 * a.f - a.dm);
-        f4 v = f4{1e-30f, 1e-30f, 1e-30f, 1e-30f};
-        if (a.mode & 1) {
-            v = *reinterpret_cast<const f4*>(a.prm + off);
+        if (e < a.f) return a.ug + u * a.f + e;
+        if (e < 2 * a.f) return a.ig + it * a.f + (e - a.f);
+        if (e < 2 * a.f + a.dm) return a.um + u * a.dm + (e - 2 * a.f);
+        return a.im + it * a.dm + (e - 2 * a.f - a.dm);
+    };
+    if (a.mode & 1) {
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+        for (int64_t q = t0; q < a.n * e4n; q += nt) {
+            const int64_t r = q / e4n;
+            const f4 v = *reinterpret_cast<const f4*>(a.prm + offset(r, (int)(q - r * e4n) * 4));
             acc.x += v.x;
             acc.y += v.y;
             acc.z += v.z;
             acc.w += v.w;
         }
-        if (a.mode & 2) {
-            atomicAdd(a.grads + off, v.x);
-            atomicAdd(a.grads + off + 1, v.y);
-            atomicAdd(a.grads + off + 2, v.z);
-            atomicAdd(a.grads + off + 3, v.w);
+        a.sink[t0] = acc.x + acc.y + acc.z + acc.w;
+    }
+    if (a.mode & 2) {
+        for (int64_t q = t0; q < a.n * en; q += nt) {
+            const int64_t r = q / en;
+            atomicAdd(a.grads + offset(r, (int)(q - r * en)), 1e-30f);
         }
     }
-    if (a.mode & 1) a.sink[(int64_t)blockIdx.x * blockDim.x + threadIdx.x] = acc.x + acc.y + acc.z + acc.w;
 }
 
 }  // namespace ncf

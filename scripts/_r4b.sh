@@ -2,14 +2,17 @@ set -u
 cd $GRAFT_REPO_ROOT
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4b_smoke.log 2>&1 || exit 1
-timeout -k 10 800 python -u -m pytest -x -v --timeout 500 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_parity.py -k "geometry_vs_oracle or tuned_launch" > gpurun_out/r4b_tests1.log 2>&1 || exit 1
-timeout -k 10 800 python -u -m pytest -x -v --timeout 500 --timeout-method thread -p no:cacheprovider \
+fault() { grep -qE "illegal memory access|hipErrorIllegalAddress|Memory access fault|GPU Hang|core dumped" "$1"; }
+timeout -k 10 800 python -u -m pytest -v -s --timeout 500 --timeout-method thread -p no:cacheprovider \
+  tests/test_gpu_parity.py -k "prepare_epoch or geometry_vs_oracle" \
   tests/test_gpu_multirank_fullsize.py tests/test_gpu_multirank.py::test_two_ranks_match_single_rank \
-  tests/test_gpu_trainer.py::test_trainer_matches_reference_script tests/test_gpu_lazy_adam.py > gpurun_out/r4b_tests2.log 2>&1 || exit 1
+  tests/test_gpu_trainer.py::test_trainer_matches_reference_script tests/test_gpu_lazy_adam.py > gpurun_out/r4b_tests2.log 2>&1
+rc=$?; echo "tests2 rc=$rc"; fault gpurun_out/r4b_tests2.log && exit 90
+[ $rc -gt 1 ] && exit $rc
 for w in 8 4; do
   NCF_WG_WAVES=$w timeout -k 10 200 python scripts/dp_modes.py c3 8 allreduce,zero1 > gpurun_out/r4b_dp_c3_w$w.json 2>&1 || exit 1
+done
+for w in 8 4 2 1; do
   NCF_WG_WAVES=$w timeout -k 10 200 python bench.py --config c2 --steps 2000 --warmup 200 --skip-cpu-baseline --e2e-epochs 0 > gpurun_out/r4b_c2_w$w.json 2>&1 || exit 1
 done
 timeout -k 10 300 python bench.py --steps 20 --skip-cpu-baseline --e2e-epochs 0 > gpurun_out/r4b_c3.json 2>&1 || exit 1

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Projected 1/2/4/8-GPU step times from measured per-rank local costs.
+
+The one-GPU pool cannot run the N-rank RCCL transport, so the curve is projected:
+
+    T(N) = local(N) + exchange(N)
+
+* local(N): the graph-replayed per-rank step measured on one MI355X with the engine
+  as rank 0 of an emulated world N (scripts/dp_modes.py: its shard of every global
+  batch, the real launches, a one-rank group whose collectives move nothing), taken
+  from the dp_modes JSON files given on the command line;
+* exchange(N): the collectives of the mode on the wire, modelled as ring collectives
+  over xGMI -- per collective  alpha + (N - 1) / N * S / B  for a reduce-scatter or an
+  all-gather of S bytes, twice that volume for an all-reduce -- with B the per-link
+  xGMI bandwidth (7 links x ~153 GB/s per MI355X: a ring is per-link bound; the
+  task's stated figure, not measured here) and alpha a per-collective latency
+  (RCCL launch + ring steps; an assumption, varied over --alpha).
+
+Usage: scaling_model.py OUT.json dp_modes_c3_n2.json dp_modes_c3_n4.json ...
+(N = 1 is the single-process bench value, --n1-us per config)."""
+import argparse
+import json
+
+
+def exchange_us(mode, n, floats, packed_floats, b_gbs, alpha_us):
+    if n == 1:
+        return 0.0
+    s = 4.0 * floats
+    ring = (n - 1) / n
+    if mode == "allreduce":
+        return alpha_us + 2 * ring * s / (b_gbs * 1e3)
+    if mode == "touched":
+        return alpha_us + 2 * ring * 4.0 * packed_floats / (b_gbs * 1e3)
+    if mode == "zero1":  # reduce-scatter + all-gather: one all-reduce's bytes, two collectives
+        return 2 * alpha_us + 2 * ring * s / (b_gbs * 1e3)
+    raise ValueError(mode)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("inputs", nargs="+")
+    ap.add_argument("--bw", type=float, default=153.0, help="xGMI GB/s per link (ring bound)")
+    ap.add_argument("--alpha", type=float, nargs="+", default=[10.0, 25.0], help="us per collective")
+    ap.add_argument("--n1-us", type=json.loads, default={"c3": 55.9, "c4": 126.0},
+                    help="single-process us/step per config (bench lines)")
+    ap.add_argument("--floats", type=json.loads, default={"c3": 790737, "c4": 13230017})
+    ap.add_argument("--packed", type=json.loads, default={"c3": 790737, "c4": 7400000},
+                    help="touched-mode packed floats per step (DESIGN §6 table)")
+    ap.add_argument("--batch", type=int, default=65536)
+    a = ap.parse_args()
+    rows = []
+    for path in a.inputs:
+        txt = open(path).read().strip().splitlines()
+        d = json.loads([line for line in txt if line.startswith("{")][-1])
+        cfg, n = d["config"], int(d["world_emulated"])
+        for mode, m in d["modes"].items():
+            local = 1e3 * m["ms_per_step_graph"]
+            # the emulated collectives (one-rank group / exact all-reduce forms) are not wire time
+            emu = sum(1e3 * v for k, v in m["launch_groups_ms"].items()
+                      if k in ("allreduce", "reduce_scatter", "all_gather"))
+            for alpha in a.alpha:
+                t = local - emu + exchange_us(mode, n, a.floats[cfg], a.packed[cfg], a.bw, alpha)
+                rows.append({"config": cfg, "n_gpus": n, "mode": mode, "alpha_us": alpha, "local_us": round(local - emu, 1),
+                             "exchange_us": round(t - local + emu, 1), "step_us": round(t, 1),
+                             "interactions_per_s": a.batch / (t * 1e-6),
+                             "vs_1gpu": a.n1_us[cfg] / t})
+    for cfg, us in a.n1_us.items():
+        rows.append({"config": cfg, "n_gpus": 1, "mode": "single", "alpha_us": 0, "local_us": us, "exchange_us": 0,
+                     "step_us": us, "interactions_per_s": a.batch / (us * 1e-6), "vs_1gpu": 1.0})
+    json.dump({"model": "T(N) = local(N) + ring collectives over xGMI", "bw_GBps_per_link": a.bw, "rows": rows},
+              open(a.out, "w"), indent=1)
+    for r in sorted(rows, key=lambda r: (r["config"], r["n_gpus"], r["mode"], r["alpha_us"])):
+        print(f"{r['config']} N={r['n_gpus']} {r['mode']:9s} a={r['alpha_us']:4.0f}  local {r['local_us']:7.1f}  "
+              f"xchg {r['exchange_us']:7.1f}  step {r['step_us']:7.1f} us  {r['interactions_per_s'] / 1e9:6.3f} G/s  "
+              f"x{r['vs_1gpu']:.2f}")
+
+
+if __name__ == "__main__":
+    main()
