@@ -21,7 +21,10 @@
 extern "C" {
 #endif
 
-#define NCF_ABI_VERSION 14
+/* 15: ncf_layout.flags gains the fused step's workgroup geometry (NCF_LAYOUT_GEO_*) and
+ * NCF_LAYOUT_FACT_DEFER_DX; new ncf_adam_step_fact, ncf_prepare_epoch2
+ * (NCF_PREP_CANONICAL), ncf_probe_gather_scatter, ncf_debug_set_geometry. */
+#define NCF_ABI_VERSION 15
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
