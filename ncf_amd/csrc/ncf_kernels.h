@@ -67,7 +67,12 @@ struct Shape {
     static constexpr bool ALT0 = MLP && ALT0_FITS;
 #endif
     static constexpr bool END_BARRIER = !ALT0;
-    static constexpr int WAVE_STAGE = ALT0 ? 2 * HALF0 : ST0 + SCR;
+    // OWN0 (small towers, dW0 at most 8 16x16 tiles): the per-row layer-0 wgrad from
+    // each wave's own rows in registers, like layers k >= 1 (ncf_train.hip) -- no
+    // cross-wave staging or barrier in the tile; its epilogue image needs rwk(0)
+    static constexpr bool OWN0 = MLP && MT(0) * KT(0) <= 8;
+    static constexpr int WAVE_STAGE_BASE = ALT0 ? 2 * HALF0 : ST0 + SCR;
+    static constexpr int WAVE_STAGE = (OWN0 && rwk(0) > WAVE_STAGE_BASE) ? rwk(0) : WAVE_STAGE_BASE;
     static_assert(!MLP || L < 2 || rwk(1) <= WAVE_STAGE, "epilogue wgrad image exceeds the staging region");
     __host__ __device__ static constexpr int boff(int k) { return k == 0 ? 0 : boff(k - 1) + 16 * MT(k - 1); }
     static_assert(!MLP || boff(L) <= 128, "bias LDS region");

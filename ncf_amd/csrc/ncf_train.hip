@@ -246,6 +246,11 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     // per-row layer-0 wgrad: each wave owns the 16-column blocks nt = w + j * NWV of
     // dW0 (j < CB0; one block at 8 waves, several in narrow workgroups)
     constexpr int CB0 = S_::MLP && !FACT ? (KT0 + NWV - 1) / NWV : 1;
+    // OWN0: layer 0's wgrad from the wave's own rows (Shape::OWN0), no staging barrier
+    constexpr bool OWN0 = S_::OWN0 && !FACT && !FWD_ONLY;
+    f4 accL0[OWN0 ? MT0 * KT0 : 1];
+#pragma unroll
+    for (int t = 0; t < (OWN0 ? MT0 * KT0 : 1); ++t) accL0[t] = f4{0.f, 0.f, 0.f, 0.f};
     f4 accW0[CB0][MT0];     // dW_0 tiles (mt, nt = w + j * NWV)
     float dbAcc[L];
     f4 dWpT[MTL];
@@ -319,7 +324,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     // fragments requested early in the tile -- MLP rows right after this tile's
     // forward has consumed X0, GMF rows after the GMF backward -- so they land long
     // before the next tile needs them instead of in its first phase.
-    constexpr bool EARLY = FACT && !FWD_ONLY;
+    constexpr bool EARLY = (FACT || OWN0) && !FWD_ONLY;
     // Item-side embedding gradients of a wave's 16 rows: rows of a tile are
     // grouped by item (ncf_prepare_epoch counting-sorts each batch by item), so
     // consecutive equal items are summed in LDS and each item segment issues one
@@ -523,8 +528,8 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         } else {
             // (d) layer-0 wgrad operand: X0 rows of the whole tile, columns 16*nt + c
             constexpr int DM = S_::DM;
-            float bx[CB0][S_::MLP && !FACT ? NWV * 4 : 1];
-            if constexpr (S_::MLP && !FACT) {
+            float bx[CB0][S_::MLP && !FACT && !OWN0 ? NWV * 4 : 1];
+            if constexpr (S_::MLP && !FACT && !OWN0) {
 #pragma unroll
                 for (int j = 0; j < CB0; ++j) {
                     const int ntj = w + j * NWV < KT0 ? w + j * NWV : KT0 - 1;
@@ -604,6 +609,65 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                     dWpT[mt].z += dz * h.z;
                     dWpT[mt].w += dz * h.w;
                 }
+                // layer-0 dX rows (orientation B: acc[nt] = C[i = row 4g+r][j = in-feature 16*nt + c])
+                // scattered into the Um / Im rows of the gradient buffer through the wave's
+                // scratch `scr`: item half segment-reduced (item_segments), user half
+                // transposed so each atomic wave-instruction adds whole contiguous rows
+                auto scatter_dx0 = [&](const f4 (&acc)[KT0], float* scr, const int* su, const int* si, int wr,
+                                       int l, int c, int g, const float (&gIg)[NI], int gf, int gq0) {
+                    constexpr int DM = S_::DM;
+                    if constexpr (DM >= 16) {  // the split is 16-column aligned
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                            for (int nt = DM / 16; nt < KT0; ++nt)
+                                scr[(4 * g + r) * S_::SCM + 16 * nt + c - DM] = lane_get(acc[nt], r);
+                        }
+                        item_segments(scr, a, su, si, wr, l, gIg, gf, gq0);
+                        // user half: transpose through the (now free) scratch so each
+                        // atomic wave-instruction adds whole contiguous rows
+                        // (min(DM, 64) floats per row) instead of 4 rows x 64 B
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                            for (int nt = 0; nt < DM / 16; ++nt)
+                                scr[(4 * g + r) * S_::SCM + 16 * nt + c] = lane_get(acc[nt], r);
+                        }
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        constexpr int RPW = DM >= 64 ? 1 : 64 / DM;  // rows per wave-instruction
+                        constexpr int FPI = DM >= 64 ? 64 : DM;
+                        constexpr int NQ = 16 / RPW, NF = DM / FPI;
+                        // read every value first (one LDS wait), then the atomics back to back
+                        float uv[NQ][NF];
+                        int uid[NQ];
+#pragma unroll
+                        for (int qi = 0; qi < NQ; ++qi) {
+                            const int q = qi * RPW + l / FPI;
+                            uid[qi] = max(su[wr + q], 0);
+#pragma unroll
+                            for (int fi = 0; fi < NF; ++fi) uv[qi][fi] = scr[q * S_::SCM + fi * FPI + l % FPI];
+                        }
+#pragma unroll
+                        for (int qi = 0; qi < NQ; ++qi) {
+#pragma unroll
+                            for (int fi = 0; fi < NF; ++fi) {
+                                const int f = fi * FPI + l % FPI;
+                                if (!DIAG_ON(a, DIAG_NO_USER_SCATTER))
+                                    atomicAdd(a.grads + lay.um + (int64_t)uid[qi] * DM + f, uv[qi][fi]);
+                            }
+                        }
+                    } else {  // DM == 8: one 16-column tile, lanes c < 8 user, c >= 8 item
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (c >= DM) scr[(4 * g + r) * S_::SCM + c - DM] = lane_get(acc[0], r);
+                        item_segments(scr, a, su, si, wr, l, gIg, gf, gq0);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int uu = max(su[wr + 4 * g + r], 0);
+                            if (c < DM) atomicAdd(a.grads + lay.um + (int64_t)uu * DM + c, lane_get(acc[0], r));
+                        }
+                    }
+                };
                 static_for<L>([&](auto ii) {
                     constexpr int k = L - 1 - decltype(ii)::value;
                     if constexpr (k >= 1) {
@@ -724,6 +788,73 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                             }
                         }
                         stamp(a, sb + 5 + 3 * (L - 1));
+                    } else if constexpr (OWN0) {
+                        // layer 0, per row, small tower (Shape::OWN0): the wgrad from this
+                        // wave's own 16 rows like layers k >= 1 (selector-MFMA transposes,
+                        // dW0 tiles in registers, summed over the waves in the epilogue),
+                        // db0 from the transposed D0, the dgrad in orientation B, then the
+                        // scatter -- nothing staged across waves, no workgroup barrier
+                        // (the next tile's ids and fragments come EARLY, as in FACT).
+                        stamp(a, sb + 3 + 3 * (L - 1));
+                        if (!(a.diag & DIAG_NO_WGRAD)) {
+                            float sel[4];
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) sel[q] = c == 4 * g + q ? 1.f : 0.f;
+                            auto tr16 = [&](const f4& x) {
+                                f4 y = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) y = MFMA4(lane_get(x, q), sel[q], y);
+                                return y;
+                            };
+                            f4 DB[MT0];
+#pragma unroll
+                            for (int mt = 0; mt < MT0; ++mt) {
+                                DB[mt] = tr16(D[0][mt]);
+                                // lane (c, g): rows 4g .. 4g+3 of feature 16mt + c; the sum over
+                                // g lands on every lane, lane 16g + c keeps feature 16g + c
+                                float sdb = (DB[mt].x + DB[mt].y) + (DB[mt].z + DB[mt].w);
+                                sdb += shfl_xor(sdb, 16);
+                                sdb += shfl_xor(sdb, 32);
+                                if (g == mt) dbAcc[0] += sdb;
+                            }
+#pragma unroll
+                            for (int t = 0; t < KT0; ++t) {
+                                const f4 HB = tr16(H[0][t]);
+#pragma unroll
+                                for (int mt = 0; mt < MT0; ++mt) {
+                                    f4& acc = accL0[mt * KT0 + t];
+#pragma unroll
+                                    for (int q = 0; q < 4; ++q) acc = MFMA4(lane_get(DB[mt], q), lane_get(HB, q), acc);
+                                }
+                            }
+                        }
+                        const float* Ws = sW + S_::woff(0);
+                        f4 acc[KT0];
+#pragma unroll
+                        for (int nt = 0; nt < KT0; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int t = 0; t < S_::MT(0); ++t) {
+                            const f4 dv = D[0][t];
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const float av = lane_get(dv, r);
+#pragma unroll
+                                for (int nt = 0; nt < KT0; ++nt) {
+                                    const float wv = Ws[(16 * t + 4 * g + r) * S_::SW(0) + 16 * nt + c];
+                                    acc[nt] = MFMA4(av, wv, acc[nt]);
+                                }
+                                __builtin_amdgcn_sched_barrier(0);
+                            }
+                        }
+                        // the next tile's fragments and rows (requested EARLY) are waited for
+                        // here, before the scatter atomics (see the FACT branch)
+                        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                        npr = npr2;
+                        ndl = ndl2;
+                        nok = nok2;
+                        stamp(a, sb + 4 + 3 * (L - 1));
+                        scatter_dx0(acc, sstage + w * S_::WAVE_STAGE, su, si, wr, l, c, g, gIg, gf, gq0);
+                        stamp(a, sb + 5 + 3 * (L - 1));
                     } else {
                         // layer 0: its wgrad needs every row of the tile -> stage this
                         // wave's D_0 rows (half titer & 1 when ALT0) and publish the next
@@ -816,57 +947,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                         // user half -> unconditional atomics (padding rows add 0 to row 0)
                         // scratch: the half / region not holding this tile's layer-0 staging
                         float* scr = sstage + w * S_::WAVE_STAGE + (S_::ALT0 ? ((titer & 1) ? 0 : S_::HALF0) : S_::ST0);
-                        if constexpr (DM >= 16) {  // the split is 16-column aligned
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-#pragma unroll
-                                for (int nt = DM / 16; nt < KT0; ++nt)
-                                    scr[(4 * g + r) * S_::SCM + 16 * nt + c - DM] = lane_get(acc[nt], r);
-                            }
-                            item_segments(scr, a, su, si, wr, l, gIg, gf, gq0);
-                            // user half: transpose through the (now free) scratch so each
-                            // atomic wave-instruction adds whole contiguous rows
-                            // (min(DM, 64) floats per row) instead of 4 rows x 64 B
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-#pragma unroll
-                                for (int nt = 0; nt < DM / 16; ++nt)
-                                    scr[(4 * g + r) * S_::SCM + 16 * nt + c] = lane_get(acc[nt], r);
-                            }
-                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                            constexpr int RPW = DM >= 64 ? 1 : 64 / DM;  // rows per wave-instruction
-                            constexpr int FPI = DM >= 64 ? 64 : DM;
-                            constexpr int NQ = 16 / RPW, NF = DM / FPI;
-                            // read every value first (one LDS wait), then the atomics back to back
-                            float uv[NQ][NF];
-                            int uid[NQ];
-#pragma unroll
-                            for (int qi = 0; qi < NQ; ++qi) {
-                                const int q = qi * RPW + l / FPI;
-                                uid[qi] = max(su[wr + q], 0);
-#pragma unroll
-                                for (int fi = 0; fi < NF; ++fi) uv[qi][fi] = scr[q * S_::SCM + fi * FPI + l % FPI];
-                            }
-#pragma unroll
-                            for (int qi = 0; qi < NQ; ++qi) {
-#pragma unroll
-                                for (int fi = 0; fi < NF; ++fi) {
-                                    const int f = fi * FPI + l % FPI;
-                                    if (!DIAG_ON(a, DIAG_NO_USER_SCATTER))
-                                        atomicAdd(a.grads + lay.um + (int64_t)uid[qi] * DM + f, uv[qi][fi]);
-                                }
-                            }
-                        } else {  // DM == 8: one 16-column tile, lanes c < 8 user, c >= 8 item
-#pragma unroll
-                            for (int r = 0; r < 4; ++r)
-                                if (c >= DM) scr[(4 * g + r) * S_::SCM + c - DM] = lane_get(acc[0], r);
-                            item_segments(scr, a, su, si, wr, l, gIg, gf, gq0);
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                const int uu = max(su[wr + 4 * g + r], 0);
-                                if (c < DM) atomicAdd(a.grads + lay.um + (int64_t)uu * DM + c, lane_get(acc[0], r));
-                            }
-                        }
+                        scatter_dx0(acc, scr, su, si, wr, l, c, g, gIg, gf, gq0);
                         stamp(a, sb + 5 + 3 * (L - 1));
                         if (S_::WGRAD0_LATE && !wv_hi) wgrad0();
                     }
@@ -882,7 +963,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
             // the next tile's first cross-wave staging goes to the other region and
             // its first barrier resynchronises, so a wave still scattering overlaps
             // the others' next forward.
-            if constexpr (S_::END_BARRIER && !FACT) lds_barrier();
+            if constexpr (S_::END_BARRIER && !FACT && !OWN0) lds_barrier();
             stamp(a, sb + 13);
             ++titer;
         }
@@ -897,8 +978,9 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         float* out = a.slab + (int64_t)blockIdx.x * len;
         const int l = l0, c = c0, g = g0;
         // layer-0 wgrad: this wave's 16-column block, already summed over the rows
-        // (FACT: formed after the step by fact_expand_kernel; its slab columns unused)
-        if constexpr (S_::MLP && !FACT) {
+        // (FACT: formed after the step by fact_expand_kernel; its slab columns unused;
+        // OWN0: per-wave tiles, summed over the waves with layers k >= 1 below)
+        if constexpr (S_::MLP && !FACT && !OWN0) {
 #pragma unroll
             for (int j = 0; j < CB0; ++j) {
                 const int ntj = w + j * NWV;
@@ -980,42 +1062,51 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         // slot was private to it during the tiles (no layer-0 wgrad across waves), so
         // each wave writes its images into it as soon as it is done, and the first
         // cross-wave read below waits at that round's barrier instead.
-        if constexpr (!FACT) lds_barrier();
+        if constexpr (!FACT && !OWN0) lds_barrier();
         stamp(a, 62);
-        if constexpr (S_::MLP && L >= 2) {
-            // Layers k >= 1: each wave writes its register partials to its own LDS
-            // image, then every thread sums its share of the entries over the waves
-            // (plain stores and loads: LDS float atomics run ~2 cycles per lane).
+        if constexpr (S_::MLP && (L >= 2 || OWN0)) {
+            // Layers k >= 1 (and layer 0 under OWN0): each wave writes its register
+            // partials to its own LDS image, then every thread sums its share of the
+            // entries over the waves (plain stores and loads: LDS float atomics run ~2
+            // cycles per lane).  OWN0's db0 rides in the tail (dbAcc[0]).
             static_for<L>([&](auto kk) {
                 constexpr int k = decltype(kk)::value;
-                if constexpr (k >= 1) {
+                if constexpr (k >= 1 || OWN0) {
                     constexpr int SK = S_::S(k), SO = S_::S(k + 1);
+                    constexpr bool BIAS = k >= 1;
                     float* im = sstage + w * S_::WAVE_STAGE;
 #pragma unroll
                     for (int mt = 0; mt < S_::MT(k); ++mt) {
 #pragma unroll
                         for (int t = 0; t < S_::KT(k); ++t) {
-                            const f4 v = accK[S_::kt_off(k) + mt * S_::KT(k) + t];
+                            f4 v;
+                            if constexpr (k >= 1)
+                                v = accK[S_::kt_off(k) + mt * S_::KT(k) + t];
+                            else
+                                v = accL0[mt * KT0 + t];
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
                                 const int o = 16 * mt + 4 * g + r;
                                 if (o < SO) im[o * SK + 16 * t + c] = lane_get(v, r);
                             }
                         }
-                        const int o = 16 * mt + c;
-                        if (o < SO) im[SO * SK + g * SO + o] = dbK[S_::mb_off(k) + mt];
+                        if constexpr (BIAS) {
+                            const int o = 16 * mt + c;
+                            if (o < SO) im[SO * SK + g * SO + o] = dbK[S_::mb_off(k) + mt];
+                        }
                     }
                     if constexpr (TAIL_MERGED && k == L - 1) write_tail();
                     lds_barrier();
+                    constexpr int NE = (SO * SK + (BIAS ? SO : 0) + NTH - 1) / NTH;
 #pragma unroll
-                    for (int j = 0; j < S_::nek(k); ++j) {
+                    for (int j = 0; j < NE; ++j) {
                         const int e = tid + j * NTH;
                         if (e < SO * SK) {
                             float s = 0.f;
 #pragma unroll
                             for (int ws = 0; ws < NWV; ++ws) s += sstage[ws * S_::WAVE_STAGE + e];
                             out[(lay.w[k] - tb) + e] = s;
-                        } else if (e < SO * SK + SO) {
+                        } else if (BIAS && e < SO * SK + SO) {
                             float s = 0.f;
 #pragma unroll
                             for (int ws = 0; ws < NWV; ++ws)
