@@ -1308,7 +1308,7 @@ static int g_diag = 0;
 static unsigned long long* g_stamps = nullptr;
 // ncf_debug_set_geometry: 0 = ncf_layout_tune decides, 4 / NWAVES = forced (A/B, tests)
 static int g_geo_waves = 0;
-// ncf_layout_tune: the widest workgroup geometry with at least this many tiles
+// ncf_layout_tune: 8-wave workgroups from this many 128-row tiles up, else 4-wave
 #ifndef NCF_GEO_MIN_WGS
 #define NCF_GEO_MIN_WGS 256
 #endif
@@ -1800,9 +1800,12 @@ int ncf_layout_tune(ncf_layout* lay, int64_t rows) {
                                (NCF_LAYOUT_WG_MASK << NCF_LAYOUT_WG_SHIFT));
     if (2 * rows < (int64_t)lay->user_num + lay->item_num) f |= NCF_LAYOUT_PER_ROW_L0;
     lay->flags = f;
-    // geometry: forced (ncf_debug_set_geometry), else the widest workgroups that still
-    // give GEO_MIN_WGS tiles -- small per-rank batches spread over more CUs with fewer
-    // waves per workgroup (shorter barriers and cross-wave sums, one wave per SIMD)
+    // geometry: forced (ncf_debug_set_geometry), else 8-wave workgroups where the
+    // batch has GEO_MIN_WGS 128-row tiles and 4-wave ones below (twice the workgroups,
+    // one wave per SIMD).  Measured on the MI355X (profiles/r04_evidence/geometry_*):
+    // C2 (1,024 rows) 22.3 / 19.1 / 19.8 / 20.8 us per step at 8 / 4 / 2 / 1 waves,
+    // C5 (256) 13.3 / 12.4 / 12.8 / 13.2, the C3 step at 8,192 rows per rank 31.0 /
+    // 27.5 (train launch); the 2- and 1-wave kernels stay for A/B.
     const KernelEntry* e = train_fused(lay);
     int g = GEO_8;
     if (e) {
@@ -1813,12 +1816,8 @@ int ncf_layout_tune(ncf_layout* lay, int64_t rows) {
         if (g_geo_waves != 0) {
             for (int gg = 0; gg < NGEO; ++gg)
                 if (geo_waves(gg) == g_geo_waves && avail(gg)) g = gg;
-        } else {
-            for (int gg = GEO_8; gg < NGEO; ++gg) {
-                if (!avail(gg)) continue;
-                g = gg;
-                if ((rows + 16 * geo_waves(gg) - 1) / (16 * geo_waves(gg)) >= GEO_MIN_WGS) break;
-            }
+        } else if ((rows + 127) / 128 < GEO_MIN_WGS && avail(GEO_4)) {
+            g = GEO_4;
         }
     }
     f |= g << NCF_LAYOUT_GEO_SHIFT;

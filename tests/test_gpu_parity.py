@@ -761,10 +761,11 @@ def geometry():
 @pytest.mark.parametrize("B,per_row", [(1024, True), (4096, True), (8192, False), (300, True), (20000, False)])
 def test_engine_tuned_launch_shape_vs_oracle(B, per_row, waves, geometry):
     """ncf_layout_tune: the engine launches ceil(B / (16 x waves)) workgroups (the
-    reductions read that many slab rows) -- by default (waves 0) the widest of 8 / 4 /
-    2 / 1-wave workgroups that gives 256 tiles, or forced -- and takes per-row layer 0
+    reductions read that many slab rows) -- by default (waves 0) 8 waves where the batch
+    has 256 128-row tiles, else 4, or forced 8 / 4 / 2 / 1 -- and takes per-row layer 0
     when 2B < U + I (config C2: NCF(8,3), bs 1024, ml-1m ids).  Every step
-    teacher-forced from the oracle."""
+    teacher-forced from the oracle.  (NCF(8,3) has every geometry: OWN0 below 8 waves
+    and at 8, the factored kernel at B >= U + I / 2.)"""
     import ncf_amd._lib as L
     geometry(waves)
     T = 6
@@ -775,7 +776,7 @@ def test_engine_tuned_launch_shape_vs_oracle(B, per_row, waves, geometry):
     labels = (rng.random((T, B)) < 0.2).astype(np.int64)
     _stream(eng, users, items, labels, B)
     assert _fact_mode(eng.lay) == (not per_row)
-    w = waves or next((x for x in (8, 4, 2, 1) if (B + 16 * x - 1) // (16 * x) >= 256), 1)
+    w = waves or (8 if (B + 127) // 128 >= 256 else 4)
     assert (8, 4, 2, 1)[(eng.lay.flags >> L.LAYOUT_GEO_SHIFT) & L.LAYOUT_GEO_MASK] == w
     tiles = (B + 16 * w - 1) // (16 * w)
     assert (eng.lay.flags >> 8) & 0xFFF == (tiles if tiles < 256 else 0)

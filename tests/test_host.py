@@ -307,11 +307,12 @@ def test_hr_ndcg_topk_ranking_matches_golden(golden, bs, k):
 
 
 def test_layout_tune_launch_geometry():
-    """ncf_layout_tune (host logic, no GPU): the fused step's workgroup geometry is the
-    widest of 8 / 4 / 2 / 1 waves (128 / 64 / 32 / 16-row tiles) that still gives 256
-    tiles, among the geometries the shape has (the factored kernel and GMF: all; the
-    per-row layer 0: narrow ones only where dW0 has at most 8 16x16 tiles), else the
-    narrowest; the workgroup count is the tile count below 256."""
+    """ncf_layout_tune (host logic, no GPU): the fused step runs 8-wave workgroups on
+    128-row tiles where a batch has 256 of them, else 4-wave workgroups on 64-row
+    tiles (measured faster for C2, C5 and the C3 step at 8,192 rows per rank) where the
+    shape has that kernel (the factored kernel and GMF: always; the per-row layer 0:
+    where dW0 has at most 8 16x16 tiles); 2 / 1 waves only when forced; the workgroup
+    count is the tile count below 256."""
     import ncf_amd._lib as L
     lib = L.hip()
 
@@ -325,14 +326,16 @@ def test_layout_tune_launch_geometry():
         finally:
             lib.ncf_debug_set_geometry(0)
 
-    assert tune(6041, 3707, 8, 3, 1024) == (1, 64)         # C2: per-row layer 0, dW0 2 x 4 tiles
-    assert tune(6041, 3707, 16, 3, 8192) == (4, 128)       # C3 at N = 8 (factored): no 2-wave kernel (weights
-    assert tune(6041, 3707, 8, 3, 8192) == (2, 0)          # staged in 21 registers); NCF(8,3): 256 tiles of 32
+    assert tune(6041, 3707, 8, 3, 1024) == (4, 16)         # C2: per-row layer 0, dW0 2 x 4 tiles
+    assert tune(6041, 3707, 16, 3, 8192) == (4, 128)       # C3 at N = 8 (factored)
     assert tune(6041, 3707, 16, 3, 65536) == (8, 0)        # C3 at N = 1: 512 tiles -> 256 workgroups
-    assert tune(6041, 3707, 16, 3, 16384) == (4, 0)        # 256 tiles of 64 rows
+    assert tune(6041, 3707, 16, 3, 32768) == (8, 0)        # 256 tiles of 128 rows
+    assert tune(6041, 3707, 16, 3, 32640) == (4, 0)        # 255 tiles of 128 rows: 510 of 64
     assert tune(138494, 26745, 16, 3, 8192) == (8, 64)     # C4 at N = 8: per-row, dW0 4 x 8 tiles
     assert tune(6041, 3707, 8, 3, 1024, waves=8) == (8, 8)
-    assert tune(6041, 3707, 8, 3, 1024, waves=4) == (4, 16)
+    assert tune(6041, 3707, 8, 3, 1024, waves=1) == (1, 64)
+    assert tune(6041, 3707, 8, 3, 8192, waves=2) == (2, 0)
+    assert tune(6041, 3707, 16, 3, 8192, waves=2) == (8, 64)  # no 2-wave kernel (weights in 21 registers)
     assert tune(6041, 3707, 16, 3, 65536, waves=4) == (4, 0)
     assert tune(138494, 26745, 16, 3, 8192, waves=1) == (8, 64)  # no 1-wave kernel there
     assert lib.ncf_debug_set_geometry(5) != 0
