@@ -40,7 +40,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
     ap.add_argument("inputs", nargs="+")
-    ap.add_argument("--bw", type=float, default=153.0, help="xGMI GB/s per link (ring bound)")
+    ap.add_argument("--bw", type=float, nargs="+", default=[153.0, 450.0],
+                    help="ring bus GB/s: one xGMI link (a single ring, per-link bound) and an "
+                         "optimistic multi-ring figure over several of the 7 links")
     ap.add_argument("--alpha", type=float, nargs="+", default=[10.0, 25.0], help="us per collective")
     ap.add_argument("--n1-us", type=json.loads, default={"c3": 55.9, "c4": 126.0},
                     help="single-process us/step per config (bench lines)")
@@ -55,25 +57,26 @@ def main():
         d = json.loads([line for line in txt if line.startswith("{")][-1])
         cfg, n = d["config"], int(d["world_emulated"])
         for mode, m in d["modes"].items():
-            local = 1e3 * m["ms_per_step_graph"]
-            # the emulated collectives (one-rank group / exact all-reduce forms) are not wire time
-            emu = sum(1e3 * v for k, v in m["launch_groups_ms"].items()
-                      if k in ("allreduce", "reduce_scatter", "all_gather"))
-            for alpha in a.alpha:
-                t = local - emu + exchange_us(mode, n, a.floats[cfg], a.packed[cfg], a.bw, alpha)
-                rows.append({"config": cfg, "n_gpus": n, "mode": mode, "alpha_us": alpha, "local_us": round(local - emu, 1),
-                             "exchange_us": round(t - local + emu, 1), "step_us": round(t, 1),
-                             "interactions_per_s": a.batch / (t * 1e-6),
-                             "vs_1gpu": a.n1_us[cfg] / t})
+            # local part: the per-rank launch groups (HIP events on the launch stream)
+            # without the emulated collectives (a one-rank group, or their exact
+            # all-reduce forms over it, move nothing between GPUs)
+            local = sum(1e3 * v for k, v in m["launch_groups_ms"].items()
+                        if k not in ("allreduce", "reduce_scatter", "all_gather"))
+            for bw in a.bw:
+                for alpha in a.alpha:
+                    x = exchange_us(mode, n, a.floats[cfg], a.packed[cfg], bw, alpha)
+                    t = local + x
+                    rows.append({"config": cfg, "n_gpus": n, "mode": mode, "bw_GBps": bw, "alpha_us": alpha,
+                                 "local_us": round(local, 1), "exchange_us": round(x, 1), "step_us": round(t, 1),
+                                 "interactions_per_s": a.batch / (t * 1e-6), "vs_1gpu": a.n1_us[cfg] / t})
     for cfg, us in a.n1_us.items():
-        rows.append({"config": cfg, "n_gpus": 1, "mode": "single", "alpha_us": 0, "local_us": us, "exchange_us": 0,
-                     "step_us": us, "interactions_per_s": a.batch / (us * 1e-6), "vs_1gpu": 1.0})
-    json.dump({"model": "T(N) = local(N) + ring collectives over xGMI", "bw_GBps_per_link": a.bw, "rows": rows},
-              open(a.out, "w"), indent=1)
-    for r in sorted(rows, key=lambda r: (r["config"], r["n_gpus"], r["mode"], r["alpha_us"])):
-        print(f"{r['config']} N={r['n_gpus']} {r['mode']:9s} a={r['alpha_us']:4.0f}  local {r['local_us']:7.1f}  "
-              f"xchg {r['exchange_us']:7.1f}  step {r['step_us']:7.1f} us  {r['interactions_per_s'] / 1e9:6.3f} G/s  "
-              f"x{r['vs_1gpu']:.2f}")
+        rows.append({"config": cfg, "n_gpus": 1, "mode": "single", "bw_GBps": 0, "alpha_us": 0, "local_us": us,
+                     "exchange_us": 0, "step_us": us, "interactions_per_s": a.batch / (us * 1e-6), "vs_1gpu": 1.0})
+    json.dump({"model": "T(N) = local(N) + ring collectives over xGMI", "rows": rows}, open(a.out, "w"), indent=1)
+    for r in sorted(rows, key=lambda r: (r["config"], r["n_gpus"], r["mode"], r["bw_GBps"], r["alpha_us"])):
+        print(f"{r['config']} N={r['n_gpus']} {r['mode']:9s} B={r['bw_GBps']:4.0f} a={r['alpha_us']:3.0f}  "
+              f"local {r['local_us']:6.1f}  xchg {r['exchange_us']:6.1f}  step {r['step_us']:6.1f} us  "
+              f"{r['interactions_per_s'] / 1e9:6.3f} G/s  x{r['vs_1gpu']:.2f}")
 
 
 if __name__ == "__main__":
