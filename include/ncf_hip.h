@@ -21,10 +21,12 @@
 extern "C" {
 #endif
 
-/* 15: ncf_layout.flags gains the fused step's workgroup geometry (NCF_LAYOUT_GEO_*) and
+/* 16: NCF_LAYOUT_USER_STORE (ncf_layout_tune; ncf_uses_user_order covers it),
+ * ncf_debug_set_user_store; ncf_adam_step_fact's gshard is written (dX formed in place).
+ * 15: ncf_layout.flags gains the fused step's workgroup geometry (NCF_LAYOUT_GEO_*) and
  * NCF_LAYOUT_FACT_DEFER_DX; new ncf_adam_step_fact, ncf_prepare_epoch2
  * (NCF_PREP_CANONICAL), ncf_probe_gather_scatter, ncf_debug_set_geometry. */
-#define NCF_ABI_VERSION 15
+#define NCF_ABI_VERSION 16
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -84,6 +86,12 @@ typedef struct ncf_layout {
 #define NCF_LAYOUT_FACT_DEFER_DX 0x8 /* factored layer 0: the step forms only the dW0 partials and leaves the
                                         per-entity sums G in grads' Um / Im rows (ncf_adam_step_fact expands them
                                         per shard after the reduce-scatter); set by the caller, kept by tune */
+#define NCF_LAYOUT_USER_STORE 0x10  /* fused step (set by ncf_layout_tune when ncf_debug_set_user_store
+                                       enables it; since ABI 16): the user-side embedding gradients of each
+                                       row are stored plainly into the workspace and summed per user by a
+                                       second launch over ncf_user_order's runs instead of float atomics
+                                       (needs the user_order argument of ncf_train_step, else the atomics
+                                       stay) */
 
 /* Device-resident step control block (16-byte aligned, 6 x int64).  Lets a
  * captured hipGraph replay consecutive batches with no host involvement. */
@@ -153,7 +161,10 @@ int64_t ncf_slab_stride(const ncf_layout *lay);
  * user_order (optional, may be NULL; since ABI 12): ncf_user_order of the same rows,
  * batch_global and world.  Where ncf_uses_user_order(lay), the step then sums the
  * user-side layer-0 gradients over runs of equal users before its atomics instead
- * of adding per row (same gradient up to fp32 summation order).
+ * of adding per row (same gradient up to fp32 summation order); on the fused path
+ * with NCF_LAYOUT_USER_STORE every user-side gradient row (Um and Ug) is stored into
+ * the workspace and a second launch sums each 32-position piece of the user order
+ * (one float atomic per user and piece instead of one per row).
  */
 int ncf_train_step(const ncf_layout *lay, const float *params, float *grads, const uint64_t *rows,
                    const int64_t *user_order,
@@ -292,16 +303,18 @@ int ncf_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq
  * NCF_LAYOUT_FACT_DEFER_DX; replaces optimizer.step(), train_neumf.py:90,115, on
  * this rank's shard).  gshard holds the reduce-scattered flat gradient shard
  * [shard_begin, shard_begin + n): in its Um / Im rows the summed per-entity D0 sums
- * G (the step deferred their expansion), elsewhere the gradient itself.  The kernel
- * forms dUm / dIm of its rows as G W0[:, half], W0 being the weights the step ran
- * with (saved in the step's workspace: the same launch updates W0 when the shard
- * holds it), and runs Adam on the active ranges (shard-relative) of params (the
- * flat parameters + shard_begin); gshard is not cleared.  Fused path, factored layer
- * 0 with dm <= 64 and shard_begin a multiple of 64: NCF_E_UNSUPPORTED otherwise.
+ * G (the step deferred their expansion), elsewhere the gradient itself.  Two
+ * launches: the expansion of the shard's Um / Im rows, dX = G W0[:, half] written
+ * over G (W0 being the weights the step ran with, saved in the step's workspace,
+ * since the Adam launch updates W0 when the shard holds it; MFMA tiles, the rows
+ * inside [shard_begin, shard_begin + max range end)), then ncf_adam_step on the
+ * active ranges (shard-relative) of params (the flat parameters + shard_begin),
+ * which clears gshard's active ranges.  Fused path, factored layer 0 with dm <= 64,
+ * shard_begin a multiple of 64: NCF_E_UNSUPPORTED otherwise.
  * Loss bookkeeping as ncf_adam_step (loss_slot shard-relative, or loss_hist NULL on
  * the other ranks).
  */
-int ncf_adam_step_fact(const ncf_layout *lay, const void *workspace, float *params, const float *gshard,
+int ncf_adam_step_fact(const ncf_layout *lay, const void *workspace, float *params, float *gshard,
                        float *exp_avg, float *exp_avg_sq, const int64_t *ranges, int nranges, int64_t shard_begin,
                        ncf_step_ctl *ctl, double lr, double beta1, double beta2, double eps, int64_t loss_slot,
                        float *loss_hist, int64_t hist_len, void *stream);
@@ -499,6 +512,9 @@ int ncf_probe_gather_scatter(const ncf_layout *lay, const float *params, float *
  * the per-rank batch (narrower workgroups for small batches), 8, 4, 2 or 1 waves =
  * forced where that kernel exists (A/B measurements, tests).  NCF_E_ARG otherwise. */
 int ncf_debug_set_geometry(int waves);
+/* User-side store-and-sum (NCF_LAYOUT_USER_STORE) for later ncf_layout_tune calls:
+ * 0 = never (the default), -1 = from 16,384 rows per launch, 1 = wherever it applies. */
+int ncf_debug_set_user_store(int mode);
 
 /* Diagnostics only: device buffer of ncf_slab_rows() x 64 uint64 that the next
  * ncf_train_step launches fill with per-workgroup s_memtime phase stamps

@@ -106,6 +106,11 @@ struct TrainArgs {
     int64_t fwd_n;  // FWD_ONLY: number of rows
     int diag;       // DIAG_* ablation switches (0 in production)
     unsigned long long* stamps;  // diagnostics: per-workgroup s_memtime stamps (nullptr in production)
+    // NCF_LAYOUT_USER_STORE: the user-side embedding gradients of row k of the slice go
+    // with plain stores to ustore[k * uw ...] ([Um part DM][Ug part F]) instead of float
+    // atomics into grads; user_sum_kernel (ncf_ops.hip) sums them per user afterwards.
+    float* ustore;
+    int uw;
 };
 
 constexpr int NSTAMP = 64;  // stamps per workgroup

@@ -273,72 +273,6 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
     record_loss(ctl, g, loss_slot, loss_hist, hist_len);
 }
 
-// Sharded Adam of the factored path (dp_mode "zero1" with NCF_LAYOUT_FACT_DEFER_DX):
-// the reduce-scattered gradient shard holds, in the Um / Im rows, the summed
-// per-entity D0 sums G (the train step expanded only the dW0 partials), so the
-// gradient of element (row, col) of table X is formed here, by the rank that owns
-// it, as  dX[row][col] = sum_j G[row][j] W0[j][koff + col]  (koff = 0 for Um, DM
-// for Im; the re-association of fact_expand_kernel's dX = G W0half) -- then Adam.
-// The shard is 64-float aligned and DM divides 64, so a G row never straddles two
-// shards.  g is not cleared (the next reduce-scatter overwrites the shard).
-struct FactShard {
-    const float* w0s;      // W0 as the step ran with it ([DM][2 DM], fact_w0_snap)
-    int64_t um, im, nu, ni;  // table offsets and float counts (U * DM, I * DM)
-    int64_t base;          // flat index of shard element 0
-    int dm;
-};
-
-__global__ __launch_bounds__(256) void adam_fact_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                        float* __restrict__ m, float* __restrict__ v, Ranges R,
-                                                        FactShard F, const ncf_step_ctl* ctl, double lr, double beta1,
-                                                        double beta2, float eps, int64_t loss_slot, float* loss_hist,
-                                                        int64_t hist_len, ScCache* scc) {
-#pragma clang fp contract(off)
-    __shared__ float sc[2];
-    const int64_t t_step = ctl->adam_t;
-    step_scalars(scc, t_step, lr, beta1, beta2, sc);
-    step_scalars_ahead(scc, t_step, lr, beta1, beta2);
-    __syncthreads();
-    const float neg_step = sc[0], bc2s = sc[1];
-    const float w1 = (float)(1.0 - beta1);
-    const float b2 = (float)beta2;
-    const float omb2 = (float)(1.0 - beta2);
-    const int64_t total = R.prefix[R.n];
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
-        int which;
-        const int64_t i = range_locate(R, q, &which);
-        const int64_t fi = F.base + i;
-        f4 gg;
-        const bool isu = fi >= F.um && fi < F.um + F.nu, isi = fi >= F.im && fi < F.im + F.ni;
-        if (isu || isi) {
-            const int64_t rel = fi - (isu ? F.um : F.im);
-            const int64_t row = rel / F.dm;
-            const int col = (int)(rel - row * F.dm);
-            const float* G = g + (i - col);  // the row's first float (same shard)
-            const float* W = F.w0s + (isu ? 0 : F.dm) + col;
-            gg = f4{0.f, 0.f, 0.f, 0.f};
-            for (int j = 0; j < F.dm; ++j) {
-                const float gj = G[j];
-                const f4 w = *reinterpret_cast<const f4*>(W + (int64_t)j * 2 * F.dm);
-                gg.x = fmaf(gj, w.x, gg.x);
-                gg.y = fmaf(gj, w.y, gg.y);
-                gg.z = fmaf(gj, w.z, gg.z);
-                gg.w = fmaf(gj, w.w, gg.w);
-            }
-        } else {
-            gg = *reinterpret_cast<const f4*>(g + i);
-        }
-        f4 mm = *reinterpret_cast<const f4*>(m + i);
-        f4 vv = *reinterpret_cast<const f4*>(v + i);
-        f4 pp = *reinterpret_cast<const f4*>(p + i);
-        adam_f4(pp, mm, vv, gg, w1, b2, omb2, bc2s, eps, neg_step);
-        *reinterpret_cast<f4*>(m + i) = mm;
-        *reinterpret_cast<f4*>(v + i) = vv;
-        *reinterpret_cast<f4*>(p + i) = pp;
-    }
-    record_loss(ctl, g, loss_slot, loss_hist, hist_len);
-}
-
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* __restrict__ g, Ranges R,
                                                   const ncf_step_ctl* ctl, float lr, int64_t loss_slot, float* loss_hist,
                                                   int64_t hist_len) {
@@ -1218,6 +1152,80 @@ __global__ __launch_bounds__(UO_THREADS) void user_order_kernel(const uint64_t* 
     }
 }
 
+// User store-and-sum (NCF_LAYOUT_USER_STORE).  Float atomics run at the memory side at
+// ~1.3 TB/s of added bytes (MI355X_MICROARCH.md, Global float atomics), plain stores at
+// ~6 TB/s: at C3 the user half of the step's scatter (65,536 rows x (64 + 16) floats,
+// ~10.8 rows per user per batch, rows in item order so nothing merges in a tile) was
+// the largest single atomic stream of the step.  The step stores each row's user-side
+// gradient into ustore[row][uw] ([Um part][Ug part], row = slice offset); this launch
+// walks the slice's user order (ncf_user_order: entries user << 32 | offset, users
+// ascending, padding last) in pieces of US_SPAN positions, one wave per piece: the
+// piece's rows are loaded together, summed per run of equal users in order, and each
+// run's sum is added to its user's Um / Ug rows by one float atomic per column -- every
+// wave the same work whatever the user skew, and ~US_SPAN / (runs + 1) times fewer
+// atomic bytes than per row.  Lane = column (uw <= 64 * US_NCH).
+constexpr int US_SPAN = 32, US_WAVES = 4, US_NCH = 4;
+struct UsArgs {
+    const float* ustore;
+    const int64_t* order;
+    float* grads;
+    const ncf_step_ctl* ctl;
+    int64_t batch_global, um, ug;
+    int world, rank, dmu, f, uw;
+};
+template <int NCH>
+__global__ __launch_bounds__(US_WAVES * 64) void user_sum_kernel(UsArgs A) {
+    // this rank's slice of the current batch (ncf_train.hip: the step's own rows)
+    const int64_t ntot = A.ctl->n_total;
+    const int64_t nbatch = (ntot + A.batch_global - 1) / A.batch_global;
+    const int64_t b = nbatch > 0 ? A.ctl->batch % nbatch : 0;
+    const int64_t b0 = b * A.batch_global;
+    int64_t gb = ntot - b0;
+    if (gb > A.batch_global) gb = A.batch_global;
+    if (gb < 0) gb = 0;
+    const int64_t per = (gb + A.world - 1) / A.world;
+    int64_t lo = (int64_t)A.rank * per, hi = lo + per;
+    if (lo > gb) lo = gb;
+    if (hi > gb) hi = gb;
+    const int64_t base = b0 + lo, nloc = hi - lo;
+    const int lane = threadIdx.x & 63;
+    const int64_t p0 = ((int64_t)blockIdx.x * US_WAVES + (threadIdx.x >> 6)) * US_SPAN;
+    if (p0 >= nloc) return;  // wave-uniform
+    const int64_t e = lane < US_SPAN && p0 + lane < nloc ? A.order[base + p0 + lane] : -1;
+    const int eu = (int)(e >> 32), eo = (int)(uint32_t)e;  // past the slice: user -1 (stop)
+    float v[US_SPAN][NCH];
+#pragma unroll
+    for (int t = 0; t < US_SPAN; ++t) {
+        const int ut = __builtin_amdgcn_readlane(eu, t), ot = __builtin_amdgcn_readlane(eo, t);
+        const float* src = A.ustore + (int64_t)ot * A.uw;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch)
+            v[t][ch] = (ut >= 0 && ch * 64 + lane < A.uw) ? src[ch * 64 + lane] : 0.f;
+    }
+    float acc[NCH];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) acc[ch] = 0.f;
+#pragma unroll
+    for (int t = 0; t < US_SPAN; ++t) {
+        const int ut = __builtin_amdgcn_readlane(eu, t);
+        if (ut < 0) break;  // padding rows sort last
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) acc[ch] += v[t][ch];
+        const int un = t + 1 < US_SPAN ? __builtin_amdgcn_readlane(eu, t + 1) : -1;
+        if (un != ut) {  // the run (or this piece of it) ends: one atomic per column
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch) {
+                const int col = ch * 64 + lane;
+                if (col < A.dmu)
+                    atomicAdd(A.grads + A.um + (int64_t)ut * A.dmu + col, acc[ch]);
+                else if (col < A.uw)
+                    atomicAdd(A.grads + A.ug + (int64_t)ut * A.f + (col - A.dmu), acc[ch]);
+                acc[ch] = 0.f;
+            }
+        }
+    }
+}
+
 static int prep_parts(int64_t B) {
     if (B <= PART_ROWS) return 1;
     const int64_t need = (B + PART_ROWS - 1) / PART_ROWS;
@@ -1308,6 +1316,13 @@ static int g_diag = 0;
 static unsigned long long* g_stamps = nullptr;
 // ncf_debug_set_geometry: 0 = ncf_layout_tune decides, 4 / NWAVES = forced (A/B, tests)
 static int g_geo_waves = 0;
+// ncf_debug_set_user_store: 0 = off (the default: measured slower),
+// -1 = ncf_layout_tune decides by the per-rank batch, 1 = wherever it applies
+static int g_user_store = 0;
+// ncf_layout_tune: user store-and-sum from this many rows per launch up
+#ifndef NCF_US_MIN_ROWS
+#define NCF_US_MIN_ROWS 16384
+#endif
 // ncf_layout_tune: 8-wave workgroups from this many 128-row tiles up, else 4-wave
 #ifndef NCF_GEO_MIN_WGS
 #define NCF_GEO_MIN_WGS 256
@@ -1492,11 +1507,25 @@ struct FxShape {
     static constexpr int64_t LDS = ((int64_t)DM * ST + 3LL * CH * ST) * 4;
 };
 
+// Expansion modes: FX_FULL (dX over G and the dW0 partials), FX_DW0 (NCF_LAYOUT_FACT_
+// DEFER_DX: the dW0 partials only, the W0 the step ran with saved to the snapshot),
+// FX_DX (ncf_adam_step_fact: dX only, over the Um / Im rows of one rank's reduce-
+// scattered gradient shard, W0 from the snapshot).
+enum { FX_FULL = 0, FX_DW0 = 1, FX_DX = 2 };
+struct FxArgs {
+    const float* prm;   // X rows (params; FX_FULL / FX_DW0)
+    const float* w0;    // W0 [DM][2 DM] (row stride 2 DM): params' W0, or the snapshot (FX_DX)
+    float* g;           // G rows: flat element q of the gradient at g[q - gofs]; dX written over them
+    int64_t gofs;
+    int64_t xoff[2];    // Um / Im offsets
+    int64_t r0[2], r1[2];  // rows [r0, r1) of each table expanded
+    float* partials;    // [nblk][DM][DM] (FX_FULL / FX_DW0)
+    float* w0snap;      // FX_DW0: the snapshot written
+    int nbu, mode;
+};
+
 template <int DM>
-__global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout lay, const float* __restrict__ prm,
-                                                                     float* __restrict__ grads,
-                                                                     float* __restrict__ partials, int nbu,
-                                                                     int dw0_only, float* __restrict__ w0snap) {
+__global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(FxArgs A) {
     using X_ = FxShape<DM>;
     constexpr int CH = X_::CH, ST = X_::ST, NT = X_::NT, Q4 = X_::Q4, TPW = X_::TPW, cpb = X_::CPB;
     extern __shared__ __attribute__((aligned(16))) float fsm[];
@@ -1505,27 +1534,29 @@ __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout l
     float* sX = sG + CH * ST;  // X rows  [CH][ST]
     float* sO = sX + CH * ST;  // dX rows [CH][ST]
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, c = l & 15, g = l >> 4;
-    const bool user = (int)blockIdx.x < nbu;
-    const int64_t nrows = user ? lay.user_num : lay.item_num;
-    const int64_t xoff = user ? lay.um : lay.im;
-    const int koff = user ? 0 : DM;
-    const int64_t rb = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * cpb * CH;  // first row of the block
+    const int t = (int)blockIdx.x < A.nbu ? 0 : 1;  // 0: Um, 1: Im
+    const int64_t rend = A.r1[t];
+    const int64_t xoff = A.xoff[t];
+    const int koff = t * DM;
+    const bool want_dw = A.mode != FX_DX, want_dx = A.mode != FX_DW0;
+    const int64_t rb = A.r0[t] + (int64_t)(t == 0 ? blockIdx.x : blockIdx.x - A.nbu) * cpb * CH;  // first row
+    float* gx = A.g + (xoff - A.gofs);  // row r of the table's G at gx + r DM
     // the W0 half: loads issued here, stored to LDS behind the first chunk's loads
     constexpr int NW4 = DM * Q4, PW = (NW4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
     f4 wv[PW];
 #pragma unroll
     for (int q = 0; q < PW; ++q) {
         const int e4 = tid + q * FX_WAVES * 64, j = e4 / Q4, k4 = e4 - j * Q4;
-        wv[q] = e4 < NW4 ? *reinterpret_cast<const f4*>(prm + lay.w[0] + (int64_t)j * 2 * DM + koff + 4 * k4)
+        wv[q] = e4 < NW4 ? *reinterpret_cast<const f4*>(A.w0 + (int64_t)j * 2 * DM + koff + 4 * k4)
                          : f4{0.f, 0.f, 0.f, 0.f};
     }
-    // dW0-only mode: the first block of each table saves its W0 half (the weights this
-    // step ran with) for the sharded dX expansion of ncf_adam_step_fact
-    if (dw0_only && w0snap != nullptr && (blockIdx.x == 0 || (int)blockIdx.x == nbu)) {
+    // FX_DW0: the first block of each table saves its W0 half (the weights this step
+    // ran with) for the sharded dX expansion of ncf_adam_step_fact
+    if (A.mode == FX_DW0 && A.w0snap != nullptr && (blockIdx.x == 0 || (int)blockIdx.x == A.nbu)) {
 #pragma unroll
         for (int q = 0; q < PW; ++q) {
             const int e4 = tid + q * FX_WAVES * 64, j = e4 / Q4, k4 = e4 - j * Q4;
-            if (e4 < NW4) *reinterpret_cast<f4*>(w0snap + (int64_t)j * 2 * DM + koff + 4 * k4) = wv[q];
+            if (e4 < NW4) *reinterpret_cast<f4*>(A.w0snap + (int64_t)j * 2 * DM + koff + 4 * k4) = wv[q];
         }
     }
     f4 accw[TPW];
@@ -1534,19 +1565,18 @@ __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout l
 #pragma unroll
     for (int ch = 0; ch < cpb; ++ch) {
         const int64_t r0 = rb + (int64_t)ch * CH;
-        if (r0 >= nrows) break;  // block-uniform
+        if (r0 >= rend) break;  // block-uniform
         if (ch > 0) __syncthreads();  // the previous chunk's images are consumed
-        {   // the chunk's G and X rows -> LDS (each thread's loads issued together)
+        {   // the chunk's G (and X) rows -> LDS (each thread's loads issued together)
             constexpr int NR4 = CH * Q4, PR = (NR4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
             f4 gv[PR], xv[PR];
 #pragma unroll
             for (int q = 0; q < PR; ++q) {
                 const int e4 = tid + q * FX_WAVES * 64, row = e4 / Q4, k4 = e4 - row * Q4;
-                const bool ok = e4 < NR4 && r0 + row < nrows;
-                gv[q] = ok ? *reinterpret_cast<const f4*>(grads + xoff + (r0 + row) * DM + 4 * k4)
-                           : f4{0.f, 0.f, 0.f, 0.f};
-                xv[q] = ok ? *reinterpret_cast<const f4*>(prm + xoff + (r0 + row) * DM + 4 * k4)
-                           : f4{0.f, 0.f, 0.f, 0.f};
+                const bool ok = e4 < NR4 && r0 + row < rend;
+                gv[q] = ok ? *reinterpret_cast<const f4*>(gx + (r0 + row) * DM + 4 * k4) : f4{0.f, 0.f, 0.f, 0.f};
+                xv[q] = ok && want_dw ? *reinterpret_cast<const f4*>(A.prm + xoff + (r0 + row) * DM + 4 * k4)
+                                      : f4{0.f, 0.f, 0.f, 0.f};
             }
             if (ch == 0) {
 #pragma unroll
@@ -1560,32 +1590,33 @@ __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout l
                 const int e4 = tid + q * FX_WAVES * 64, row = e4 / Q4, k4 = e4 - row * Q4;
                 if (e4 < NR4) {
                     *reinterpret_cast<f4*>(sG + row * ST + 4 * k4) = gv[q];
-                    *reinterpret_cast<f4*>(sX + row * ST + 4 * k4) = xv[q];
+                    if (want_dw) *reinterpret_cast<f4*>(sX + row * ST + 4 * k4) = xv[q];
                 }
             }
         }
         __syncthreads();
         // dW0 partial, tiles (mt, nt) dealt round-robin to the waves:
         // A[i = j][k = row] = G[row][j],  B[k = row][n = k'] = X[row][k']
+        if (want_dw) {
 #pragma unroll
-        for (int q = 0; q < TPW; ++q) {
-            const int tt = w + q * FX_WAVES;
-            if (tt >= NT * NT) break;
-            const int mt = tt / NT, nt = tt - mt * NT;
-            const bool jok = 16 * mt + c < DM, kok = 16 * nt + c < DM;
-            f4 a0 = accw[q], a1 = f4{0.f, 0.f, 0.f, 0.f};
+            for (int q = 0; q < TPW; ++q) {
+                const int tt = w + q * FX_WAVES;
+                if (tt >= NT * NT) break;
+                const int mt = tt / NT, nt = tt - mt * NT;
+                const bool jok = 16 * mt + c < DM, kok = 16 * nt + c < DM;
+                f4 a0 = accw[q], a1 = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-            for (int s4 = 0; s4 < CH / 4; s4 += 2) {
-                const int ra = 4 * s4 + g, rb2 = ra + 4;
-                a0 = MFMA4(jok ? sG[ra * ST + 16 * mt + c] : 0.f, kok ? sX[ra * ST + 16 * nt + c] : 0.f, a0);
-                a1 = MFMA4(jok ? sG[rb2 * ST + 16 * mt + c] : 0.f, kok ? sX[rb2 * ST + 16 * nt + c] : 0.f, a1);
+                for (int s4 = 0; s4 < CH / 4; s4 += 2) {
+                    const int ra = 4 * s4 + g, rb2 = ra + 4;
+                    a0 = MFMA4(jok ? sG[ra * ST + 16 * mt + c] : 0.f, kok ? sX[ra * ST + 16 * nt + c] : 0.f, a0);
+                    a1 = MFMA4(jok ? sG[rb2 * ST + 16 * mt + c] : 0.f, kok ? sX[rb2 * ST + 16 * nt + c] : 0.f, a1);
+                }
+                a0.x += a1.x; a0.y += a1.y; a0.z += a1.z; a0.w += a1.w;
+                accw[q] = a0;
             }
-            a0.x += a1.x; a0.y += a1.y; a0.z += a1.z; a0.w += a1.w;
-            accw[q] = a0;
         }
-        // NCF_LAYOUT_FACT_DEFER_DX: G stays; the owner of each row expands it after the
-        // reduce-scatter (ncf_adam_step_fact)
-        if (dw0_only) continue;
+        // FX_DW0: G stays; the owner of each row expands it after the reduce-scatter
+        if (!want_dx) continue;
         // dX = G W0h, tiles (rt, nt): A[i = row][k = j] = G[row][j],  B[k = j][n = k'] = W0h[j][k']
         for (int tt = w; tt < (CH / 16) * NT; tt += FX_WAVES) {
             const int rt = tt / NT, nt = tt - rt * NT;
@@ -1601,13 +1632,13 @@ __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(ncf_layout l
         __syncthreads();
         for (int e = tid; e < CH * Q4; e += FX_WAVES * 64) {
             const int row = e / Q4, q = e - row * Q4;
-            if (r0 + row < nrows)
-                *reinterpret_cast<f4*>(grads + xoff + (r0 + row) * DM + 4 * q) =
-                    *reinterpret_cast<const f4*>(sO + row * ST + 4 * q);
+            if (r0 + row < rend)
+                *reinterpret_cast<f4*>(gx + (r0 + row) * DM + 4 * q) = *reinterpret_cast<const f4*>(sO + row * ST + 4 * q);
         }
     }
+    if (!want_dw) return;
     // the block's dW0 partial: plain stores (every block covers the same W0 half)
-    float* pb = partials + (int64_t)blockIdx.x * DM * DM;
+    float* pb = A.partials + (int64_t)blockIdx.x * DM * DM;
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
         const int tt = w + q * FX_WAVES;
@@ -1698,6 +1729,22 @@ static int fact_blocks(const ncf_layout* lay, int* nbu) {
     return bu + bi;
 }
 
+// NCF_LAYOUT_USER_STORE: user-side gradient row width ([Um part][Ug part]) and
+// whether the fused step can run it (user_order_kernel's user bound, the sum
+// kernel's columns, vector-aligned parts).
+static int us_uw(const ncf_layout* lay) {
+    const bool mlp = lay->model_type != NCF_MODEL_GMF, gmf = lay->model_type != NCF_MODEL_MLP;
+    return (mlp ? (lay->factor_num << (lay->num_layers - 1)) : 0) + (gmf ? lay->factor_num : 0);
+}
+static bool us_applies(const ncf_layout* lay) {
+    return train_fused(lay) != nullptr && lay->user_num <= UO_MAX_USERS && lay->factor_num % 4 == 0 &&
+           us_uw(lay) <= 64 * US_NCH;
+}
+static bool us_on(const ncf_layout* lay) { return (lay->flags & NCF_LAYOUT_USER_STORE) && us_applies(lay); }
+static int64_t us_floats(const ncf_layout* lay, int64_t rows) {
+    return us_on(lay) ? ((rows + TILE_ROWS + 63) & ~(int64_t)63) * us_uw(lay) : 0;
+}
+
 static int64_t fact_partials_floats(const ncf_layout* lay) {
     if (fact_dm(lay) > FACT_LDS_DM) return 0;  // W0 into the slab (the layered GEMM expansion)
     int nbu;
@@ -1739,27 +1786,81 @@ static W0Part w0_part(const ncf_layout* lay, const void* workspace) {
     return wp;
 }
 
+static int fact_expand_entry(int DM, const void** fe, int64_t* lds) {
+    switch (DM) {
+#define NCF_FX(D) case D: *fe = reinterpret_cast<const void*>(&fact_expand_kernel<D>); *lds = FxShape<D>::LDS; break;
+        NCF_FX(8) NCF_FX(16) NCF_FX(32) NCF_FX(64) NCF_FX(128)
+#undef NCF_FX
+        default: return NCF_E_UNSUPPORTED;
+    }
+    return ensure_lds(*fe, *lds) == NCF_OK ? NCF_OK : NCF_E_LAUNCH;
+}
+
+static int launch_fx(const void* fe, int64_t lds, FxArgs& A, int nblk, hipStream_t st) {
+    if (nblk <= 0) return NCF_OK;
+    void* ae[] = {&A};
+    if (hipLaunchKernel(fe, dim3((unsigned)nblk), dim3(FX_WAVES * 64), ae, (size_t)lds, st) != hipSuccess)
+        return NCF_E_LAUNCH;
+    return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
+}
+
+// After the train step: FX_FULL, or FX_DW0 under NCF_LAYOUT_FACT_DEFER_DX.
 static int launch_fact_expand(const ncf_layout* lay, const float* params, float* grads, float* partials,
                               float* w0snap, hipStream_t st) {
     const int DM = lay->factor_num << (lay->num_layers - 1);
     if (DM > FACT_LDS_DM) return NCF_OK;  // expanded by the layered path itself (lyr_run)
     const void* fe;
     int64_t lds;
-    switch (DM) {
-#define NCF_FX(D) case D: fe = reinterpret_cast<const void*>(&fact_expand_kernel<D>); lds = FxShape<D>::LDS; break;
-        NCF_FX(8) NCF_FX(16) NCF_FX(32) NCF_FX(64) NCF_FX(128)
-#undef NCF_FX
-        default: return NCF_E_UNSUPPORTED;
+    int rc = fact_expand_entry(DM, &fe, &lds);
+    if (rc != NCF_OK) return rc;
+    FxArgs A;
+    memset(&A, 0, sizeof(A));
+    A.prm = params;
+    A.w0 = params + lay->w[0];
+    A.g = grads;
+    A.xoff[0] = lay->um;
+    A.xoff[1] = lay->im;
+    A.r1[0] = lay->user_num;
+    A.r1[1] = lay->item_num;
+    A.partials = partials;
+    A.w0snap = w0snap;
+    A.mode = (lay->flags & NCF_LAYOUT_FACT_DEFER_DX) ? FX_DW0 : FX_FULL;
+    const int nblk = fact_blocks(lay, &A.nbu);
+    return launch_fx(fe, lds, A, nblk, st);
+}
+
+// ncf_adam_step_fact: FX_DX over the Um / Im rows inside one rank's gradient shard
+// [shard_begin, shard_begin + shard_len) -- G in gshard, dX written over it.
+static int launch_fact_dx(const ncf_layout* lay, const float* w0snap, float* gshard, int64_t shard_begin,
+                          int64_t shard_len, hipStream_t st) {
+    const int DM = fact_dm(lay);
+    const void* fe;
+    int64_t lds;
+    int rc = fact_expand_entry(DM, &fe, &lds);
+    if (rc != NCF_OK) return rc;
+    FxArgs A;
+    memset(&A, 0, sizeof(A));
+    A.w0 = w0snap;
+    A.g = gshard;
+    A.gofs = shard_begin;
+    A.xoff[0] = lay->um;
+    A.xoff[1] = lay->im;
+    A.mode = FX_DX;
+    const int64_t nrows[2] = {lay->user_num, lay->item_num};
+    const int64_t per = (int64_t)fact_ch(lay) * fact_cpb(lay);
+    int64_t nb[2];
+    for (int t = 0; t < 2; ++t) {  // the table's rows inside the shard (rows never straddle: 64-aligned)
+        int64_t lo = (shard_begin - A.xoff[t] + DM - 1), hi = shard_begin + shard_len - A.xoff[t];
+        lo = lo < 0 ? 0 : lo / DM;
+        hi = hi < 0 ? 0 : hi / DM;
+        if (hi > nrows[t]) hi = nrows[t];
+        if (lo > hi) lo = hi;
+        A.r0[t] = lo;
+        A.r1[t] = hi;
+        nb[t] = (hi - lo + per - 1) / per;
     }
-    ncf_layout l = *lay;
-    int nbu;
-    int nblk = fact_blocks(lay, &nbu);
-    int dw0_only = (lay->flags & NCF_LAYOUT_FACT_DEFER_DX) ? 1 : 0;
-    if (ensure_lds(fe, lds) != NCF_OK) return NCF_E_LAUNCH;
-    void* ae[] = {&l, (void*)&params, (void*)&grads, (void*)&partials, &nbu, &dw0_only, (void*)&w0snap};
-    if (hipLaunchKernel(fe, dim3((unsigned)nblk), dim3(FX_WAVES * 64), ae, (size_t)lds, st) != hipSuccess)
-        return NCF_E_LAUNCH;
-    return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
+    A.nbu = (int)nb[0];
+    return launch_fx(fe, lds, A, (int)(nb[0] + nb[1]), st);
 }
 
 }  // namespace ncf
@@ -1797,7 +1898,7 @@ int64_t ncf_fact_partials_bytes(const ncf_layout* lay) {
 int ncf_layout_tune(ncf_layout* lay, int64_t rows) {
     if (!lay || rows <= 0) return NCF_E_ARG;
     int32_t f = lay->flags & ~(NCF_LAYOUT_PER_ROW_L0 | (NCF_LAYOUT_GEO_MASK << NCF_LAYOUT_GEO_SHIFT) |
-                               (NCF_LAYOUT_WG_MASK << NCF_LAYOUT_WG_SHIFT));
+                               (NCF_LAYOUT_WG_MASK << NCF_LAYOUT_WG_SHIFT) | NCF_LAYOUT_USER_STORE);
     if (2 * rows < (int64_t)lay->user_num + lay->item_num) f |= NCF_LAYOUT_PER_ROW_L0;
     lay->flags = f;
     // geometry: forced (ncf_debug_set_geometry), else 8-wave workgroups where the
@@ -1821,10 +1922,23 @@ int ncf_layout_tune(ncf_layout* lay, int64_t rows) {
         }
     }
     f |= g << NCF_LAYOUT_GEO_SHIFT;
+    // user store-and-sum (user_sum_kernel), when enabled: forced, or by the per-rank
+    // batch (-1).  Off by default: at C3 the step kernel went 41.1 -> 39.2 us without
+    // its user atomics but the sum launch took 11.0 us (and the user order 1.7 us per
+    // step), 65.4 -> 75.6 us per step (profiles/r04_evidence/user_store_ab.json)
+    lay->flags = f;
+    if (us_applies(lay) && (g_user_store == 1 || (g_user_store < 0 && rows >= NCF_US_MIN_ROWS)))
+        f |= NCF_LAYOUT_USER_STORE;
     const int tr = 16 * geo_waves(g);
     const int64_t tiles = (rows + tr - 1) / tr;
     if (tiles < SLAB_ROWS) f |= (int32_t)tiles << NCF_LAYOUT_WG_SHIFT;
     lay->flags = f;
+    return NCF_OK;
+}
+
+int ncf_debug_set_user_store(int mode) {
+    if (mode < -1 || mode > 1) return NCF_E_ARG;
+    g_user_store = mode;
     return NCF_OK;
 }
 
@@ -1871,11 +1985,15 @@ int ncf_supported(int mode, int F, int L) {
     return F <= LYR_MAX_FACTOR ? NCF_PATH_LAYERED : 0;
 }
 
+// fused-path workspace: slab rows, [factored: dW0 partials, W0 snapshot], [user store]
+static int64_t us_base_floats(const ncf_layout* lay) {
+    return (int64_t)SLAB_ROWS * ncf_slab_stride(lay) + (fact_mode(lay) ? fact_partials_floats(lay) + fact_w0_snap_floats(lay) : 0);
+}
+
 int64_t ncf_workspace_bytes(const ncf_layout* lay, int64_t rows) {
     if (!lay || rows < 0) return -1;
     if (train_fused(lay))
-        return ((int64_t)SLAB_ROWS * ncf_slab_stride(lay) +
-                (fact_mode(lay) ? fact_partials_floats(lay) + fact_w0_snap_floats(lay) : 0)) * 4;
+        return (us_base_floats(lay) + us_floats(lay, rows)) * 4;
     return lyr_workspace_floats(lay, rows, true, fact_mode(lay) ? fact_partials_floats(lay) : -1) * 4;
 }
 
@@ -1947,12 +2065,45 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
     a.stamps = g_stamps;
     a.slab = slab;
     a.logits_out = logits_out;
+    const bool us = us_on(lay) && user_order != nullptr;
+    if (us) {
+        a.ustore = slab + us_base_floats(lay);
+        a.uw = us_uw(lay);
+    }
     void* args[] = {&a};
     if (hipLaunchKernel(fn, dim3(slab_rows_of(lay)), dim3(geo_waves(geo) * WAVE), args, (size_t)lds,
                         (hipStream_t)stream) != hipSuccess)
         return NCF_E_LAUNCH;
-    const int rc = launch_status();
-    if (rc != NCF_OK || !fact_mode(lay)) return rc;
+    int rc = launch_status();
+    if (rc != NCF_OK) return rc;
+    if (us) {  // the stored user-side rows summed per user (before the factored expansion reads G)
+        UsArgs ua;
+        memset(&ua, 0, sizeof(ua));
+        ua.ustore = a.ustore;
+        ua.order = user_order;
+        ua.grads = grads;
+        ua.ctl = ctl;
+        ua.batch_global = batch_global;
+        ua.um = lay->um;
+        ua.ug = lay->ug;
+        ua.world = world;
+        ua.rank = rank;
+        ua.uw = a.uw;
+        ua.dmu = lay->model_type != NCF_MODEL_GMF ? (lay->factor_num << (lay->num_layers - 1)) : 0;
+        ua.f = lay->factor_num;
+        const int64_t waves = (rows_max + US_SPAN - 1) / US_SPAN;
+        const dim3 grid((unsigned)((waves + US_WAVES - 1) / US_WAVES)), blk(US_WAVES * 64);
+        const hipStream_t st = (hipStream_t)stream;
+        switch ((a.uw + 63) / 64) {
+            case 1: hipLaunchKernelGGL(user_sum_kernel<1>, grid, blk, 0, st, ua); break;
+            case 2: hipLaunchKernelGGL(user_sum_kernel<2>, grid, blk, 0, st, ua); break;
+            case 3: hipLaunchKernelGGL(user_sum_kernel<3>, grid, blk, 0, st, ua); break;
+            default: hipLaunchKernelGGL(user_sum_kernel<US_NCH>, grid, blk, 0, st, ua); break;
+        }
+        rc = launch_status();
+        if (rc != NCF_OK) return rc;
+    }
+    if (!fact_mode(lay)) return rc;
     // factored layer 0: the per-user / per-item D0 sums -> dUm, dIm, dW0 partials
     return launch_fact_expand(lay, params, grads, fact_partials(lay, workspace), fact_w0_snap(lay, workspace),
                               (hipStream_t)stream);
@@ -2085,34 +2236,31 @@ int ncf_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
     return launch_status();
 }
 
-int ncf_adam_step_fact(const ncf_layout* lay, const void* workspace, float* params, const float* gshard,
+// Sharded Adam of the factored path (dp_mode "zero1" with NCF_LAYOUT_FACT_DEFER_DX):
+// the reduce-scattered gradient shard holds, in its Um / Im rows, the summed
+// per-entity D0 sums G (the train step expanded only the dW0 partials), so the rank
+// that owns them forms dX = G W0half (the W0 the step ran with, from the snapshot)
+// in place -- fact_expand_kernel's FX_DX mode over the shard's rows -- and the plain
+// Adam launch follows.  The shard is 64-float aligned and DM divides 64 (and the
+// table offsets), so a G row never straddles two shards; its length is the ranges'
+// largest end.
+int ncf_adam_step_fact(const ncf_layout* lay, const void* workspace, float* params, float* gshard,
                        float* exp_avg, float* exp_avg_sq, const int64_t* ranges, int nranges, int64_t shard_begin,
                        ncf_step_ctl* ctl, double lr, double beta1, double beta2, double eps, int64_t loss_slot,
                        float* loss_hist, int64_t hist_len, void* stream) {
-    if (!lay || !workspace || !params || !gshard || !exp_avg || !exp_avg_sq || !ranges || !ctl) return NCF_E_ARG;
+    if (!lay || !workspace || !params || !gshard || !exp_avg || !exp_avg_sq || !ranges || !ctl || nranges <= 0)
+        return NCF_E_ARG;
     const int dm = fact_dm(lay);
-    if (!fact_mode(lay) || !train_fused(lay) || dm > 64 || (shard_begin & 63) ||
+    if (!fact_mode(lay) || !train_fused(lay) || dm > 64 || (shard_begin & 63) || (lay->um % dm) || (lay->im % dm) ||
         !(lay->flags & NCF_LAYOUT_FACT_DEFER_DX))
         return NCF_E_UNSUPPORTED;
-    int err = 0;
-    Ranges R = make_ranges(ranges, nranges, &err);
-    if (err) return NCF_E_ARG;
-    FactShard F;
-    F.w0s = fact_w0_snap(lay, const_cast<void*>(workspace));
-    F.um = lay->um;
-    F.im = lay->im;
-    F.nu = (int64_t)lay->user_num * dm;
-    F.ni = (int64_t)lay->item_num * dm;
-    F.base = shard_begin;
-    F.dm = dm;
-    const int64_t total = R.prefix[R.n];
-    int64_t grid = (total + 255) / 256;
-    if (grid > 4096) grid = 4096;
-    if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(adam_fact_kernel, dim3((int)grid), dim3(256), 0, (hipStream_t)stream, params, gshard, exp_avg,
-                       exp_avg_sq, R, F, ctl, lr, beta1, beta2, (float)eps, loss_slot, loss_hist, hist_len,
-                       sc_cache_for(ctl, stream));
-    return launch_status();
+    int64_t shard_len = 0;
+    for (int r = 0; r < nranges; ++r) shard_len = ranges[2 * r + 1] > shard_len ? ranges[2 * r + 1] : shard_len;
+    int rc = launch_fact_dx(lay, fact_w0_snap(lay, const_cast<void*>(workspace)), gshard, shard_begin, shard_len,
+                            (hipStream_t)stream);
+    if (rc != NCF_OK) return rc;
+    return ncf_adam_step(params, gshard, exp_avg, exp_avg_sq, ranges, nranges, ctl, lr, beta1, beta2, eps, loss_slot,
+                         loss_hist, hist_len, stream);
 }
 
 int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* params, float* grads, float* exp_avg,
@@ -2506,7 +2654,7 @@ int ncf_user_order(const uint64_t* rows, int64_t n, int64_t batch_global, int wo
 
 int ncf_uses_user_order(const ncf_layout* lay) {
     if (!lay) return 0;
-    return (fact_mode(lay) && !train_fused(lay) && lay->user_num <= UO_MAX_USERS) ? 1 : 0;
+    return ((fact_mode(lay) && !train_fused(lay) && lay->user_num <= UO_MAX_USERS) || us_on(lay)) ? 1 : 0;
 }
 
 int ncf_hr_ndcg(const float* logits, const int32_t* items, int64_t n, int batch, int top_k, int32_t* hr, float* ndcg,

@@ -583,7 +583,10 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                     const float dzq = sdz[q];
                     dWpG += dzq * (ugv[j] * igv[j]);
                     const float dgm = dzq * wpf;
-                    if (!DIAG_ON(a, DIAG_NO_GMF_SCATTER)) atomicAdd(a.grads + lay.ug + (int64_t)max(su[q], 0) * F + gf, dgm * igv[j]);
+                    if (a.ustore != nullptr)  // NCF_LAYOUT_USER_STORE: [Um part][Ug part] of row q
+                        a.ustore[(row0 + q) * a.uw + (S_::MLP ? S_::DM : 0) + gf] = dgm * igv[j];
+                    else if (!DIAG_ON(a, DIAG_NO_GMF_SCATTER))
+                        atomicAdd(a.grads + lay.ug + (int64_t)max(su[q], 0) * F + gf, dgm * igv[j]);
                     gIg[j] = dgm * ugv[j];
                 }
                 if constexpr (EARLY) load_gmf(su2 + (buf ^ 1) * TRW, si2 + (buf ^ 1) * TRW, l);
@@ -652,7 +655,9 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
                             for (int fi = 0; fi < NF; ++fi) {
                                 const int f = fi * FPI + l % FPI;
-                                if (!DIAG_ON(a, DIAG_NO_USER_SCATTER))
+                                if (a.ustore != nullptr)
+                                    a.ustore[(row0 + wr + qi * RPW + l / FPI) * a.uw + f] = uv[qi][fi];
+                                else if (!DIAG_ON(a, DIAG_NO_USER_SCATTER))
                                     atomicAdd(a.grads + lay.um + (int64_t)uid[qi] * DM + f, uv[qi][fi]);
                             }
                         }
@@ -664,7 +669,10 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int uu = max(su[wr + 4 * g + r], 0);
-                            if (c < DM) atomicAdd(a.grads + lay.um + (int64_t)uu * DM + c, lane_get(acc[0], r));
+                            if (c < DM && a.ustore != nullptr)
+                                a.ustore[(row0 + wr + 4 * g + r) * a.uw + c] = lane_get(acc[0], r);
+                            else if (c < DM)
+                                atomicAdd(a.grads + lay.um + (int64_t)uu * DM + c, lane_get(acc[0], r));
                         }
                     }
                 };
@@ -783,7 +791,9 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
                             for (int fi = 0; fi < NF; ++fi) {
                                 const int f = fi * FPI + l % FPI;
-                                if (!DIAG_ON(a, DIAG_NO_USER_SCATTER))
+                                if (a.ustore != nullptr)
+                                    a.ustore[(row0 + wr + qi * RPW + l / FPI) * a.uw + f] = uv[qi][fi];
+                                else if (!DIAG_ON(a, DIAG_NO_USER_SCATTER))
                                     atomicAdd(a.grads + lay.um + (int64_t)uid[qi] * DM + f, uv[qi][fi]);
                             }
                         }

@@ -263,6 +263,11 @@ class TrainEngine:
             wg = os.environ.get("NCF_WG_WAVES")
             if wg:
                 L.check(L.hip().ncf_debug_set_geometry(int(wg)), "ncf_debug_set_geometry")
+            # user store-and-sum (NCF_LAYOUT_USER_STORE, off by default): NCF_USER_STORE=1
+            # forces it, =auto applies the per-rank batch rule (A/B)
+            us = os.environ.get("NCF_USER_STORE")
+            if us in ("0", "1", "auto"):
+                L.check(L.hip().ncf_debug_set_user_store(-1 if us == "auto" else int(us)), "ncf_debug_set_user_store")
             L.check(L.hip().ncf_layout_tune(ctypes.byref(self.lay), per), "ncf_layout_tune")
             if os.environ.get("NCF_FORCE_LAYERED", "0") == "1":  # A/B: the layered path for any shape
                 self.lay.flags |= L.LAYOUT_LAYERED
@@ -306,8 +311,9 @@ class TrainEngine:
                                           self.model.item_num, self._touched_buf(rows).data_ptr(),
                                           L.stream_ptr(self.device)), "ncf_batch_touched")
         self.lazy = lazy
-        # layered factored layer 0: the rows of each rank slice by user, once per epoch
-        # (the step then sums user runs before its atomics, ncf_user_order)
+        # the rows of each rank slice by user, once per epoch (ncf_user_order): the layered
+        # factored layer 0 sums user runs before its atomics; the fused step with
+        # NCF_LAYOUT_USER_STORE sums its stored user-side rows over them
         self._uses_order = (os.environ.get("NCF_USER_ORDER", "1") == "1"
                             and bool(L.hip().ncf_uses_user_order(ctypes.byref(self.lay))))
         if self._uses_order:

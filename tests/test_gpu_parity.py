@@ -213,6 +213,59 @@ def _one_step(mt, f, Lyr, B, U, I, seed=11, zipf=1.3, flags=0, order=False, data
     return lay
 
 
+@pytest.mark.parametrize("mt,f,Lyr,B", [("NeuMF-end", 16, 3, 65536),  # C3 (factored layer 0)
+                                         ("NeuMF-end", 16, 3, 8192),   # C3 at N = 8
+                                         ("NeuMF-end", 8, 3, 1024),    # C2 (per-row layer 0, DM 32)
+                                         ("NeuMF-end", 8, 2, 4096),    # per-row, DM 16
+                                         ("NeuMF-end", 8, 1, 3000),    # per-row, DM 8
+                                         ("NeuMF-end", 32, 2, 8192),   # uw 96: two column chunks
+                                         ("NeuMF-end", 64, 1, 20000),  # uw 128
+                                         ("MLP", 8, 2, 4096), ("GMF", 16, 1, 3000)])
+def test_one_step_user_store_vs_oracle(mt, f, Lyr, B):
+    """NCF_LAYOUT_USER_STORE: the step stores every row's user-side gradient (Um and Ug
+    parts) into the workspace and user_sum_kernel adds each run of the user order
+    (pieces of 32 positions) into the user rows -- every gradient vs the oracle at
+    ml-1m ids on the tuned layout with the flag forced on, hot (zipf) items."""
+    import ncf_amd._lib as L
+    from ncf_amd import ops
+    U, I = 6041, 3707
+    _, m = _models(mt, f, Lyr, U=U, I=I, seed=11)
+    lay = type(ops.ensure_flat(m)[1]).from_buffer_copy(ops.ensure_flat(m)[1])
+    L.check(L.hip().ncf_layout_tune(L.ctypes.byref(lay), B), "tune")
+    lay = _one_step(mt, f, Lyr, B, U, I, flags=int(lay.flags) | L.LAYOUT_USER_STORE, order=True)
+    assert L.hip().ncf_uses_user_order(L.ctypes.byref(lay)) == 1
+
+
+@pytest.mark.parametrize("B,store", [(4096, 1), (20000, -1), (20000, 0)])
+def test_engine_user_store_trajectory_vs_oracle(B, store):
+    """The engine with the user store-and-sum (an option, off by default: forced on at
+    4,096 rows; by the tune rule at 20,000, and off) over 6 graph-replayed steps of
+    NCF(16,3) at ml-1m ids: losses vs the oracle's trajectory, then every step
+    teacher-forced."""
+    import ncf_amd._lib as L
+    assert L.hip().ncf_debug_set_user_store(store) == 0
+    try:
+        T = 6
+        ref, m, eng = _engine_for("NeuMF-end", 16, 3, 6041, 3707, 23)
+        rng = np.random.default_rng(47)
+        users = rng.integers(0, 6041, (T, B))
+        items = np.minimum(rng.zipf(1.3, (T, B)) - 1, 3706)
+        labels = (rng.random((T, B)) < 0.2).astype(np.int64)
+        _stream(eng, users, items, labels, B)
+        assert bool(eng.lay.flags & L.LAYOUT_USER_STORE) == (store != 0)
+        assert eng.user_order_ptr() is not None or store == 0
+        ref0 = {k: v.clone() for k, v in ref.state_dict().items()}
+        eng.run(T, use_graph=True)
+        torch.cuda.synchronize()
+        got_losses = eng.epoch_losses()[:T].copy()
+        opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+        np.testing.assert_allclose(got_losses, O.train_steps(ref, opt, users, items, labels), rtol=1e-5)
+        ref.load_state_dict(ref0)
+        _teacher_forced_steps(ref, m, eng, users, items, labels)
+    finally:
+        L.hip().ncf_debug_set_user_store(0)
+
+
 @pytest.mark.parametrize("waves", [8, 4, 2, 1])
 @pytest.mark.parametrize("mt,f,Lyr,B,U,I", [("NeuMF-end", 8, 3, 1024, 6041, 3707),     # C2 (per-row layer 0)
                                             ("NeuMF-end", 16, 3, 8192, 6041, 3707),    # C3 at N = 8 (factored)

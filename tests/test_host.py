@@ -339,3 +339,48 @@ def test_layout_tune_launch_geometry():
     assert tune(6041, 3707, 16, 3, 65536, waves=4) == (4, 0)
     assert tune(138494, 26745, 16, 3, 8192, waves=1) == (8, 64)  # no 1-wave kernel there
     assert lib.ncf_debug_set_geometry(5) != 0
+
+
+def test_layout_tune_user_store():
+    """NCF_LAYOUT_USER_STORE (the fused step stores its user-side gradient rows and a
+    second launch sums them per user over ncf_user_order): never set by default
+    (measured slower at C3); with ncf_debug_set_user_store(-1) ncf_layout_tune sets it
+    from 16,384 rows per launch up, where the fused path runs and the user order
+    exists (user_num <= 32,767), with 1 wherever it applies; the workspace grows by
+    (rows + 128, rounded to 64) x ([Um part][Ug part]) floats; ncf_uses_user_order
+    follows the flag on the fused path."""
+    import ncf_amd._lib as L
+    lib = L.hip()
+
+    def tune(U, I, f, nl, rows, mode=-1, mt="NeuMF-end"):
+        assert lib.ncf_debug_set_user_store(mode) == 0
+        try:
+            lay = L.layout(U, I, f, nl, mt)
+            assert lib.ncf_layout_tune(ctypes.byref(lay), rows) == 0
+            return bool(lay.flags & L.LAYOUT_USER_STORE), lay
+        finally:
+            lib.ncf_debug_set_user_store(0)
+
+    lay = L.layout(6041, 3707, 16, 3, "NeuMF-end")
+    assert lib.ncf_layout_tune(ctypes.byref(lay), 65536) == 0 and not lay.flags & L.LAYOUT_USER_STORE  # default
+
+    assert tune(6041, 3707, 16, 3, 65536)[0]           # C3 at N = 1, 2, 4
+    assert tune(6041, 3707, 16, 3, 16384)[0]
+    assert not tune(6041, 3707, 16, 3, 8192)[0]        # C3 at N = 8
+    assert not tune(6041, 3707, 8, 3, 1024)[0]         # C2
+    assert not tune(138494, 26745, 16, 3, 65536)[0]    # C4: no user order above 32,767 users
+    assert tune(6041, 3707, 8, 3, 1024, mode=1)[0]
+    assert not tune(6041, 3707, 16, 3, 65536, mode=0)[0]
+    assert lib.ncf_debug_set_user_store(2) != 0
+    on, lay = tune(6041, 3707, 16, 3, 65536)
+    off, lay0 = tune(6041, 3707, 16, 3, 65536, mode=0)
+    assert lib.ncf_uses_user_order(ctypes.byref(lay)) == 1 and lib.ncf_uses_user_order(ctypes.byref(lay0)) == 0
+    extra = lib.ncf_workspace_bytes(ctypes.byref(lay), 65536) - lib.ncf_workspace_bytes(ctypes.byref(lay0), 65536)
+    assert extra == 4 * (65536 + 128) * (64 + 16)
+    assert not tune(6041, 3707, 32, 3, 65536, mode=1)[0]  # layered path: its own user runs
+    for mt, f, nl, uw in (("MLP", 8, 2, 16), ("GMF", 16, 1, 16), ("NeuMF-end", 32, 2, 96), ("NeuMF-end", 64, 1, 128)):
+        on, lay = tune(6041, 3707, f, nl, 20000, mt=mt)
+        off, lay0 = tune(6041, 3707, f, nl, 20000, mode=0, mt=mt)
+        assert on and not off, mt
+        extra = lib.ncf_workspace_bytes(ctypes.byref(lay), 20000) - lib.ncf_workspace_bytes(ctypes.byref(lay0), 20000)
+        assert extra == 4 * ((20000 + 128 + 63) // 64 * 64) * uw, mt
