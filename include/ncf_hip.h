@@ -22,7 +22,8 @@ extern "C" {
 #endif
 
 /* 16: NCF_LAYOUT_USER_STORE (ncf_layout_tune; ncf_uses_user_order covers it),
- * ncf_debug_set_user_store; ncf_adam_step_fact's gshard is written (dX formed in place).
+ * ncf_debug_set_user_store; ncf_adam_step_fact: one launch, clears the local bucket
+ * (grads_local, grads_n arguments), gshard may be written.
  * 15: ncf_layout.flags gains the fused step's workgroup geometry (NCF_LAYOUT_GEO_*) and
  * NCF_LAYOUT_FACT_DEFER_DX; new ncf_adam_step_fact, ncf_prepare_epoch2
  * (NCF_PREP_CANONICAL), ncf_probe_gather_scatter, ncf_debug_set_geometry. */
@@ -303,21 +304,24 @@ int ncf_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq
  * NCF_LAYOUT_FACT_DEFER_DX; replaces optimizer.step(), train_neumf.py:90,115, on
  * this rank's shard).  gshard holds the reduce-scattered flat gradient shard
  * [shard_begin, shard_begin + n): in its Um / Im rows the summed per-entity D0 sums
- * G (the step deferred their expansion), elsewhere the gradient itself.  Two
- * launches: the expansion of the shard's Um / Im rows, dX = G W0[:, half] written
- * over G (W0 being the weights the step ran with, saved in the step's workspace,
- * since the Adam launch updates W0 when the shard holds it; MFMA tiles, the rows
- * inside [shard_begin, shard_begin + max range end)), then ncf_adam_step on the
- * active ranges (shard-relative) of params (the flat parameters + shard_begin),
- * which clears gshard's active ranges.  Fused path, factored layer 0 with dm <= 64,
- * shard_begin a multiple of 64: NCF_E_UNSUPPORTED otherwise.
- * Loss bookkeeping as ncf_adam_step (loss_slot shard-relative, or loss_hist NULL on
- * the other ranks).
+ * G (the step deferred their expansion), elsewhere the gradient itself.  One launch
+ * (since ABI 16): blocks over the shard's Um / Im rows form dX = G W0[:, half] on
+ * MFMA tiles (W0 being the weights the step ran with, saved in the step's workspace)
+ * and apply Adam to those elements from LDS; other blocks run Adam on the remaining
+ * active ranges (shard-relative) of params (the flat parameters + shard_begin); the
+ * rest clear grads_local[0, grads_n) (the local gradient bucket; may be NULL with
+ * grads_n 0) for the next step.  gshard itself is not cleared (the next
+ * reduce-scatter overwrites it).  Where a table window is not inside one active range
+ * or more than 8 ranges remain, the expansion runs in place in gshard and
+ * ncf_adam_step follows (same result).  Fused path, factored layer 0 with dm <= 64,
+ * shard_begin a multiple of 64: NCF_E_UNSUPPORTED otherwise.  Loss bookkeeping as
+ * ncf_adam_step (loss_slot shard-relative, or loss_hist NULL on the other ranks).
  */
 int ncf_adam_step_fact(const ncf_layout *lay, const void *workspace, float *params, float *gshard,
                        float *exp_avg, float *exp_avg_sq, const int64_t *ranges, int nranges, int64_t shard_begin,
-                       ncf_step_ctl *ctl, double lr, double beta1, double beta2, double eps, int64_t loss_slot,
-                       float *loss_hist, int64_t hist_len, void *stream);
+                       float *grads_local, int64_t grads_n, ncf_step_ctl *ctl, double lr, double beta1,
+                       double beta2, double eps, int64_t loss_slot, float *loss_hist, int64_t hist_len,
+                       void *stream);
 
 /*
  * ncf_reduce_slab + ncf_adam_step in one launch (single-process training: no

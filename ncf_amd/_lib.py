@@ -95,7 +95,7 @@ _HIP_PROTOS = {
                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                      c_i64, c_vp, c_i64, c_vp]),
     "ncf_adam_step_fact": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp,
-                                          ctypes.POINTER(c_i64), ctypes.c_int, c_i64, c_vp, ctypes.c_double,
+                                          ctypes.POINTER(c_i64), ctypes.c_int, c_i64, c_vp, c_i64, c_vp, ctypes.c_double,
                                           ctypes.c_double, ctypes.c_double, ctypes.c_double, c_i64, c_vp, c_i64,
                                           c_vp]),
     "ncf_reduce_adam_step": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_vp,

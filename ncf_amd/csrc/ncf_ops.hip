@@ -1654,6 +1654,148 @@ __global__ __launch_bounds__(FX_WAVES * 64) void fact_expand_kernel(FxArgs A) {
 }
 
 
+// ncf_adam_step_fact in one launch (dp_mode "zero1", NCF_LAYOUT_FACT_DEFER_DX, DM <= 64):
+// three block roles over the rank's gradient shard --
+//   [0, nbx)           one CH-row chunk of the Um / Im rows inside the shard each: G rows
+//                      (gshard) and the W0 half (the step's snapshot) to LDS, dX = G W0h
+//                      on MFMA tiles into LDS, then Adam on those elements straight from
+//                      LDS (their p, m, v requested before the MFMAs);
+//   [nbx, nbx + nba)   Adam over the shard's other active ranges (RA: the ranges minus the
+//                      two table windows);
+//   the rest           clear the local gradient bucket for the next step's accumulation.
+// gshard is not cleared (the next reduce-scatter overwrites all of it).
+struct FsArgs {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;            // shard views: element i = flat shard_begin + i
+    const float* w0s;    // W0 as the step ran with it, [DM][2 DM]
+    int64_t xrel[2];     // Um / Im offset - shard_begin
+    int64_t r0[2], r1[2];
+    int nbu, nbx, nba;
+    Ranges RA;
+    f4* zero;            // local bucket (f4s), may be null
+    int64_t zn4;
+    const ncf_step_ctl* ctl;
+    double lr, beta1, beta2;
+    float eps;
+    int64_t loss_slot;
+    float* loss_hist;
+    int64_t hist_len;
+    ScCache* scc;
+};
+
+template <int DM>
+__global__ __launch_bounds__(FX_WAVES * 64) void adam_fact_shard_kernel(FsArgs A) {
+#pragma clang fp contract(off)
+    using X_ = FxShape<DM>;
+    constexpr int CH = X_::CH, ST = X_::ST, NT = X_::NT, Q4 = X_::Q4;
+    static_assert(X_::CPB == 1, "one chunk per block");
+    __shared__ float sc[2];
+    const int tid = threadIdx.x, b = (int)blockIdx.x;
+    const int64_t t_step = A.ctl->adam_t;  // advanced by ncf_reduce_slab
+    if (b >= A.nbx + A.nba) {  // clear the local bucket
+        const int64_t nthr = (int64_t)(gridDim.x - A.nbx - A.nba) * blockDim.x;
+        for (int64_t q = (int64_t)(b - A.nbx - A.nba) * blockDim.x + tid; q < A.zn4; q += nthr)
+            A.zero[q] = f4{0.f, 0.f, 0.f, 0.f};
+        return;
+    }
+    step_scalars(A.scc, t_step, A.lr, A.beta1, A.beta2, sc);
+    step_scalars_ahead(A.scc, t_step, A.lr, A.beta1, A.beta2);
+    const float w1 = (float)(1.0 - A.beta1), b2 = (float)A.beta2, omb2 = (float)(1.0 - A.beta2);
+    if (b >= A.nbx) {  // plain Adam over RA
+        __syncthreads();
+        const float neg_step = sc[0], bc2s = sc[1];
+        const int64_t total = A.RA.prefix[A.RA.n];
+        const int64_t nthr = (int64_t)A.nba * blockDim.x;
+        for (int64_t q = (int64_t)(b - A.nbx) * blockDim.x + tid; q < total; q += nthr) {
+            int which;
+            const int64_t i = range_locate(A.RA, q, &which);
+            const f4 gg = *reinterpret_cast<const f4*>(A.g + i);
+            f4 mm = *reinterpret_cast<const f4*>(A.m + i);
+            f4 vv = *reinterpret_cast<const f4*>(A.v + i);
+            f4 pp = *reinterpret_cast<const f4*>(A.p + i);
+            adam_f4(pp, mm, vv, gg, w1, b2, omb2, bc2s, A.eps, neg_step);
+            *reinterpret_cast<f4*>(A.m + i) = mm;
+            *reinterpret_cast<f4*>(A.v + i) = vv;
+            *reinterpret_cast<f4*>(A.p + i) = pp;
+        }
+        if (b == A.nbx && tid == 0 && A.loss_hist != nullptr && A.loss_slot >= 0 && A.hist_len > 0) {
+            const int64_t bt = A.ctl->batch - 1;  // ncf_reduce_slab advanced it (record_loss)
+            A.loss_hist[((bt % A.hist_len) + A.hist_len) % A.hist_len] = A.g[A.loss_slot];
+        }
+        return;
+    }
+    // expansion + Adam of one chunk of table rows
+    extern __shared__ __attribute__((aligned(16))) float fsm[];
+    float* sW = fsm;           // W0[:, koff : koff + DM]  [DM][ST]
+    float* sG = sW + DM * ST;  // G rows  [CH][ST]
+    float* sO = sG + CH * ST;  // dX rows [CH][ST] (FxShape's X image unused)
+    const int w = tid >> 6, l = tid & 63, c = l & 15, g = l >> 4;
+    const int t = b < A.nbu ? 0 : 1;
+    const int64_t rend = A.r1[t];
+    const int64_t r0 = A.r0[t] + (int64_t)(t == 0 ? b : b - A.nbu) * CH;
+    const int64_t xrel = A.xrel[t];
+    constexpr int NW4 = DM * Q4, PW = (NW4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
+    constexpr int NR4 = CH * Q4, PR = (NR4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
+    f4 wv[PW], gv[PR], pp[PR], mm[PR], vv[PR];
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+        const int e4 = tid + q * FX_WAVES * 64, j = e4 / Q4, k4 = e4 - j * Q4;
+        wv[q] = e4 < NW4 ? *reinterpret_cast<const f4*>(A.w0s + (int64_t)j * 2 * DM + t * DM + 4 * k4)
+                         : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int q = 0; q < PR; ++q) {
+        const int e4 = tid + q * FX_WAVES * 64, row = e4 / Q4, k4 = e4 - row * Q4;
+        const bool ok = e4 < NR4 && r0 + row < rend;
+        const int64_t i = xrel + (r0 + row) * DM + 4 * k4;
+        const f4 z = f4{0.f, 0.f, 0.f, 0.f};
+        gv[q] = ok ? *reinterpret_cast<const f4*>(A.g + i) : z;
+        pp[q] = ok ? *reinterpret_cast<const f4*>(A.p + i) : z;
+        mm[q] = ok ? *reinterpret_cast<const f4*>(A.m + i) : z;
+        vv[q] = ok ? *reinterpret_cast<const f4*>(A.v + i) : z;
+    }
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+        const int e4 = tid + q * FX_WAVES * 64, j = e4 / Q4, k4 = e4 - j * Q4;
+        if (e4 < NW4) *reinterpret_cast<f4*>(sW + j * ST + 4 * k4) = wv[q];
+    }
+#pragma unroll
+    for (int q = 0; q < PR; ++q) {
+        const int e4 = tid + q * FX_WAVES * 64, row = e4 / Q4, k4 = e4 - row * Q4;
+        if (e4 < NR4) *reinterpret_cast<f4*>(sG + row * ST + 4 * k4) = gv[q];
+    }
+    __syncthreads();
+    // dX = G W0h, tiles (rt, nt): A[i = row][k = j] = G[row][j],  B[k = j][n = k'] = W0h[j][k']
+    for (int tt = w; tt < (CH / 16) * NT; tt += FX_WAVES) {
+        const int rt = tt / NT, nt = tt - rt * NT;
+        const bool nok = 16 * nt + c < DM;
+        f4 d = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < DM / 4; ++kk)
+            d = MFMA4(sG[(16 * rt + c) * ST + 4 * kk + g], nok ? sW[(4 * kk + g) * ST + 16 * nt + c] : 0.f, d);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (nok) sO[(16 * rt + 4 * g + q) * ST + 16 * nt + c] = lane_get(d, q);
+    }
+    __syncthreads();
+    const float neg_step = sc[0], bc2s = sc[1];
+#pragma unroll
+    for (int q = 0; q < PR; ++q) {
+        const int e4 = tid + q * FX_WAVES * 64, row = e4 / Q4, k4 = e4 - row * Q4;
+        if (e4 < NR4 && r0 + row < rend) {
+            const int64_t i = xrel + (r0 + row) * DM + 4 * k4;
+            const f4 gg = *reinterpret_cast<const f4*>(sO + row * ST + 4 * k4);
+            adam_f4(pp[q], mm[q], vv[q], gg, w1, b2, omb2, bc2s, A.eps, neg_step);
+            *reinterpret_cast<f4*>(A.m + i) = mm[q];
+            *reinterpret_cast<f4*>(A.v + i) = vv[q];
+            *reinterpret_cast<f4*>(A.p + i) = pp[q];
+        }
+    }
+}
+
+
 int launch_zero_f32(float* p, int64_t n, hipStream_t st) {
     if (!p || n < 0 || (n & 3) || (reinterpret_cast<uintptr_t>(p) & 15)) return NCF_E_ARG;
     if (n == 0) return NCF_OK;
@@ -2240,27 +2382,137 @@ int ncf_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
 // the reduce-scattered gradient shard holds, in its Um / Im rows, the summed
 // per-entity D0 sums G (the train step expanded only the dW0 partials), so the rank
 // that owns them forms dX = G W0half (the W0 the step ran with, from the snapshot)
-// in place -- fact_expand_kernel's FX_DX mode over the shard's rows -- and the plain
-// Adam launch follows.  The shard is 64-float aligned and DM divides 64 (and the
-// table offsets), so a G row never straddles two shards; its length is the ranges'
-// largest end.
+// and Adam applies it -- one launch, adam_fact_shard_kernel (each window of table rows
+// inside one active range, at most 8 other ranges), else fact_expand_kernel's FX_DX
+// mode in place and the plain Adam launch.  The same launch clears the local gradient
+// bucket (grads_local, grads_n floats) for the next step.  The shard is 64-float
+// aligned and DM divides 64 (and the table offsets), so a G row never straddles two
+// shards; its length is the ranges' largest end.
 int ncf_adam_step_fact(const ncf_layout* lay, const void* workspace, float* params, float* gshard,
                        float* exp_avg, float* exp_avg_sq, const int64_t* ranges, int nranges, int64_t shard_begin,
-                       ncf_step_ctl* ctl, double lr, double beta1, double beta2, double eps, int64_t loss_slot,
-                       float* loss_hist, int64_t hist_len, void* stream) {
+                       float* grads_local, int64_t grads_n, ncf_step_ctl* ctl, double lr, double beta1, double beta2,
+                       double eps, int64_t loss_slot, float* loss_hist, int64_t hist_len, void* stream) {
     if (!lay || !workspace || !params || !gshard || !exp_avg || !exp_avg_sq || !ranges || !ctl || nranges <= 0)
         return NCF_E_ARG;
+    if (grads_n < 0 || (grads_n & 3) || (grads_n > 0 && !grads_local)) return NCF_E_ARG;
     const int dm = fact_dm(lay);
     if (!fact_mode(lay) || !train_fused(lay) || dm > 64 || (shard_begin & 63) || (lay->um % dm) || (lay->im % dm) ||
         !(lay->flags & NCF_LAYOUT_FACT_DEFER_DX))
         return NCF_E_UNSUPPORTED;
+    int err = 0;
+    (void)make_ranges(ranges, nranges, &err);
+    if (err) return NCF_E_ARG;
+    const hipStream_t st = (hipStream_t)stream;
     int64_t shard_len = 0;
     for (int r = 0; r < nranges; ++r) shard_len = ranges[2 * r + 1] > shard_len ? ranges[2 * r + 1] : shard_len;
-    int rc = launch_fact_dx(lay, fact_w0_snap(lay, const_cast<void*>(workspace)), gshard, shard_begin, shard_len,
-                            (hipStream_t)stream);
-    if (rc != NCF_OK) return rc;
-    return ncf_adam_step(params, gshard, exp_avg, exp_avg_sq, ranges, nranges, ctl, lr, beta1, beta2, eps, loss_slot,
-                         loss_hist, hist_len, stream);
+    const float* w0s = fact_w0_snap(lay, const_cast<void*>(workspace));
+    FsArgs A;
+    memset(&A, 0, sizeof(A));
+    // the Um / Im rows inside the shard (rows never straddle: 64-aligned shard, DM | 64)
+    const int64_t xoff[2] = {lay->um, lay->im}, nrows[2] = {lay->user_num, lay->item_num};
+    int64_t wb[2], we[2];  // shard-relative windows
+    int nbt[2];
+    const int CH = fact_ch(lay);
+    for (int t = 0; t < 2; ++t) {
+        int64_t lo = shard_begin - xoff[t] + dm - 1, hi = shard_begin + shard_len - xoff[t];
+        lo = lo < 0 ? 0 : lo / dm;
+        hi = hi < 0 ? 0 : hi / dm;
+        if (hi > nrows[t]) hi = nrows[t];
+        if (lo > hi) lo = hi;
+        A.r0[t] = lo;
+        A.r1[t] = hi;
+        A.xrel[t] = xoff[t] - shard_begin;
+        wb[t] = A.xrel[t] + lo * dm;
+        we[t] = A.xrel[t] + hi * dm;
+        nbt[t] = (int)((hi - lo + CH - 1) / CH);
+    }
+    // the active ranges minus the windows; each window wholly inside one active range
+    // (else the two-launch form below)
+    int64_t ra[16];
+    int nra = 0;
+    bool fused = fact_cpb(lay) == 1;
+    for (int t = 0; t < 2 && fused; ++t) {
+        if (we[t] <= wb[t]) continue;
+        bool cov = false;
+        for (int r = 0; r < nranges; ++r) cov |= ranges[2 * r] <= wb[t] && we[t] <= ranges[2 * r + 1];
+        fused = cov;
+    }
+    for (int r = 0; r < nranges && fused; ++r) {
+        int64_t pieces[6] = {ranges[2 * r], ranges[2 * r + 1]};
+        int np = 1;
+        for (int t = 0; t < 2; ++t) {
+            if (we[t] <= wb[t]) continue;
+            int64_t out[6];
+            int no = 0;
+            for (int k = 0; k < np; ++k) {
+                const int64_t b = pieces[2 * k], e = pieces[2 * k + 1];
+                if (we[t] <= b || e <= wb[t]) { out[2 * no] = b; out[2 * no + 1] = e; ++no; continue; }
+                if (b < wb[t]) { out[2 * no] = b; out[2 * no + 1] = wb[t]; ++no; }
+                if (we[t] < e) { out[2 * no] = we[t]; out[2 * no + 1] = e; ++no; }
+            }
+            np = no;
+            for (int k = 0; k < 2 * np; ++k) pieces[k] = out[k];
+        }
+        for (int k = 0; k < np && fused; ++k) {
+            if (pieces[2 * k + 1] <= pieces[2 * k]) continue;
+            if (nra == 8) { fused = false; break; }
+            ra[2 * nra] = pieces[2 * k];
+            ra[2 * nra + 1] = pieces[2 * k + 1];
+            ++nra;
+        }
+    }
+    if (!fused) {  // two launches (+ the clear): the expansion in place, then the plain Adam
+        if (grads_n > 0) {
+            const int rc0 = launch_zero_f32(grads_local, grads_n, st);
+            if (rc0 != NCF_OK) return rc0;
+        }
+        const int rc = launch_fact_dx(lay, w0s, gshard, shard_begin, shard_len, st);
+        if (rc != NCF_OK) return rc;
+        return ncf_adam_step(params, gshard, exp_avg, exp_avg_sq, ranges, nranges, ctl, lr, beta1, beta2, eps,
+                             loss_slot, loss_hist, hist_len, stream);
+    }
+    if (nra == 0) {  // nothing outside the windows: an empty range keeps the loss bookkeeping
+        ra[0] = ra[1] = 0;
+        nra = 1;
+    }
+    A.RA = make_ranges(ra, nra, &err);
+    if (err) return NCF_E_ARG;
+    A.p = params;
+    A.g = gshard;
+    A.m = exp_avg;
+    A.v = exp_avg_sq;
+    A.w0s = w0s;
+    A.nbu = nbt[0];
+    A.nbx = nbt[0] + nbt[1];
+    const int64_t na4 = A.RA.prefix[A.RA.n];
+    int64_t nba = (na4 + FX_WAVES * 64 - 1) / (FX_WAVES * 64);
+    A.nba = (int)(nba < 1 ? 1 : (nba > 512 ? 512 : nba));
+    A.zero = reinterpret_cast<f4*>(grads_local);
+    A.zn4 = grads_n / 4;
+    int64_t nbz = (A.zn4 + 4 * FX_WAVES * 64 - 1) / (4 * FX_WAVES * 64);  // 4 f4 per thread
+    if (nbz > 512) nbz = 512;
+    A.ctl = ctl;
+    A.lr = lr;
+    A.beta1 = beta1;
+    A.beta2 = beta2;
+    A.eps = (float)eps;
+    A.loss_slot = loss_slot;
+    A.loss_hist = loss_hist;
+    A.hist_len = hist_len;
+    A.scc = sc_cache_for(ctl, stream);
+    const void* fn;
+    int64_t lds;
+    switch (dm) {
+#define NCF_FS(D) case D: fn = reinterpret_cast<const void*>(&adam_fact_shard_kernel<D>); lds = FxShape<D>::LDS; break;
+        NCF_FS(8) NCF_FS(16) NCF_FS(32) NCF_FS(64)
+#undef NCF_FS
+        default: return NCF_E_UNSUPPORTED;
+    }
+    if (ensure_lds(fn, lds) != NCF_OK) return NCF_E_LAUNCH;
+    void* ae[] = {&A};
+    const unsigned grid = (unsigned)(A.nbx + A.nba + nbz);
+    if (hipLaunchKernel(fn, dim3(grid), dim3(FX_WAVES * 64), ae, (size_t)lds, st) != hipSuccess) return NCF_E_LAUNCH;
+    return launch_status();
 }
 
 int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* params, float* grads, float* exp_avg,

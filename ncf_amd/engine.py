@@ -489,7 +489,9 @@ class TrainEngine:
                                                   "ncf_lazy_adam_step_packed")
             return
         if self.dp_mode in ("zero1", "sparse"):
-            if self.dp_mode == "zero1":  # the shard gradient is in gshard: clear the local bucket now
+            if self.dp_mode == "zero1" and not self._fact_shard:
+                # the shard gradient is in gshard: clear the local bucket now (the
+                # factored launch below clears it itself)
                 L.check(lib.ncf_zero_f32(self.grads.data_ptr(), self.grads.numel(), st), "ncf_zero_f32")
             ranges, nr = self._sranges, self._nsranges
             hist = self.loss_hist.data_ptr() if self.rank == self.loss_owner else None
@@ -497,9 +499,10 @@ class TrainEngine:
             ranges, nr = self._ranges, self._nranges
             hist = self.loss_hist.data_ptr()
         p, g = self._opt_ptrs
-        if self._fact_shard:  # the shard's G rows expanded inside the optimizer launch
+        if self._fact_shard:  # the shard's G rows expanded inside the optimizer launch (+ the bucket cleared)
             L.check(lib.ncf_adam_step_fact(ctypes.byref(self.lay), self.ws.data_ptr(), p, g, self.exp_avg.data_ptr(),
                                            self.exp_avg_sq.data_ptr(), ranges, nr, self.rank * self.shard,
+                                           self.grads.data_ptr(), self.grads.numel(),
                                            self.ctl.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps,
                                            self._loss_slot, hist, hist_len, st), "ncf_adam_step_fact")
         elif self.optimizer == "adam":
