@@ -631,6 +631,8 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
     if bm:
         host["boundary_join"] = float(np.mean([x[0] for x in bm]))
         host["boundary_rest"] = float(np.mean([x[1] for x in bm]))
+    host["sampler_threads"] = pipe.ds._get_sampler().threads if pipe.S else 0
+    host["words_threads"] = pipe._wordgen.threads
     return {"eng": eng, "model": model, "pipe": pipe, "snap": snap, "value": epochs * n_rows / dt, "dt": dt, "steps": k,
             "epochs": epochs, "fresh_epochs": fresh, "rows_per_epoch": n_rows, "batches_per_epoch": nb,
             "warmup_run": {"steps": warm + extra, "seconds": round(warm_s, 3), "trained_steps_kept": warm,

@@ -42,13 +42,30 @@ def _run(world, rank, group, mt, f, nl, use_graph, dp_mode=None):
     torch.manual_seed(3)
     m = NCF(U, I, f, nl, 0.0, mt).to("cuda:0")
     want = None
+    split = dp_mode == "zero1-split"
     if dp_mode == "auto-zero1":  # "auto" whose packed test fails on a model above the all-reduce size
         TrainEngine.ALLREDUCE_MAX_FLOATS = 1
         dp_mode, want = "auto", "zero1"
+    if split:
+        dp_mode = "zero1"
     eng = TrainEngine(m, lr=1e-3, world_size=world, rank=rank, process_group=group, dp_mode=dp_mode)
+    if split:
+        # every shard range cut in two (the same elements): a table window no longer
+        # sits inside one range, so ncf_adam_step_fact takes its two-launch form
+        import ctypes
+        rng = [(eng._sranges[2 * k], eng._sranges[2 * k + 1]) for k in range(eng._nsranges)]
+        cut = []
+        for b, e in rng:
+            mid = b + ((e - b) // 2 // 64) * 64
+            cut += [(b, mid), (mid, e)] if b < mid < e else [(b, e)]
+        assert len(cut) > len(rng)
+        eng._sranges = (ctypes.c_int64 * (2 * len(cut)))(*[x for q in cut for x in q])
+        eng._nsranges = len(cut)
     u, i, y = _batches()
     rows = torch.as_tensor(ops.pack_rows_host(u, i, y), device="cuda:0")
     eng.set_epoch_stream(rows, B)
+    if split:
+        assert eng._fact_shard  # the factored shard expansion is what the split ranges exercise
     eng.run(T, use_graph=use_graph)
     torch.cuda.synchronize()
     if want is not None:
@@ -96,7 +113,8 @@ def _free_port():
                                                        ("GMF", 16, 3, True, "sparse"),
                                                        ("NeuMF-end", 32, 3, True, "zero1"),
                                                        ("GMF", 16, 3, True, "zero1"),
-                                                       ("NeuMF-end", 16, 3, True, "auto-zero1")])
+                                                       ("NeuMF-end", 16, 3, True, "auto-zero1"),
+                                                       ("NeuMF-end", 16, 3, True, "zero1-split")])
 def test_two_ranks_match_single_rank(mt, f, nl, use_graph, dp_mode):
     _ranks_match_single_rank(2, mt, f, nl, use_graph, dp_mode)
 
