@@ -421,6 +421,8 @@ def setup_engine(cfg, ds, train, world, rank, dev, group, global_batch, seed=0):
 BOUNDARY = os.environ.get("NCF_BENCH_BOUNDARY", "auto")
 WARM_S = float(os.environ.get("NCF_BENCH_WARM_S", "0.5"))
 EARLY_MAX_STEPS = 1024
+# fresh epochs of the `sustained` figure (epochs above EARLY_MAX_STEPS steps: a quarter)
+SUSTAINED_EPOCHS = int(os.environ.get("NCF_BENCH_SUSTAINED_EPOCHS", "8"))
 
 
 def _early_boundary(eng):
@@ -633,7 +635,37 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
         host["boundary_rest"] = float(np.mean([x[1] for x in bm]))
     host["sampler_threads"] = pipe.ds._get_sampler().threads if pipe.S else 0
     host["words_threads"] = pipe._wordgen.threads
+    # sustained: SUSTAINED_EPOCHS more fresh epochs from the timed state -- each epoch's
+    # negatives, permutation and grouping built while earlier epochs train (the
+    # pipeline's side-stream build shares the device with the steps), as a long
+    # training run pays it; `value`'s short timed region starts with two epochs
+    # already built during the warm-up
+    sustained = None
+    ns = SUSTAINED_EPOCHS if nb <= EARLY_MAX_STEPS else max(1, SUSTAINED_EPOCHS // 4)
+    if whole_epochs and ns > 0:
+        restore_state(eng, snap)
+        _barrier(group, dev)
+        torch.cuda.synchronize(dev)
+        e1 = pipe.stats["epochs"]
+        t0 = time.perf_counter()
+        run_steps(eng, ns * nb, use_graph)
+        torch.cuda.synchronize(dev)
+        dts = time.perf_counter() - t0
+        _barrier(group, dev)
+        dts = _max_over_ranks(dts, group, dev)
+        hs = pipe.stats.get("host_ms", [])[-ns:]
+        sustained = {"value": ns * n_rows / dts, "ms_per_step": dts / (ns * nb) * 1e3, "epochs": ns,
+                     "fresh_epochs": pipe.stats["epochs"] - e1,
+                     "device_build_ms_per_epoch": None,
+                     "host_stage_ms": float(np.mean([h["stage"] for h in hs if "stage" in h])) if hs else None,
+                     "note": "consecutive fresh epochs after the timed ones, every epoch's host sampling and device "
+                             "build (rows, permutation, grouping on a side stream) inside the region; `value` times "
+                             "the driver's epochs, whose streams the warm-up prefetched"}
+        ev = pipe.device_ms()
+        if ev is not None:
+            sustained["device_build_ms_per_epoch"] = float(ev[0] + ev[1])
     return {"eng": eng, "model": model, "pipe": pipe, "snap": snap, "value": epochs * n_rows / dt, "dt": dt, "steps": k,
+            "sustained": sustained,
             "epochs": epochs, "fresh_epochs": fresh, "rows_per_epoch": n_rows, "batches_per_epoch": nb,
             "warmup_run": {"steps": warm + extra, "seconds": round(warm_s, 3), "trained_steps_kept": warm,
                            "note": f"untimed: whole epochs, >= --warmup steps and >= {WARM_S} s (device ramp on a fresh box); "
@@ -910,6 +942,7 @@ def main():
             "quality": {"HR@10": hr10, "NDCG@10": ndcg10, "epochs_trained": round(eng.state_step() / eng.num_batches, 2),
                         "last_batch_loss": m["final_loss"]},
             "e2e": e2e,
+            "sustained": m["sustained"],
             "frozen_epoch": {"value": m["frozen_value"], "ms_per_step": m["frozen_ms_per_step"],
                              "note": "the same steps with the last epoch stream reused (no new negatives or "
                                      "permutation): device + exchange rate"},

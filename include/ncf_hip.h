@@ -516,6 +516,9 @@ int ncf_probe_gather_scatter(const ncf_layout *lay, const float *params, float *
  * the per-rank batch (narrower workgroups for small batches), 8, 4, 2 or 1 waves =
  * forced where that kernel exists (A/B measurements, tests).  NCF_E_ARG otherwise. */
 int ncf_debug_set_geometry(int waves);
+/* Per-row layer 0 (NCF_LAYOUT_PER_ROW_L0) for later ncf_layout_tune calls: -1 = the
+ * tune rule (the default), 0 = never, 1 = always (A/B measurements). */
+int ncf_debug_set_per_row(int mode);
 /* User-side store-and-sum (NCF_LAYOUT_USER_STORE) for later ncf_layout_tune calls:
  * 0 = never (the default), -1 = from 16,384 rows per launch, 1 = wherever it applies. */
 int ncf_debug_set_user_store(int mode);

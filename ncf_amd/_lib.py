@@ -87,6 +87,7 @@ _HIP_PROTOS = {
     "ncf_slab_stride": (c_i64, [ctypes.POINTER(NcfLayout)]),
     "ncf_debug_set_diag": (ctypes.c_int, [ctypes.c_int]),
     "ncf_debug_set_user_store": (ctypes.c_int, [ctypes.c_int]),
+    "ncf_debug_set_per_row": (ctypes.c_int, [ctypes.c_int]),
     "ncf_debug_set_geometry": (ctypes.c_int, [ctypes.c_int]),
     "ncf_probe_gather_scatter": (ctypes.c_int, [ctypes.POINTER(NcfLayout), c_vp, c_vp, c_vp, c_vp, c_i64,
                                                 ctypes.c_int, c_vp]),

@@ -1316,6 +1316,8 @@ static int g_diag = 0;
 static unsigned long long* g_stamps = nullptr;
 // ncf_debug_set_geometry: 0 = ncf_layout_tune decides, 4 / NWAVES = forced (A/B, tests)
 static int g_geo_waves = 0;
+// ncf_debug_set_per_row: -1 = ncf_layout_tune's rule (2 rows < U + I), 0 / 1 forced (A/B)
+static int g_per_row = -1;
 // ncf_debug_set_user_store: 0 = off (the default: measured slower),
 // -1 = ncf_layout_tune decides by the per-rank batch, 1 = wherever it applies
 static int g_user_store = 0;
@@ -2041,7 +2043,8 @@ int ncf_layout_tune(ncf_layout* lay, int64_t rows) {
     if (!lay || rows <= 0) return NCF_E_ARG;
     int32_t f = lay->flags & ~(NCF_LAYOUT_PER_ROW_L0 | (NCF_LAYOUT_GEO_MASK << NCF_LAYOUT_GEO_SHIFT) |
                                (NCF_LAYOUT_WG_MASK << NCF_LAYOUT_WG_SHIFT) | NCF_LAYOUT_USER_STORE);
-    if (2 * rows < (int64_t)lay->user_num + lay->item_num) f |= NCF_LAYOUT_PER_ROW_L0;
+    if (g_per_row == 1 || (g_per_row < 0 && 2 * rows < (int64_t)lay->user_num + lay->item_num))
+        f |= NCF_LAYOUT_PER_ROW_L0;
     lay->flags = f;
     // geometry: forced (ncf_debug_set_geometry), else 8-wave workgroups where the
     // batch has GEO_MIN_WGS 128-row tiles and 4-wave ones below (twice the workgroups,
@@ -2075,6 +2078,12 @@ int ncf_layout_tune(ncf_layout* lay, int64_t rows) {
     const int64_t tiles = (rows + tr - 1) / tr;
     if (tiles < SLAB_ROWS) f |= (int32_t)tiles << NCF_LAYOUT_WG_SHIFT;
     lay->flags = f;
+    return NCF_OK;
+}
+
+int ncf_debug_set_per_row(int mode) {
+    if (mode < -1 || mode > 1) return NCF_E_ARG;
+    g_per_row = mode;
     return NCF_OK;
 }
 

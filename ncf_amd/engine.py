@@ -265,6 +265,9 @@ class TrainEngine:
                 L.check(L.hip().ncf_debug_set_geometry(int(wg)), "ncf_debug_set_geometry")
             # user store-and-sum (NCF_LAYOUT_USER_STORE, off by default): NCF_USER_STORE=1
             # forces it, =auto applies the per-rank batch rule (A/B)
+            pr = os.environ.get("NCF_PER_ROW")  # 0|1: force the layer-0 form (A/B)
+            if pr in ("0", "1"):
+                L.check(L.hip().ncf_debug_set_per_row(int(pr)), "ncf_debug_set_per_row")
             us = os.environ.get("NCF_USER_STORE")
             if us in ("0", "1", "auto"):
                 L.check(L.hip().ncf_debug_set_user_store(-1 if us == "auto" else int(us)), "ncf_debug_set_user_store")
