@@ -384,3 +384,38 @@ def test_layout_tune_user_store():
         assert on and not off, mt
         extra = lib.ncf_workspace_bytes(ctypes.byref(lay), 20000) - lib.ncf_workspace_bytes(ctypes.byref(lay0), 20000)
         assert extra == 4 * ((20000 + 128 + 63) // 64 * 64) * uw, mt
+
+
+def test_adam_step_fact_argument_checks():
+    """ncf_adam_step_fact (host logic, no GPU launch on these paths): missing pointers
+    or an odd bucket size are NCF_E_ARG; a layout without NCF_LAYOUT_FACT_DEFER_DX, a
+    per-row layer 0 or a misaligned shard are NCF_E_UNSUPPORTED; the debug switches
+    reject values outside their range."""
+    import ncf_amd._lib as L
+    lib = L.hip()
+    lay = L.layout(6041, 3707, 16, 3, "NeuMF-end")
+    assert lib.ncf_layout_tune(ctypes.byref(lay), 65536) == 0
+    buf = (ctypes.c_float * 64)()
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    rng = (ctypes.c_int64 * 2)(0, 64)
+    ctl = (ctypes.c_int64 * 6)()
+
+    def call(lay_, ws=p, grads=None, gn=0, sb=0, ranges=rng, nr=1):
+        return lib.ncf_adam_step_fact(ctypes.byref(lay_), ws, p, p, p, p, ranges, nr, sb, grads, gn,
+                                      ctypes.cast(ctl, ctypes.c_void_p), 1e-3, 0.9, 0.999, 1e-8, -1, None, 0, None)
+    assert call(lay, ws=None) == L.NCF_E_ARG
+    assert call(lay, gn=64) == L.NCF_E_ARG           # a bucket size without the bucket
+    assert call(lay, grads=p, gn=6) == L.NCF_E_ARG   # not a multiple of 4
+    assert call(lay, nr=0) == L.NCF_E_ARG
+    assert call(lay) == L.NCF_E_UNSUPPORTED          # the step did not defer dX
+    lay.flags |= L.LAYOUT_FACT_DEFER_DX
+    assert call(lay, sb=32) == L.NCF_E_UNSUPPORTED   # shard begin not 64-aligned
+    lay.flags |= 0x1                                  # NCF_LAYOUT_PER_ROW_L0: no factored layer 0
+    assert call(lay) == L.NCF_E_UNSUPPORTED
+    assert lib.ncf_debug_set_per_row(2) != 0 and lib.ncf_debug_set_per_row(-1) == 0
+    lay = L.layout(6041, 3707, 16, 3, "NeuMF-end")
+    assert lib.ncf_debug_set_per_row(1) == 0
+    try:
+        assert lib.ncf_layout_tune(ctypes.byref(lay), 65536) == 0 and lay.flags & 0x1
+    finally:
+        lib.ncf_debug_set_per_row(-1)
