@@ -826,7 +826,8 @@ def main():
     achieved_gbs = bytes_launch / (ms * 1e-3) / 1e9
     if path == L.PATH_FUSED:
         mode = {"GMF": 0, "MLP": 1}.get(mtype, 2)
-        names = [f"ncf::ncf_step_kernel<{f}, {nl}, {mode}, false, {'true' if fact else 'false'}>"]
+        waves = (8, 4, 2, 1)[(int(eng.lay.flags) >> L.LAYOUT_GEO_SHIFT) & L.LAYOUT_GEO_MASK]
+        names = [f"ncf::ncf_step_kernel<{f}, {nl}, {mode}, false, {'true' if fact else 'false'}, {waves}>"]
         if fact:
             names.append(f"ncf::fact_expand_kernel<{dm}>")
         kname = (f"ncf_step_kernel<{f},{nl},{mtype.split('-')[0]},FACT={str(fact).lower()}>"
