@@ -1173,11 +1173,15 @@ static void set_geo(KernelEntry& e) {
     using SG = Shape<F, L, MODE, NW>;
     using S8 = Shape<F, L, MODE>;
     constexpr bool regs_ok = NW == NWAVES || SG::WREG <= 16;  // the prologue's weight registers
+#ifndef NCF_FACT_WREG_MAX
+#define NCF_FACT_WREG_MAX 16
+#endif
+    constexpr bool fregs_ok = NW == NWAVES || SG::WREG <= NCF_FACT_WREG_MAX;  // (A/B switch)
     if constexpr (regs_ok && (!S8::MLP || S8::MT(0) * S8::KT(0) <= 8 || NW == NWAVES))
         e.train[G] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, false, NW>);
     else
         e.train[G] = nullptr;
-    if constexpr (S8::MLP && regs_ok)
+    if constexpr (S8::MLP && fregs_ok)
         e.train_fact[G] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, true, NW>);
     else
         e.train_fact[G] = nullptr;
