@@ -421,7 +421,7 @@ def setup_engine(cfg, ds, train, world, rank, dev, group, global_batch, seed=0):
 BOUNDARY = os.environ.get("NCF_BENCH_BOUNDARY", "auto")
 WARM_S = float(os.environ.get("NCF_BENCH_WARM_S", "0.5"))
 EARLY_MAX_STEPS = 1024
-# fresh epochs of the `sustained` figure (epochs above EARLY_MAX_STEPS steps: a quarter)
+# fresh epochs of the `sustained` figure (epochs above EARLY_MAX_STEPS steps: one)
 SUSTAINED_EPOCHS = int(os.environ.get("NCF_BENCH_SUSTAINED_EPOCHS", "8"))
 
 
@@ -641,7 +641,9 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
     # training run pays it; `value`'s short timed region starts with two epochs
     # already built during the warm-up
     sustained = None
-    ns = SUSTAINED_EPOCHS if nb <= EARLY_MAX_STEPS else max(1, SUSTAINED_EPOCHS // 4)
+    ns = SUSTAINED_EPOCHS if nb <= EARLY_MAX_STEPS else min(1, SUSTAINED_EPOCHS)
+    if os.environ.get("NCF_BENCH_SAME_DEVICE") == "1":
+        ns = 0  # a rehearsal of the N > 1 flow on one device: no measurement to extend
     if whole_epochs and ns > 0:
         restore_state(eng, snap)
         _barrier(group, dev)
