@@ -642,8 +642,6 @@ def measure(cfg, ds, train, world, rank, dev, group, global_batch, steps, warmup
     # already built during the warm-up
     sustained = None
     ns = SUSTAINED_EPOCHS if nb <= EARLY_MAX_STEPS else min(1, SUSTAINED_EPOCHS)
-    if os.environ.get("NCF_BENCH_SAME_DEVICE") == "1":
-        ns = 0  # a rehearsal of the N > 1 flow on one device: no measurement to extend
     if whole_epochs and ns > 0:
         restore_state(eng, snap)
         _barrier(group, dev)

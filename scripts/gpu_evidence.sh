@@ -71,7 +71,8 @@ if has multirank; then
     run mr_spawn2_c3 300 python bench.py --gpus 2 --steps 20 --warmup 5
     run mr_run2_c3 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5
-    run mr_spawn3_c4 400 python bench.py --gpus 3 --config c4 --no-weak --skip-eval --steps 20 --warmup 5
+    run mr_spawn3_c4 400 env NCF_BENCH_SUSTAINED_EPOCHS=0 python bench.py --gpus 3 --config c4 --no-weak \
+        --skip-eval --steps 20 --warmup 5
     unset NCF_BENCH_SAME_DEVICE NCF_BENCH_BACKEND
 fi
 if has stamps; then
