@@ -36,7 +36,7 @@ class HostSampler:
     (datasets.py:57: ``for x in self.features_ps``), membership from
     ``mem_users / mem_items`` (the keys of ``train_mat``, datasets.py:61), which
     default to the positives.  ``threads``: the parallel pass's pool (default
-    NCF_SAMPLER_THREADS or min(16, 3/4 of the CPUs); 1 = the sequential pass)."""
+    ``sampler_threads(len(pos_users))``; 1 = the sequential pass)."""
 
     def __init__(self, pos_users, pos_items, num_users, num_items, mem_users=None, mem_items=None, threads=None):
         self.pos_users = np.ascontiguousarray(pos_users, dtype=np.int32)
@@ -51,7 +51,7 @@ class HostSampler:
         if not self._h:
             raise RuntimeError("ncf_sampler_create2 failed")
         self.num_users, self.num_items = int(num_users), int(num_items)
-        self.set_threads(sampler_threads() if threads is None else threads)
+        self.set_threads(sampler_threads(len(pos_users)) if threads is None else threads)
 
     def set_threads(self, threads):
         if L.sampler_lib().ncf_sampler_set_threads(self._h, int(threads)) != 0:
@@ -106,15 +106,19 @@ class HostSampler:
         return out
 
 
-def sampler_threads():
+def sampler_threads(work=None):
     """Threads of a host sampler pool: NCF_SAMPLER_THREADS, else min(12, half this
-    rank's share of the CPUs the process may run on) -- a GPU box grants 16 CPUs per
-    GPU, and the rest are the training loop's (graph replays, the epoch pipeline's
-    staging, the HIP runtime): the pool only has to finish an epoch's draws while the
-    previous epoch trains (ml-20m on the box: 42 ms per epoch at 8 threads, 27 ms at
-    12).  The share is the CPUs divided by LOCAL_WORLD_SIZE (set by
-    torch.distributed.run and by bench.py's own spawn): the pools spin-wait inside a
-    pass, so N local ranks must not each size theirs for the whole machine."""
+    rank's share of the CPUs the process may run on), and, given the pass's size
+    `work` in positives, at most one thread per 125,000 of them (at least 4).  A GPU
+    box grants 16 CPUs per GPU, and the rest are the training loop's (graph replays,
+    the epoch pipeline's staging, the HIP runtime): the pool only has to finish an
+    epoch's draws while the previous epoch trains (ml-20m on the box: 42 ms per epoch
+    at 8 threads, 27 ms at 12; ml-1m, 994K positives: 1.4 ms at 8 threads against
+    1.9 ms at 12, profiles/r03_final/sampler_ml-1m.json and
+    profiles/r03_evidence/r03c_sampler_ml1m.jsonl).  The share is the CPUs divided by
+    LOCAL_WORLD_SIZE (set by torch.distributed.run and by bench.py's own spawn): the
+    pools spin-wait inside a pass, so N local ranks must not each size theirs for
+    the whole machine."""
     import os
     v = os.environ.get("NCF_SAMPLER_THREADS")
     if v:
@@ -124,7 +128,10 @@ def sampler_threads():
     except AttributeError:
         n = os.cpu_count() or 1
     lws = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
-    return max(1, min(12, (n // lws) // 2))
+    t = max(1, min(12, (n // lws) // 2))
+    if work is not None:
+        t = min(t, max(4, -(-int(work) // 125_000)))
+    return t
 
 
 def _membership_from(train_mat, features):

@@ -419,3 +419,21 @@ def test_adam_step_fact_argument_checks():
         assert lib.ncf_layout_tune(ctypes.byref(lay), 65536) == 0 and lay.flags & 0x1
     finally:
         lib.ncf_debug_set_per_row(-1)
+
+
+def test_sampler_threads_default(monkeypatch):
+    """sampler_threads: half the rank's CPU share, at most 12, and at most one thread per
+    125,000 positives of the pass (at least 4); NCF_SAMPLER_THREADS overrides."""
+    import os
+    from ncf_amd.data import sampler_threads
+    monkeypatch.delenv("NCF_SAMPLER_THREADS", raising=False)
+    monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(32)))
+    assert sampler_threads() == 12
+    assert sampler_threads(994_169) == 8          # ml-1m
+    assert sampler_threads(19_861_770) == 12      # ml-20m
+    assert sampler_threads(1_000) == 4
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")   # 4 CPUs per rank
+    assert sampler_threads(994_169) == 2
+    monkeypatch.setenv("NCF_SAMPLER_THREADS", "3")
+    assert sampler_threads(994_169) == 3
