@@ -659,20 +659,30 @@ class TrainEngine:
         return g
 
     # steps unrolled into one graph when the collective is captured too (single
-    # process): fewer graph launches, no host work between consecutive steps
-    GRAPH_STEPS = int(os.environ.get("NCF_GRAPH_STEPS", "8"))
+    # process): fewer graph launches, no host work between consecutive steps.
+    # NCF_GRAPH_STEPS fixes it; by default 32 for epochs above 1,024 steps (short
+    # steps: C2 19.10 -> 18.42 us, C5 12.57 -> 12.18 us against 8,
+    # profiles/r04_evidence/graph_steps_ab.log), else 8 (C3's 76-step epochs: fewer
+    # single-step remainder replays)
+    GRAPH_STEPS = int(os.environ.get("NCF_GRAPH_STEPS", "0"))
+
+    @property
+    def graph_steps(self):
+        if self.GRAPH_STEPS > 0:
+            return self.GRAPH_STEPS
+        return 32 if self.num_batches > 1024 else 8
 
     def capture(self):
         """Capture the step into hipGraph(s) (after at least one eager step)."""
         if self._capture_collective:
             self._graph = (self._graph_of(self._step_body),)
-            k = self.GRAPH_STEPS
+            k = self.graph_steps
             self._graph_k = None
             if k > 1:
                 def body():
                     for _ in range(k):
                         self._step_body()
-                self._graph_k = self._graph_of(body)
+                self._graph_k = (self._graph_of(body), k)  # the k-step graph and its step count
         else:
             self._graph = (self._graph_of(self._compute), self._graph_of(self._optimize))
             if self.dp_mode in ("allreduce", "touched"):
@@ -745,9 +755,9 @@ class TrainEngine:
             self._capture_buffers()
         left = n_steps - done
         if self._graph_k is not None:
-            k = self.GRAPH_STEPS
+            gk, k = self._graph_k
             for _ in range(left // k):
-                self._graph_k.replay()
+                gk.replay()
             left %= k
         if len(self._graph) == 3 and left >= 2:
             # eager all-reduce between graphs: compute(t0), then [optimize(t), compute(t+1)]
