@@ -660,17 +660,17 @@ class TrainEngine:
 
     # steps unrolled into one graph when the collective is captured too (single
     # process): fewer graph launches, no host work between consecutive steps.
-    # NCF_GRAPH_STEPS fixes it; by default 32 for epochs above 1,024 steps (short
-    # steps: C2 19.10 -> 18.42 us, C5 12.57 -> 12.18 us against 8,
-    # profiles/r04_evidence/graph_steps_ab.log), else 8 (C3's 76-step epochs: fewer
-    # single-step remainder replays)
+    # NCF_GRAPH_STEPS fixes it; by default the whole epoch for epochs of at most 128
+    # steps (C3's 76: 56.6 -> 56.1 us/step against 8 -- no single-step remainder
+    # replays), else 32 (C2 19.10 -> 18.42 us, C5 12.57 -> 12.18 us against 8; 128 no
+    # better), profiles/r04_evidence/graph_steps_ab.log
     GRAPH_STEPS = int(os.environ.get("NCF_GRAPH_STEPS", "0"))
 
     @property
     def graph_steps(self):
         if self.GRAPH_STEPS > 0:
             return self.GRAPH_STEPS
-        return 32 if self.num_batches > 1024 else 8
+        return self.num_batches if self.num_batches <= 128 else 32
 
     def capture(self):
         """Capture the step into hipGraph(s) (after at least one eager step)."""
