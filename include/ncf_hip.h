@@ -21,13 +21,15 @@
 extern "C" {
 #endif
 
-/* 16: NCF_LAYOUT_USER_STORE (ncf_layout_tune; ncf_uses_user_order covers it),
+/* 17: the owner-sharded sparse exchange (dp_mode "owner"): ncf_owner_plan,
+ * ncf_owner_plan_init, ncf_owner_lists, ncf_owner_pack, ncf_owner_adam, ncf_owner_unpack.
+ * 16: NCF_LAYOUT_USER_STORE (ncf_layout_tune; ncf_uses_user_order covers it),
  * ncf_debug_set_user_store; ncf_adam_step_fact: one launch, clears the local bucket
  * (grads_local, grads_n arguments), gshard may be written.
  * 15: ncf_layout.flags gains the fused step's workgroup geometry (NCF_LAYOUT_GEO_*) and
  * NCF_LAYOUT_FACT_DEFER_DX; new ncf_adam_step_fact, ncf_prepare_epoch2
  * (NCF_PREP_CANONICAL), ncf_probe_gather_scatter, ncf_debug_set_geometry. */
-#define NCF_ABI_VERSION 16
+#define NCF_ABI_VERSION 17
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -409,6 +411,66 @@ int ncf_lazy_adam_step_packed(const ncf_layout *lay, float *params, float *exp_a
                               const int32_t *touched, int64_t n_total, int64_t batch_global,
                               int32_t *last_step, float *step_scalars, int64_t ring, const float *packed,
                               void *stream);
+
+/*
+ * Owner-sharded sparse gradient exchange (data-parallel dp_mode "owner"; since ABI 17).
+ * Replaces, across `world` ranks, the reference's single-device loss.backward() +
+ * optimizer.step() over dense nn.Embedding tables (scripts/train_neumf.py:90,114-115;
+ * src/ncf/models.py:11-16): the embedding row `id` of either side (user, item) is owned
+ * by rank id % world; every rank holds the same epoch stream, so every rank knows the
+ * rows each rank slice of each global batch touches.  Per step, after ncf_train_step:
+ *   ncf_owner_pack    this rank's gradient rows of batch b into send[o] (o = 0..world-1,
+ *                     plan.send_floats each): slot k of side s holds the row of the k-th
+ *                     id (ascending) of S_b(o, s) = the ids of this rank's slice owned by o;
+ *                     the tower gradient (slab + W0 partials + loss, ncf_slab_stride
+ *                     floats) at plan.tail_offset of every chunk; those grads rows cleared
+ *   all_to_all        recv[r] = rank r's send[this rank]   (equal chunks; caller's RCCL)
+ *   ncf_owner_adam    for every row this rank owns: the world ranks' rows summed in rank
+ *                     order (R_b(r, s) = the ids of rank r's slice owned here), dense Adam
+ *                     over every owned row (torch.optim.Adam, _single_tensor_adam
+ *                     arithmetic, as ncf_adam_step); the tower: the world tails summed in
+ *                     rank order, Adam on the active ranges (replicated: bitwise the same
+ *                     on every rank); loss_hist and ctl as ncf_reduce_adam_step (snapshot);
+ *                     the updated rows of R_{b+1}(q, s) into send2[q] (plan.param_floats
+ *                     each, same slot order), q != this rank
+ *   all_to_all        recv2[o] = rank o's send2[this rank]
+ *   ncf_owner_unpack  rows of S_{b+1}(o, s), o != this rank, from recv2[o] into params.
+ * b + 1 wraps to batch 0 of the same stream.  A rank's replica holds current values of
+ * the rows it reads; every other row may be stale until the caller gathers the owners'
+ * rows (e.g. at the end of a run).  exp_avg / exp_avg_sq: full flat layout; the owned rows
+ * and the tower are used.
+ *
+ * ncf_owner_plan_init (host): geometry for the stream (n_total rows, batch_global) and
+ * max_u / max_i list slots per (rank, owner) -- the all_to_all chunk sizes.
+ * ncf_owner_lists: the per-batch records (plan.lists_bytes) for this rank, and in
+ * max_counts[2] (device int32, overwritten) the longest S list over every (batch, rank,
+ * owner) per side.  If max_counts exceeds max_u / max_i, the lists were truncated: build
+ * a plan with larger slots and call again before any step uses them.
+ * Limits: world <= 16, factor_num % 4 == 0, user_num, item_num <= 2^19.
+ */
+typedef struct ncf_owner_plan {
+    int32_t world, rank, max_u, max_i;
+    int64_t n_total, batch_global, nb;  /* the epoch stream and its batches */
+    int32_t row_u, row_i;               /* floats per user / item row (its active tables) */
+    int32_t chunk_u, chunk_i;           /* owned rows per optimizer block */
+    int64_t nchunk_u, nchunk_i;
+    int64_t record_ints, lists_bytes;   /* int32 per batch record; bytes of the lists */
+    int64_t send_floats, param_floats;  /* floats per destination: gradient / parameter exchange */
+    int64_t tail_offset;                /* tower gradient inside a gradient chunk */
+    int64_t off[4];                     /* Ug, Ig, Um, Im flat offsets (-1: inactive) */
+} ncf_owner_plan;
+int ncf_owner_plan_init(const ncf_layout *lay, const int64_t *ranges, int nranges, int64_t n_total,
+                        int64_t batch_global, int world, int rank, int max_u, int max_i, ncf_owner_plan *out);
+int ncf_owner_lists(const ncf_owner_plan *plan, const ncf_layout *lay, const uint64_t *rows, int32_t *lists,
+                    int32_t *max_counts, void *stream);
+int ncf_owner_pack(const ncf_owner_plan *plan, const ncf_layout *lay, const void *workspace, float *grads,
+                   const int32_t *lists, const ncf_step_ctl *ctl, float *send, void *stream);
+int ncf_owner_adam(const ncf_owner_plan *plan, const ncf_layout *lay, float *params, float *exp_avg,
+                   float *exp_avg_sq, const int64_t *ranges, int nranges, const int32_t *lists, ncf_step_ctl *ctl,
+                   double lr, double beta1, double beta2, double eps, float *loss_hist, int64_t hist_len,
+                   const float *recv, float *send2, void *stream);
+int ncf_owner_unpack(const ncf_owner_plan *plan, const ncf_layout *lay, float *params, const int32_t *lists,
+                     const ncf_step_ctl *ctl, const float *recv2, void *stream);
 
 /* Plain SGD p -= lr * g (optim.SGD(lr*10) on the --pretraining path, train_neumf.py:87-88). */
 int ncf_sgd_step(float *params, float *grads, const int64_t *ranges, int nranges,

@@ -29,7 +29,7 @@ NCF_E_ARG = -2
 NCF_E_LAUNCH = -3
 MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
 DZ_BCE, DZ_DLOGIT, DZ_KD = 0, 1, 2
-ABI_VERSION = 16  # include/ncf_hip.h NCF_ABI_VERSION
+ABI_VERSION = 17  # include/ncf_hip.h NCF_ABI_VERSION
 PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 LAYOUT_PER_ROW_L0, LAYOUT_WG_SHIFT, LAYOUT_WG_MASK = 0x1, 8, 0xFFF  # ncf_layout.flags (ncf_layout_tune)
 LAYOUT_LAYERED = 0x2  # ncf_layout.flags: training on the layered path even where a fused kernel exists
@@ -63,6 +63,17 @@ class NcfStepCtl(ctypes.Structure):
                 ("snap_batch", c_i64), ("snap_t", c_i64)]
 
 
+class NcfOwnerPlan(ctypes.Structure):
+    """include/ncf_hip.h ncf_owner_plan (dp_mode "owner", ABI 17)."""
+    _fields_ = [("world", c_i32), ("rank", c_i32), ("max_u", c_i32), ("max_i", c_i32),
+                ("n_total", c_i64), ("batch_global", c_i64), ("nb", c_i64),
+                ("row_u", c_i32), ("row_i", c_i32), ("chunk_u", c_i32), ("chunk_i", c_i32),
+                ("nchunk_u", c_i64), ("nchunk_i", c_i64), ("record_ints", c_i64), ("lists_bytes", c_i64),
+                ("send_floats", c_i64), ("param_floats", c_i64), ("tail_offset", c_i64), ("off", c_i64 * 4)]
+
+
+_OWNER = ctypes.POINTER(NcfOwnerPlan)
+_LAY = ctypes.POINTER(NcfLayout)
 _HIP_PROTOS = {
     "ncf_abi_version": (ctypes.c_int, []),
     "ncf_supported": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
@@ -137,6 +148,14 @@ _HIP_PROTOS = {
                                            ctypes.POINTER(c_i64), ctypes.c_int, c_vp,
                                            ctypes.c_double, ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_i64,
                                            c_vp]),
+    "ncf_owner_plan_init": (ctypes.c_int, [_LAY, ctypes.POINTER(c_i64), ctypes.c_int, c_i64, c_i64, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_int, _OWNER]),
+    "ncf_owner_lists": (ctypes.c_int, [_OWNER, _LAY, c_vp, c_vp, c_vp, c_vp]),
+    "ncf_owner_pack": (ctypes.c_int, [_OWNER, _LAY, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "ncf_owner_adam": (ctypes.c_int, [_OWNER, _LAY, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), ctypes.c_int, c_vp, c_vp,
+                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_vp, c_i64,
+                                      c_vp, c_vp, c_vp]),
+    "ncf_owner_unpack": (ctypes.c_int, [_OWNER, _LAY, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
 _SAMPLER_PROTOS = {

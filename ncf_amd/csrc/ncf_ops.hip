@@ -44,11 +44,11 @@ __device__ __forceinline__ f4 w0_part_sum(const W0Part& P, int j, int rg) {
     return s;
 }
 
-__global__ __launch_bounds__(256) void reduce_slab_kernel(const float* __restrict__ slab, float* __restrict__ out,
-                                                          int lo, int stride, int rows, ncf_step_ctl* ctl, W0Part wp) {
-    __shared__ f4 part[16][16];
-    const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
-    const int j = lo + (blockIdx.x * 16 + c4) * 4;
+// One float4 column j of the slab reduction by the 16 row groups of a 256-thread
+// block (thread = column c4 of 16, row group rg): the total, for the rg == 0 threads
+// (j < stride); every thread of the block must call it (one barrier).
+__device__ __forceinline__ f4 slab_column_total(const float* __restrict__ slab, int j, int stride, int rows,
+                                                const W0Part& wp, int rg, int c4, f4 (*part)[16]) {
     f4 s = f4{0.f, 0.f, 0.f, 0.f};
     if (j < wp.cols) {
         s = w0_part_sum(wp, j, rg);
@@ -67,15 +67,24 @@ __global__ __launch_bounds__(256) void reduce_slab_kernel(const float* __restric
     }
     part[rg][c4] = s;
     __syncthreads();
+    f4 t = part[0][c4];
     if (rg == 0 && j < stride) {
-        f4 t = part[0][c4];
 #pragma unroll
         for (int q = 1; q < 16; ++q) {
             const f4 v = part[q][c4];
             t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
         }
-        *reinterpret_cast<f4*>(out + j) = t;
     }
+    return t;
+}
+
+__global__ __launch_bounds__(256) void reduce_slab_kernel(const float* __restrict__ slab, float* __restrict__ out,
+                                                          int lo, int stride, int rows, ncf_step_ctl* ctl, W0Part wp) {
+    __shared__ f4 part[16][16];
+    const int c4 = threadIdx.x & 15, rg = threadIdx.x >> 4;
+    const int j = lo + (blockIdx.x * 16 + c4) * 4;
+    const f4 t = slab_column_total(slab, j, stride, rows, wp, rg, c4, part);
+    if (rg == 0 && j < stride) *reinterpret_cast<f4*>(out + j) = t;
     if (ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
         ctl->batch = ctl->batch + 1;
         ctl->adam_t = ctl->adam_t + 1;
@@ -484,7 +493,7 @@ __device__ __forceinline__ void stage_ring(const LazyArgs& a, int64_t t, float2*
     }
 }
 
-__device__ __forceinline__ int lz_row_w4(const LazyArgs& a, int side) {
+__host__ __device__ __forceinline__ int lz_row_w4(const LazyArgs& a, int side) {
     return (a.off[side] >= 0 ? a.w4[side] : 0) + (a.off[side + 2] >= 0 ? a.w4[side + 2] : 0);
 }
 
@@ -2931,3 +2940,6 @@ int ncf_hr_ndcg(const float* logits, const int32_t* items, int64_t n, int batch,
 }
 
 }  // extern "C"
+
+// dp_mode "owner" (ABI 17): the owner-sharded sparse exchange
+#include "ncf_owner.inc"

@@ -19,6 +19,11 @@ contiguous shard of each global batch.  The gradient exchange has two forms
   gradient buffer; the small dense tower / predict tail is all-reduced.  The
   parameter all-gather stays dense: dense Adam moves every row every step.
 
+* ``"owner"``: embedding row id owned by rank id % W; the touched rows' gradients go
+  to their owners and the rows each rank's next batch reads come back, two
+  fixed-size all-to-alls per step (device kernels ncf_owner_*, engine.py);
+  ``owner_gather_rows`` brings every replica up to date at the end of a run.
+
 All keep dense-Adam parity with the single-device run (Adam is elementwise).
 """
 from __future__ import annotations
@@ -178,6 +183,56 @@ def sparse_exchange(grads, tables, tail, shard, rank, world, group=None):
             table.index_add_(0, r_ids, r_rows)
         sent += (8 + 4 * w) * sum(in_s)
     return sent
+
+
+def capturable(t: torch.Tensor, group) -> bool:
+    """Collectives on `t` can sit inside a captured hipGraph: RCCL on device tensors."""
+    return group is not None and dist.get_backend(group) != "gloo" and t.device.type == "cuda"
+
+
+def all_to_all_equal(out: torch.Tensor, inp: torch.Tensor, group=None):
+    """out[r-th chunk] = rank r's inp[this rank's chunk], equal chunks (RCCL: one
+    all_to_all_single; gloo with device tensors: through host copies)."""
+    if _coll_ok(inp, group):
+        dist.all_to_all_single(out, inp, group=group)
+        return out
+    o = torch.empty(out.shape, dtype=out.dtype)
+    dist.all_to_all_single(o, inp.cpu(), group=group)
+    out.copy_(o)
+    return out
+
+
+def owner_gather_rows(flat: torch.Tensor, tables, world: int, rank: int, group=None):
+    """dp_mode "owner": every rank's owned rows (id % world == rank) of each table to
+    every rank, in place.  tables: [(flat offset, row width, rows)].  One all-gather of
+    the rows this rank owns, padded to ceil(rows / world) per table."""
+    dev = flat.device
+    pers = [(n + world - 1) // world for _, _, n in tables]
+    size = sum(p * w for p, (_, w, _) in zip(pers, tables))
+    mine = torch.zeros(size, dtype=flat.dtype, device=dev)
+    pos = 0
+    for p, (off, w, n) in zip(pers, tables):
+        t = flat[off:off + n * w].view(n, w)
+        own = t[rank::world]
+        mine[pos:pos + own.numel()].copy_(own.reshape(-1))
+        pos += p * w
+    if _coll_ok(mine, group):
+        out = torch.empty(world * size, dtype=flat.dtype, device=dev)
+        dist.all_gather_into_tensor(out, mine, group=group)
+    else:
+        parts = [torch.empty(size, dtype=flat.dtype) for _ in range(world)]
+        dist.all_gather(parts, mine.cpu(), group=group)
+        out = torch.cat(parts).to(dev)
+    out = out.view(world, size)
+    pos = 0
+    for p, (off, w, n) in zip(pers, tables):
+        t = flat[off:off + n * w].view(n, w)
+        for o in range(world):
+            k = len(range(o, n, world))
+            if k:
+                t[o::world] = out[o, pos:pos + k * w].view(k, w)
+        pos += p * w
+    return flat
 
 
 def init_from_env(backend="nccl"):

@@ -19,6 +19,14 @@ with the all-reduce issued between them, see ``_capture_collective``):
                          (train_neumf.py:90,115)
   5. zero1 / sparse: RCCL all-gather of the updated parameter shards (in place)
 
+dp_mode "owner" (ncf_owner_* in include/ncf_hip.h): embedding row id is owned by
+rank id % W; per step train + ncf_owner_pack (this rank's gradient rows bucketed by
+owner, the tower gradient in every bucket) -> all_to_all -> ncf_owner_adam (the
+owner sums the W contributions in rank order and runs dense Adam over all its rows;
+tower Adam replicated; the rows each rank's next batch reads packed) -> all_to_all
+-> ncf_owner_unpack.  No host synchronisation: the bucket lists of every step are
+built once per epoch from the stream every rank holds.
+
 Data parallelism: every rank holds the same epoch stream (same seeds, same
 sampler, same permutation); rank r processes rows [r*ceil(gb/W), ...) of each
 global batch, with dlogit scaled by 1/global_batch, so the summed gradient is
@@ -139,10 +147,12 @@ class TrainEngine:
                 if self.world_size > 1 else "single"
         # an explicit exchange mode stands at world 1 (a one-rank group still runs the
         # real collectives: how the captured-collective graph is tested on one GPU)
-        if dp_mode not in ("single", "zero1", "allreduce", "sparse", "touched", "auto"):
+        if dp_mode not in ("single", "zero1", "allreduce", "sparse", "touched", "auto", "owner"):
             raise ValueError(f"dp_mode {dp_mode!r}")
-        if dp_mode in ("touched", "auto") and not touched_ok:
-            raise ValueError("dp_mode 'touched' needs Adam, factor_num % 4 == 0 and tables of <= 2^19 rows")
+        if dp_mode in ("touched", "auto", "owner") and not touched_ok:
+            raise ValueError(f"dp_mode {dp_mode!r} needs Adam, factor_num % 4 == 0 and tables of <= 2^19 rows")
+        if dp_mode == "owner" and (distill is not None or self.world_size > 16):
+            raise ValueError("dp_mode 'owner': no distillation, at most 16 ranks")
         self.dp_mode = dp_mode
         # flat buffers padded to world x shard floats where the exchange shards them
         # (rank r owns [r*S, (r+1)*S)); "auto" pads too when its fallback would be zero1
@@ -203,6 +213,13 @@ class TrainEngine:
         self._last = None
         self._ring = None
         self._touched_lists = {}
+        # dp_mode "owner": plan (ncf_owner_plan), list slots high-water (max_u, max_i),
+        # per-stream-buffer bucket lists, the four exchange buffers
+        self._ow_plan = None
+        self._ow_M = (0, 0)
+        self._ow_lists = {}
+        self._ow_bufs = None
+        self._ow_max = None
         if dp_mode == "touched":  # packed gradients of the touched rows + tower, all-reduced
             self._packed = torch.zeros(int(L.hip().ncf_touched_packed_floats(ctypes.byref(self.lay), self._ranges,
                                                                              self._nranges, 1)),
@@ -292,6 +309,8 @@ class TrainEngine:
             self.ctl[0:1].zero_()
         if self.dp_mode == "auto":
             self._resolve_auto(batch_size)
+        if self.dp_mode == "owner":
+            self._owner_prepare(rows)
         # deferred Adam: touched rows of every batch of this stream (once per epoch)
         lazy = self._lazy_wanted()
         if self.lazy and not lazy:
@@ -348,6 +367,108 @@ class TrainEngine:
         else:
             lay.flags &= ~L.LAYOUT_FACT_DEFER_DX
 
+    # ------------------------------------------------------------ owner exchange
+    # list slots grow to OWNER_SLACK x the longest list seen (+16, multiples of 16): the
+    # exchange chunks keep one size (and the captured graphs stay valid) across epochs
+    OWNER_SLACK = 1.08
+
+    def _owner_plan_for(self, mu, mi):
+        P = L.NcfOwnerPlan()
+        L.check(L.hip().ncf_owner_plan_init(ctypes.byref(self.lay), self._ranges, self._nranges, self.n_total,
+                                            self.batch_size, self.world_size, self.rank, int(mu), int(mi),
+                                            ctypes.byref(P)), "ncf_owner_plan_init")
+        return P
+
+    def _owner_lists_buf(self, rows, plan):
+        key = (rows.data_ptr(), rows.numel(), self.batch_size)
+        ints = (int(plan.lists_bytes) + 3) // 4
+        buf = self._ow_lists.get(key)
+        if buf is None or buf.numel() < ints:
+            buf = self._ow_lists[key] = torch.zeros(ints, dtype=torch.int32, device=self.device)
+        return buf
+
+    def _owner_prepare(self, rows):
+        """The epoch's bucket lists (ncf_owner_lists) for stream buffer `rows`; the list
+        slots grow (the exchange buffers with them, graphs re-captured) when a list of
+        this stream is longer than the slots -- the same decision on every rank, which
+        all hold the same stream.  One host read of the two maxima per epoch."""
+        lib = L.hip()
+        st = L.stream_ptr(self.device)
+        if self._ow_max is None:
+            self._ow_max = torch.zeros(2, dtype=torch.int32, device=self.device)
+        mu, mi = self._ow_M
+        while True:
+            plan = self._owner_plan_for(mu, mi)
+            lists = self._owner_lists_buf(rows, plan)
+            L.check(lib.ncf_owner_lists(ctypes.byref(plan), ctypes.byref(self.lay), rows.data_ptr(), lists.data_ptr(),
+                                        self._ow_max.data_ptr(), st), "ncf_owner_lists")
+            need_u, need_i = (int(x) for x in self._ow_max.cpu().tolist())
+            if need_u <= mu and need_i <= mi:
+                break
+            grow = lambda need, cur: max(cur, (int(need * self.OWNER_SLACK) + 16 + 15) // 16 * 16)  # noqa: E731
+            mu, mi = grow(need_u, mu), grow(need_i, mi)
+        old = self._ow_plan
+        self._ow_plan, self._ow_M = plan, (mu, mi)
+        same = old is not None and all(getattr(old, k) == getattr(plan, k) for k in ("max_u", "max_i", "n_total",
+                                                                                      "batch_global", "send_floats"))
+        if not same:
+            W = self.world_size
+            mk = lambda n: torch.zeros(W * int(n), dtype=torch.float32, device=self.device)  # noqa: E731
+            self._ow_bufs = (mk(plan.send_floats), mk(plan.send_floats), mk(plan.param_floats), mk(plan.param_floats))
+            self._drop_graphs()
+
+    def owner_bytes_per_step(self):
+        """(sent, received) bytes of this rank per step in the two all-to-alls (the chunk
+        for itself excluded)."""
+        P = self._ow_plan
+        per = 4 * (int(P.send_floats) + int(P.param_floats)) * (self.world_size - 1)
+        return per, per
+
+    def _owner_pack(self):
+        send = self._ow_bufs[0]
+        L.check(L.hip().ncf_owner_pack(ctypes.byref(self._ow_plan), ctypes.byref(self.lay), self.ws.data_ptr(),
+                                       self.grads.data_ptr(), self._owner_lists_buf(self.rows, self._ow_plan).data_ptr(),
+                                       self.ctl.data_ptr(), send.data_ptr(), L.stream_ptr(self.device)),
+                "ncf_owner_pack")
+
+    def _owner_a2a(self, k):
+        """k = 0: gradient buckets to their owners; 1: updated rows to their readers."""
+        out, inp = (self._ow_bufs[1], self._ow_bufs[0]) if k == 0 else (self._ow_bufs[3], self._ow_bufs[2])
+        if self.world_size == 1 and self.group is None:
+            out.copy_(inp)
+            return
+        D.all_to_all_equal(out, inp, self.group)
+
+    def _owner_adam(self):
+        _, recv, send2, _ = self._ow_bufs
+        L.check(L.hip().ncf_owner_adam(ctypes.byref(self._ow_plan), ctypes.byref(self.lay), self.flat.data_ptr(),
+                                       self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self._ranges,
+                                       self._nranges, self._owner_lists_buf(self.rows, self._ow_plan).data_ptr(),
+                                       self.ctl.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps,
+                                       self.loss_hist.data_ptr(), self.num_batches, recv.data_ptr(),
+                                       send2.data_ptr(), L.stream_ptr(self.device)), "ncf_owner_adam")
+
+    def _owner_unpack(self):
+        L.check(L.hip().ncf_owner_unpack(ctypes.byref(self._ow_plan), ctypes.byref(self.lay), self.flat.data_ptr(),
+                                         self._owner_lists_buf(self.rows, self._ow_plan).data_ptr(),
+                                         self.ctl.data_ptr(), self._ow_bufs[3].data_ptr(), L.stream_ptr(self.device)),
+                "ncf_owner_unpack")
+
+    def _owner_tables(self):
+        lay, m = self.lay, self.model
+        f, dm = m.factor_num, m.factor_num << (m.num_layers - 1)
+        P = self._ow_plan
+        return [(int(P.off[k]), w, n) for k, (w, n) in enumerate(((f, m.user_num), (f, m.item_num),
+                                                                   (dm, m.user_num), (dm, m.item_num)))
+                if P is not None and int(P.off[k]) >= 0]
+
+    def owner_sync(self):
+        """dp_mode "owner": every owner's rows of every table to every rank (the replica
+        of a rank is otherwise current only on the rows it reads).  A collective."""
+        if self.dp_mode != "owner" or self._ow_plan is None or self.world_size == 1:
+            return
+        D.owner_gather_rows(self.flat, self._owner_tables(), self.world_size, self.rank, self.group)
+
     def _order_buf(self, rows):
         """The user-order buffer that goes with epoch-stream buffer `rows`."""
         key = (rows.data_ptr(), rows.numel())
@@ -393,6 +514,8 @@ class TrainEngine:
     def flush(self):
         """Deferred Adam: every embedding row brought up to the current step (the
         parameters and moments are then the dense optimizer's).  No-op otherwise."""
+        if self.dp_mode == "owner":
+            self.owner_sync()
         if not self.lazy:
             return
         L.check(L.hip().ncf_lazy_adam_flush(ctypes.byref(self.lay), self.flat.data_ptr(), self.grads.data_ptr(),
@@ -423,6 +546,9 @@ class TrainEngine:
         gradients into the buffer the all-reduce sums; ctl advances in the optimizer)."""
         st = L.stream_ptr(self.device)
         self._train_launch()
+        if self.dp_mode == "owner":
+            self._owner_pack()
+            return
         if self.dp_mode == "touched":
             L.check(L.hip().ncf_touched_pack(ctypes.byref(self.lay), self.ws.data_ptr(), self.grads.data_ptr(),
                                              self._ranges, self._nranges, self._touched_buf(self.rows).data_ptr(),
@@ -439,7 +565,9 @@ class TrainEngine:
         allreduce: in-place sum of the whole flat gradient."""
         if self.dp_mode == "single":
             return
-        if self.dp_mode == "touched":
+        if self.dp_mode == "owner":
+            self._owner_a2a(0)
+        elif self.dp_mode == "touched":
             D.allreduce_flat_grads(self._packed, self.group)
         elif self.dp_mode == "zero1":
             D.reduce_scatter_flat(self.gshard, self.grads, self.rank, self.group)
@@ -468,8 +596,12 @@ class TrainEngine:
         self._hb += 1
 
     def _allgather(self):
-        """Launch 5 (zero1, sparse): every rank's updated parameter shard to every rank."""
-        if self.dp_mode in ("zero1", "sparse"):
+        """Launch 5 (zero1, sparse): every rank's updated parameter shard to every rank;
+        owner: the rows of every rank's next batch to it, then unpacked."""
+        if self.dp_mode == "owner":
+            self._owner_a2a(1)
+            self._owner_unpack()
+        elif self.dp_mode in ("zero1", "sparse"):
             if self._ag_scratch is None and not D._native_ok(self.flat, self.group):
                 self._ag_scratch = torch.empty_like(self.flat)
             D.all_gather_flat(self.flat, self.rank, self.shard, self.group, self._ag_scratch)
@@ -481,6 +613,9 @@ class TrainEngine:
         st = L.stream_ptr(self.device)
         lib = L.hip()
         hist_len = self.num_batches
+        if self.dp_mode == "owner":
+            self._owner_adam()
+            return
         if self.dp_mode == "touched":
             L.check(lib.ncf_lazy_adam_step_packed(ctypes.byref(self.lay), self.flat.data_ptr(), self.exp_avg.data_ptr(),
                                                   self.exp_avg_sq.data_ptr(), self._ranges, self._nranges,
@@ -582,6 +717,9 @@ class TrainEngine:
                      ({"zero1": "reduce_scatter", "sparse": "sparse_exchange"}.get(self.dp_mode, "allreduce"),
                       self._allreduce),
                      ("optimizer", self._optimize)]
+            if self.dp_mode == "owner":  # the pack is part of _compute, the unpack of the second exchange
+                parts = [("ncf_train_step+ncf_owner_pack", self._compute), ("all_to_all_grads", self._allreduce),
+                         ("ncf_owner_adam", self._optimize), ("all_to_all_params+ncf_owner_unpack", self._allgather)]
             if self.dp_mode == "touched":  # the pack is part of _compute
                 parts = [("ncf_train_step+ncf_touched_pack", self._compute), ("allreduce", self._allreduce),
                          ("ncf_lazy_adam_step_packed", self._optimize)]
@@ -646,6 +784,9 @@ class TrainEngine:
             return True
         if self.dp_mode == "sparse":  # bucket sizes go through the host every step
             return False
+        if self.dp_mode == "owner":  # RCCL: both all-to-alls inside the step graph unless turned off
+            default = "1" if D.capturable(self.grads, self.group) else "0"
+            return os.environ.get("NCF_CAPTURE_ALLREDUCE", default) == "1"
         return os.environ.get("NCF_CAPTURE_ALLREDUCE", "0") == "1"
 
     def _graph_of(self, fn):
@@ -683,6 +824,15 @@ class TrainEngine:
                     for _ in range(k):
                         self._step_body()
                 self._graph_k = (self._graph_of(body), k)  # the k-step graph and its step count
+        elif self.dp_mode == "owner":
+            # (compute, optimize, unpack + next compute, unpack): the collectives between
+            # them from the host (_run_owner)
+            def unpack_compute():
+                self._owner_unpack()
+                self._compute()
+            self._graph = ("owner", self._graph_of(self._compute), self._graph_of(self._optimize),
+                           self._graph_of(unpack_compute), self._graph_of(self._owner_unpack))
+            self._graph_k = None
         else:
             self._graph = (self._graph_of(self._compute), self._graph_of(self._optimize))
             if self.dp_mode in ("allreduce", "touched"):
@@ -711,6 +861,8 @@ class TrainEngine:
                     self._order_buf(buf)  # allocated outside the capture (filled when the buffer is set)
                 if self.lazy:
                     self._touched_buf(buf)
+                if self.dp_mode == "owner":  # allocated outside the capture (filled when the buffer is set)
+                    self._owner_lists_buf(buf, self._ow_plan)
                 self.capture()
         finally:
             self.rows, self._graph, self._graph_k = cur
@@ -720,6 +872,9 @@ class TrainEngine:
         self._graphs = {}
 
     def _replay(self):
+        if self._graph[0] == "owner":
+            self._run_owner(1)
+            return
         if len(self._graph) == 1:
             self._graph[0].replay()
         else:  # (compute, optimize[, optimize + compute])
@@ -759,6 +914,9 @@ class TrainEngine:
             for _ in range(left // k):
                 gk.replay()
             left %= k
+        if self._graph[0] == "owner":
+            self._run_owner(left)
+            return
         if len(self._graph) == 3 and left >= 2:
             # eager all-reduce between graphs: compute(t0), then [optimize(t), compute(t+1)]
             # per step, the last optimize after the loop -- the launch order of
@@ -772,6 +930,19 @@ class TrainEngine:
             return
         for _ in range(left):
             self._replay()
+
+    def _run_owner(self, n):
+        """n owner-mode steps from the graphs of capture(): compute(t0), then per step
+        a2a, optimize, a2a, [unpack(t) + compute(t + 1)], and the last unpack."""
+        if n <= 0:
+            return
+        _, g_c, g_o, g_uc, g_u = self._graph
+        g_c.replay()
+        for s in range(n):
+            self._owner_a2a(0)
+            g_o.replay()
+            self._owner_a2a(1)
+            (g_uc if s + 1 < n else g_u).replay()
 
     def epoch_losses(self):
         """Per-batch mean BCE of the last epoch (host copy).  zero1: the rank owning

@@ -328,3 +328,166 @@ def test_gloo_sparse_matches_single_process_adam(world):
         opt.step()
     ref = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).numpy()
     np.testing.assert_allclose(res[0][1], ref, rtol=1e-4, atol=1e-6)
+
+
+# ---------------------------------------------------------------------------
+# owner: row id owned by rank id % W; gradient rows to their owners, the next batch's
+# rows back to their readers (TrainEngine(dp_mode="owner"), include/ncf_hip.h
+# ncf_owner_*).  The protocol on CPU tensors, with the lists of tests/owner_model.py.
+
+def test_owner_lists_partition_each_slice():
+    """Model lists: per (batch, slice) the S lists of a rank partition its slice's
+    unique ids by owner; R(r) of owner o is S(o) of rank r; chunk starts bracket the
+    owned rows."""
+    from owner_model import chunk_starts, owner_lists, slice_ids, slices
+    rng = np.random.default_rng(0)
+    n, B, U, I = 2000, 300, 97, 61
+    rows = (rng.integers(0, U, n).astype(np.uint64) | (rng.integers(0, I, n).astype(np.uint64) << np.uint64(32)))
+    rows[5] = np.uint64(0xFFFFFFFF) | (np.uint64(0x7FFFFFFF) << np.uint64(32))  # padding row
+    for W in (1, 2, 3, 8):
+        per_rank = [owner_lists(rows, n, B, W, me)[0] for me in range(W)]
+        for b, r, lo, hi in slices(n, B, W):
+            uu, ii = slice_ids(rows, lo, hi)
+            for o in range(W):
+                for s, ids in enumerate((uu, ii)):
+                    want = ids[ids % W == o]
+                    assert np.array_equal(per_rank[r][b]["S"][o][s], want)
+                    assert np.array_equal(per_rank[o][b]["R"][r][s], want)
+                    ch = 4
+                    st = chunk_starts(want, o, W, ch, (max(U, I) + ch - 1) // ch)
+                    local = (want - o) // W
+                    for c in range(len(st) - 1):
+                        seg = local[st[c]:st[c + 1]]
+                        assert ((seg >= c * ch) & (seg < (c + 1) * ch)).all()
+
+
+def _owner_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle import ncf_oracle as O
+    from ncf_amd.distributed import all_to_all_equal, owner_gather_rows
+    from owner_model import owner_lists, slices
+    U, I, f, dm, B, T = 40, 60, 8, 32, 257, 3
+    torch.manual_seed(5)
+    m = O.OracleNCF(U, I, f, 3, 0.0, "NeuMF-end")
+    params = list(m.parameters())
+    n = sum(p.numel() for p in params)
+    offs = np.cumsum([0] + [p.numel() for p in params])
+    flat = torch.nn.Parameter(torch.cat([p.detach().reshape(-1) for p in params]))
+    opt = torch.optim.Adam([flat], lr=1e-2)
+    rng = np.random.default_rng(2)
+    u = rng.integers(0, U, B * T)
+    i = rng.integers(0, I, B * T)
+    y = (rng.random(B * T) < 0.3).astype(np.float32)
+    rows = u.astype(np.uint64) | (i.astype(np.uint64) << np.uint64(32))
+    lists, mx = owner_lists(rows, B * T, B, world, rank)
+    Mu, Mi = mx
+    tables = [(int(offs[k]), w, nr) for k, (w, nr) in enumerate(((f, U), (f, I), (dm, U), (dm, I)))]
+    tail0 = int(offs[4])
+    wrow = f + dm
+
+    def rows_of(vec, s, ids):  # [len(ids), f + dm] row records (GMF part, then MLP part)
+        g = vec[tables[s][0]:tables[s][0] + tables[s][2] * f].view(-1, f)[ids]
+        mm = vec[tables[s + 2][0]:tables[s + 2][0] + tables[s + 2][2] * dm].view(-1, dm)[ids]
+        return torch.cat([g, mm], 1)
+
+    def set_rows(vec, s, ids, val):
+        vec[tables[s][0]:tables[s][0] + tables[s][2] * f].view(-1, f)[ids] = val[:, :f]
+        vec[tables[s + 2][0]:tables[s + 2][0] + tables[s + 2][2] * dm].view(-1, dm)[ids] = val[:, f:]
+
+    M = (Mu, Mi)
+    D = (Mu + Mi) * wrow + (n - tail0)
+    D2 = (Mu + Mi) * wrow
+    sl = {(b, r): (lo, hi) for b, r, lo, hi in slices(B * T, B, world)}
+    for b in range(T):
+        with torch.no_grad():  # the replica into the model (rows this rank does not read may be stale)
+            for p, o0 in zip(params, offs[:-1]):
+                p.copy_(flat[o0:o0 + p.numel()].view_as(p))
+        m.zero_grad()
+        lo, hi = sl[(b, rank)]
+        logit = m(torch.as_tensor(u[lo:hi]), torch.as_tensor(i[lo:hi]))
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(logit, torch.as_tensor(y[lo:hi]),
+                                                                    reduction="sum") / B
+        loss.backward()
+        g = torch.cat([p.grad.reshape(-1) for p in params])
+        send = torch.zeros(world, D)
+        for o in range(world):
+            for s in range(2):
+                ids = torch.as_tensor(lists[b]["S"][o][s])
+                base = 0 if s == 0 else Mu * wrow
+                send[o, base:base + len(ids) * wrow] = rows_of(g, s, ids).reshape(-1)
+            send[o, D2:] = g[tail0:]
+        recv = torch.zeros(world, D)
+        all_to_all_equal(recv.view(-1), send.view(-1))
+        gsum = torch.zeros(n)  # owned rows and the tail, summed in rank order
+        for r in range(world):
+            gsum[tail0:] += recv[r, D2:]
+            for s in range(2):
+                ids = torch.as_tensor(lists[b]["R"][r][s])
+                base = 0 if s == 0 else Mu * wrow
+                got = recv[r, base:base + len(ids) * wrow].view(-1, wrow)
+                set_rows(gsum, s, ids, rows_of(gsum, s, ids) + got)
+        flat.grad = gsum
+        opt.step()
+        b1 = (b + 1) % T
+        send2 = torch.zeros(world, D2)
+        with torch.no_grad():
+            for qr in range(world):
+                for s in range(2):
+                    ids = torch.as_tensor(lists[b1]["R"][qr][s])
+                    base = 0 if s == 0 else Mu * wrow
+                    send2[qr, base:base + len(ids) * wrow] = rows_of(flat.detach(), s, ids).reshape(-1)
+            recv2 = torch.zeros(world, D2)
+            all_to_all_equal(recv2.view(-1), send2.view(-1))
+            for o in range(world):
+                if o == rank:
+                    continue
+                for s in range(2):
+                    ids = torch.as_tensor(lists[b1]["S"][o][s])
+                    base = 0 if s == 0 else Mu * wrow
+                    set_rows(flat.data, s, ids, recv2[o, base:base + len(ids) * wrow].view(-1, wrow))
+    with torch.no_grad():
+        owner_gather_rows(flat.data, tables, world, rank)
+    q.put((rank, flat.detach().numpy().copy(), M))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_owner_protocol_matches_single_process_adam(world):
+    """Three steps of the owner exchange (gradient rows to owners, dense Adam on every
+    owned row, the next batch's rows fetched, replicas stale elsewhere) then the
+    end-of-run gather: ranks bitwise equal, equal to single-process dense Adam."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 33500 + (os.getpid() % 1000) + 10 * world
+    procs = [ctx.Process(target=_owner_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, f, M in res[1:]:
+        assert M == res[0][2]
+        assert np.array_equal(f, res[0][1]), "ranks hold different parameters after the gather"
+    from oracle import ncf_oracle as O
+    torch.manual_seed(5)
+    m = O.OracleNCF(40, 60, 8, 3, 0.0, "NeuMF-end")
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+    rng = np.random.default_rng(2)
+    B, T = 257, 3
+    u = rng.integers(0, 40, B * T)
+    i = rng.integers(0, 60, B * T)
+    y = (rng.random(B * T) < 0.3).astype(np.float32)
+    for b in range(T):
+        s = slice(b * B, (b + 1) * B)
+        opt.zero_grad()
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(m(torch.as_tensor(u[s]), torch.as_tensor(i[s])),
+                                                                    torch.as_tensor(y[s]))
+        loss.backward()
+        opt.step()
+    ref = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).numpy()
+    np.testing.assert_allclose(res[0][1], ref, rtol=1e-4, atol=1e-6)

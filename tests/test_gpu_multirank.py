@@ -114,14 +114,20 @@ def _free_port():
                                                        ("NeuMF-end", 32, 3, True, "zero1"),
                                                        ("GMF", 16, 3, True, "zero1"),
                                                        ("NeuMF-end", 16, 3, True, "auto-zero1"),
-                                                       ("NeuMF-end", 16, 3, True, "zero1-split")])
+                                                       ("NeuMF-end", 16, 3, True, "zero1-split"),
+                                                       ("NeuMF-end", 16, 3, True, "owner"),
+                                                       ("NeuMF-end", 16, 3, False, "owner"),
+                                                       ("GMF", 16, 3, True, "owner"),
+                                                       ("MLP", 8, 2, True, "owner"),
+                                                       ("NeuMF-end", 32, 3, True, "owner")])
 def test_two_ranks_match_single_rank(mt, f, nl, use_graph, dp_mode):
     _ranks_match_single_rank(2, mt, f, nl, use_graph, dp_mode)
 
 
-def test_three_ranks_touched_match_single_rank():
-    """dp_mode "touched" at world 3 (B = 1000: shards of 334 / 334 / 332 rows)."""
-    _ranks_match_single_rank(3, "NeuMF-end", 16, 3, True, "touched")
+@pytest.mark.parametrize("dp_mode", ["touched", "owner"])
+def test_three_ranks_match_single_rank(dp_mode):
+    """World 3 (B = 1000: shards of 334 / 334 / 332 rows; owner: ids % 3)."""
+    _ranks_match_single_rank(3, "NeuMF-end", 16, 3, True, dp_mode)
 
 
 def _ranks_match_single_rank(world, mt, f, nl, use_graph, dp_mode):
@@ -164,7 +170,7 @@ def _rccl_worker(port, dp_mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dp_mode", ["zero1", "allreduce", "touched"])
+@pytest.mark.parametrize("dp_mode", ["zero1", "allreduce", "touched", "owner"])
 def test_rccl_collective_captured_in_step_graph(dp_mode):
     """NCF_CAPTURE_ALLREDUCE=1 on backend nccl (RCCL): the gradient exchange is
     captured inside the step graphs.  One GPU holds one RCCL rank, so a one-rank
