@@ -717,9 +717,10 @@ class TrainEngine:
                      ({"zero1": "reduce_scatter", "sparse": "sparse_exchange"}.get(self.dp_mode, "allreduce"),
                       self._allreduce),
                      ("optimizer", self._optimize)]
-            if self.dp_mode == "owner":  # the pack is part of _compute, the unpack of the second exchange
-                parts = [("ncf_train_step+ncf_owner_pack", self._compute), ("all_to_all_grads", self._allreduce),
-                         ("ncf_owner_adam", self._optimize), ("all_to_all_params+ncf_owner_unpack", self._allgather)]
+            if self.dp_mode == "owner":  # the pack is part of _compute
+                parts = [("ncf_train_step+ncf_owner_pack", self._compute),
+                         ("all_to_all_grads", lambda: self._owner_a2a(0)), ("ncf_owner_adam", self._optimize),
+                         ("all_to_all_params", lambda: self._owner_a2a(1)), ("ncf_owner_unpack", self._owner_unpack)]
             if self.dp_mode == "touched":  # the pack is part of _compute
                 parts = [("ncf_train_step+ncf_touched_pack", self._compute), ("allreduce", self._allreduce),
                          ("ncf_lazy_adam_step_packed", self._optimize)]

@@ -52,6 +52,11 @@ def main():
         ms = (time.perf_counter() - t0) / k * 1e3
         kt = eng.time_kernels(20)
         res[mode] = {"ms_per_step_graph": ms, "launch_groups_ms": kt}
+        if mode == "owner":  # the two all-to-alls' chunk per peer (bytes), the list slots
+            P = eng._ow_plan
+            res[mode]["owner"] = {"grad_chunk_bytes": 4 * int(P.send_floats), "param_chunk_bytes": 4 * int(P.param_floats),
+                                  "max_u": int(P.max_u), "max_i": int(P.max_i),
+                                  "lists_MB": int(P.lists_bytes) / 1e6}
         del eng, model
         torch.cuda.empty_cache()
     pipe.close()

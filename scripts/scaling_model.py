@@ -15,6 +15,12 @@ The one-GPU pool cannot run the N-rank RCCL transport, so the curve is projected
   xGMI bandwidth (7 links x ~153 GB/s per MI355X: a ring is per-link bound; the
   task's stated figure, not measured here) and alpha a per-collective latency
   (RCCL launch + ring steps; an assumption, varied over --alpha).
+* dp_mode "owner": two all-to-alls of fixed chunks per peer (the gradient rows with the
+  tower tail, then the next batch's rows); on the 8-GPU node every pair of GPUs has its
+  own xGMI link, so each all-to-all is  alpha + chunk / B_link  (the W - 1 chunks go out
+  on W - 1 links at once); B_link over --link-bw (the task's 153 GB/s per link, and a
+  pessimistic figure for RCCL's all-to-all).  The chunk sizes are the ones the engine
+  allocated at that world (dp_modes JSON "owner").
 
 Usage: scaling_model.py OUT.json dp_modes_c3_n2.json dp_modes_c3_n4.json ...
 (N = 1 is the single-process bench value, --n1-us per config)."""
@@ -22,9 +28,11 @@ import argparse
 import json
 
 
-def exchange_us(mode, n, floats, packed_floats, b_gbs, alpha_us):
+def exchange_us(mode, n, floats, packed_floats, b_gbs, alpha_us, owner=None):
     if n == 1:
         return 0.0
+    if mode == "owner":  # two all-to-alls, every peer on its own link
+        return 2 * alpha_us + (owner["grad_chunk_bytes"] + owner["param_chunk_bytes"]) / (b_gbs * 1e3)
     s = 4.0 * floats
     ring = (n - 1) / n
     if mode == "allreduce":
@@ -44,6 +52,9 @@ def main():
                     help="ring bus GB/s: one xGMI link (a single ring, per-link bound) and an "
                          "optimistic multi-ring figure over several of the 7 links")
     ap.add_argument("--alpha", type=float, nargs="+", default=[10.0, 25.0], help="us per collective")
+    ap.add_argument("--link-bw", type=float, nargs="+", default=[153.0, 64.0],
+                    help="all-to-all GB/s per peer link (owner mode): the stated xGMI link figure and a "
+                         "pessimistic one")
     ap.add_argument("--n1-us", type=json.loads, default={"c3": 55.9, "c4": 126.0},
                     help="single-process us/step per config (bench lines)")
     ap.add_argument("--floats", type=json.loads, default={"c3": 790737, "c4": 13230017})
@@ -61,10 +72,11 @@ def main():
             # without the emulated collectives (a one-rank group, or their exact
             # all-reduce forms over it, move nothing between GPUs)
             local = sum(1e3 * v for k, v in m["launch_groups_ms"].items()
-                        if k not in ("allreduce", "reduce_scatter", "all_gather"))
-            for bw in a.bw:
+                        if k not in ("allreduce", "reduce_scatter", "all_gather", "all_to_all_grads",
+                                     "all_to_all_params"))
+            for bw in (a.link_bw if mode == "owner" else a.bw):
                 for alpha in a.alpha:
-                    x = exchange_us(mode, n, a.floats[cfg], a.packed[cfg], bw, alpha)
+                    x = exchange_us(mode, n, a.floats[cfg], a.packed[cfg], bw, alpha, m.get("owner"))
                     t = local + x
                     rows.append({"config": cfg, "n_gpus": n, "mode": mode, "bw_GBps": bw, "alpha_us": alpha,
                                  "local_us": round(local, 1), "exchange_us": round(x, 1), "step_us": round(t, 1),
@@ -72,7 +84,8 @@ def main():
     for cfg, us in a.n1_us.items():
         rows.append({"config": cfg, "n_gpus": 1, "mode": "single", "bw_GBps": 0, "alpha_us": 0, "local_us": us,
                      "exchange_us": 0, "step_us": us, "interactions_per_s": a.batch / (us * 1e-6), "vs_1gpu": 1.0})
-    json.dump({"model": "T(N) = local(N) + ring collectives over xGMI", "rows": rows}, open(a.out, "w"), indent=1)
+    json.dump({"model": "T(N) = local(N) + ring collectives over xGMI (owner: two all-to-alls over the "
+                        "point-to-point links)", "rows": rows}, open(a.out, "w"), indent=1)
     for r in sorted(rows, key=lambda r: (r["config"], r["n_gpus"], r["mode"], r["bw_GBps"], r["alpha_us"])):
         print(f"{r['config']} N={r['n_gpus']} {r['mode']:9s} B={r['bw_GBps']:4.0f} a={r['alpha_us']:3.0f}  "
               f"local {r['local_us']:6.1f}  xchg {r['exchange_us']:6.1f}  step {r['step_us']:6.1f} us  "
