@@ -851,15 +851,16 @@ def main():
             tables_mb = 4 * (U + I) * (f + dm) / 1e6
             state_mb = 4 * 4 * int(eng.lay.total) / 1e6  # params, grads, two Adam moments
             roofline_cache = {
-                "bound": "cache", "achieved": achieved_gbs, "peak": ceil, "unit": "GB/s", "frac": achieved_gbs / ceil,
+                "achieved": achieved_gbs, "reference_rate": ceil, "unit": "GB/s", "ratio": achieved_gbs / ceil,
                 "probe": probe, "tables_MB": round(tables_mb, 2), "model_state_MB": round(state_mb, 2),
                 "resident": ("L2/MALL (tables fit the 4 MB L2 per XCD and the 256 MB MALL)" if tables_mb <= 4 else
                              "MALL-assisted (tables and optimizer state fit the 256 MB MALL)" if state_mb <= 256 else
                              "HBM (model state above the 256 MB MALL)"),
                 "note": "achieved = the step launch group's gather+scatter algorithmic bytes (roofline_hbm) / its "
-                        "time; peak = ncf_probe_gather_scatter: the same 16-byte row gathers and row-contiguous "
-                        "float-atomic adds (one per float: the step also sums item runs first), same rows and "
-                        "tables, no arithmetic, launches back to back -- the rate of the access pattern alone"}
+                        "time; reference_rate = ncf_probe_gather_scatter: the same 16-byte row gathers and "
+                        "row-contiguous float-atomic adds, same rows and tables, no arithmetic, launches back to "
+                        "back.  Not a ceiling: the probe issues one atomic per gathered float, the step sums item "
+                        "runs first (and the factored layer 0 scatters D0 rows), so ratio > 1 is possible"}
 
     # ---- weak scaling (extra field): global batch x N, per-GPU batch fixed -----
     weak = None

@@ -446,7 +446,7 @@ int ncf_lazy_adam_step_packed(const ncf_layout *lay, float *params, float *exp_a
  * max_counts[2] (device int32, overwritten) the longest S list over every (batch, rank,
  * owner) per side.  If max_counts exceeds max_u / max_i, the lists were truncated: build
  * a plan with larger slots and call again before any step uses them.
- * Limits: world <= 16, factor_num % 4 == 0, user_num, item_num <= 2^19.
+ * Limits: world <= 16, factor_num % 4 == 0, user_num, item_num <= 2^19, rows of at most 1,024 floats.
  */
 typedef struct ncf_owner_plan {
     int32_t world, rank, max_u, max_i;

@@ -307,6 +307,7 @@ class TrainEngine:
             self._ctl_n = n
         else:
             self.ctl[0:1].zero_()
+        self._check_stream_agreement(rows)
         if self.dp_mode == "auto":
             self._resolve_auto(batch_size)
         if self.dp_mode == "owner":
@@ -366,6 +367,54 @@ class TrainEngine:
             lay.flags |= L.LAYOUT_FACT_DEFER_DX
         else:
             lay.flags &= ~L.LAYOUT_FACT_DEFER_DX
+
+    def _check_stream_agreement(self, rows):
+        """world > 1: every rank must train on the same epoch stream (same seeds, and
+        the canonical grouping of ncf_prepare_epoch2): a device checksum of the stream,
+        max and -min over the ranks in one all-reduce.  The first stream is checked at
+        once; later ones asynchronously (flag copied to pinned memory, read at a later
+        epoch boundary when done), so the host does not wait for the running epoch.
+        Raises RuntimeError on a mismatch."""
+        if self.world_size == 1 or self.group is None:
+            return
+        import torch.distributed as dist
+        if dist.get_world_size(self.group) != self.world_size:
+            return  # an emulated world (scripts/dp_modes.py)
+        pend = getattr(self, "_stream_checks", None)
+        if pend is None:
+            pend = self._stream_checks = []
+        self._poll_stream_checks(block=False)
+        c = ops.stream_checksum(rows)
+        t = torch.stack([c, -c])
+        if D._coll_ok(t, self.group):
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        else:
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.MAX, group=self.group)
+            t = h.to(self.device)
+        bad = (t[0] + t[1]) != 0
+        flag = torch.empty(1, dtype=torch.bool, pin_memory=True)
+        flag.copy_(bad.view(1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        pend.append((flag, ev))
+        if not getattr(self, "_stream_checked_once", False):
+            self._stream_checked_once = True
+            self._poll_stream_checks(block=True)
+
+    def _poll_stream_checks(self, block):
+        keep = []
+        for flag, ev in getattr(self, "_stream_checks", []):
+            if block:
+                ev.synchronize()
+            if not ev.query():
+                keep.append((flag, ev))
+                continue
+            if bool(flag.item()):
+                raise RuntimeError("data-parallel ranks hold different epoch streams: build them from the same "
+                                   "seeds with the canonical grouping (ncf_prepare_epoch2 NCF_PREP_CANONICAL, "
+                                   "ops.EpochPrep(canonical=True) / EpochPipeline(canonical=True))")
+        self._stream_checks = keep
 
     # ------------------------------------------------------------ owner exchange
     # list slots grow to OWNER_SLACK x the longest list seen (+16, multiples of 16): the
@@ -467,6 +516,9 @@ class TrainEngine:
         of a rank is otherwise current only on the rows it reads).  A collective."""
         if self.dp_mode != "owner" or self._ow_plan is None or self.world_size == 1:
             return
+        import torch.distributed as dist
+        if self.group is None or dist.get_world_size(self.group) != self.world_size:
+            return  # an emulated world on a smaller group (scripts/dp_modes.py): timing only
         D.owner_gather_rows(self.flat, self._owner_tables(), self.world_size, self.rank, self.group)
 
     def _order_buf(self, rows):

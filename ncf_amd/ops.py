@@ -146,17 +146,43 @@ def pack_rows_host(users, items, labels=None):
     return r
 
 
+def default_canonical():
+    """True when torch.distributed runs more than one rank (the grouping must then be
+    NCF_PREP_CANONICAL so every rank's stream is identical)."""
+    import torch.distributed as dist
+    return bool(dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
+
+_CHECK_W = {}
+
+
+def stream_checksum(rows):
+    """Order-sensitive int64 checksum of a device epoch stream (one launch group, no
+    host sync): sum_k rows[k] * w_k (mod 2^64), w_k = odd hash of k."""
+    n = rows.numel()
+    key = (n, rows.device)
+    w = _CHECK_W.get(key)
+    if w is None:
+        w = (torch.arange(n, dtype=torch.int64, device=rows.device) * -7046029254386353131) | 1
+        _CHECK_W.clear()
+        _CHECK_W[key] = w
+    return (rows * w).sum()
+
+
 class EpochPrep:
     """ncf_prepare_epoch with its device workspace kept between epochs (stable
     pointers, so the output can feed a captured step graph).  canonical: the rows
     of one item inside a batch in (user, label) order (NCF_PREP_CANONICAL), so that
     every data-parallel rank building the stream gets the same positions."""
 
-    def __init__(self, device, canonical=False):
+    def __init__(self, device, canonical=None):
+        """canonical None: on whenever torch.distributed is initialised with more than
+        one rank (a data-parallel caller needs it; TrainEngine also checks that the
+        ranks' streams agree)."""
         self.device = torch.device(device)
         self.ws = None
         self.out = None
-        self.canonical = bool(canonical)
+        self.canonical = default_canonical() if canonical is None else bool(canonical)
 
     def __call__(self, rows, perm, batch_size, item_num, out=None):
         """On the current stream; into `out` (n int64 on the device) if given."""

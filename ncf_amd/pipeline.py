@@ -113,10 +113,11 @@ class EpochPipeline:
     depth + 1 sets of buffers, one being trained from."""
 
     def __init__(self, dataset, device, batch_size, item_num, user_num=None, prefetch=True, depth=None,
-                 canonical=False):
+                 canonical=None):
         """canonical: rows of one item inside a batch in (user, label) order
         (ncf_prepare_epoch2 NCF_PREP_CANONICAL) -- every rank of a data-parallel group
-        then builds the identical stream (set for world > 1)."""
+        then builds the identical stream; None: on when torch.distributed runs more
+        than one rank (ops.default_canonical)."""
         self.ds = dataset
         self.device = torch.device(device)
         self.batch_size = int(batch_size)

@@ -187,3 +187,45 @@ def test_rccl_collective_captured_in_step_graph(dp_mode):
     flat1, losses1 = _run(1, 0, None, "NeuMF-end", 16, 3, True)
     np.testing.assert_allclose(losses, losses1, rtol=1e-5)
     np.testing.assert_allclose(flat, flat1, rtol=1e-4, atol=1e-6)
+
+
+def _mismatch_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from ncf_amd import ops
+    from ncf_amd.engine import TrainEngine
+    from ncf_amd.models import NCF
+    torch.manual_seed(3)
+    m = NCF(U, I, 16, 3, 0.0, "NeuMF-end").to("cuda:0")
+    eng = TrainEngine(m, lr=1e-3, world_size=world, rank=rank, process_group=dist.group.WORLD, dp_mode="allreduce")
+    u, i, y = _batches()
+    if rank == 1:  # the same rows in another order: a non-canonical grouping would do this
+        u, i, y = u[::-1].copy(), i[::-1].copy(), y[::-1].copy()
+    rows = torch.as_tensor(ops.pack_rows_host(u, i, y), device="cuda:0")
+    try:
+        eng.set_epoch_stream(rows, B)
+        q.put((rank, "accepted"))
+    except RuntimeError as e:
+        q.put((rank, str(e)))
+    dist.destroy_process_group()
+
+
+def test_ranks_with_different_streams_are_refused():
+    """TrainEngine.set_epoch_stream at world > 1 checks that every rank holds the same
+    epoch stream (a device checksum, max / -min over the ranks): a rank with its rows
+    in another order makes every rank raise instead of training on shards that give
+    some rows to two ranks and others to none."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mismatch_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=120)
+    for r in range(2):
+        assert "different epoch streams" in res[r], res

@@ -24,6 +24,15 @@ the parameters after the run against the single-rank run by the trajectory crite
 of the single-rank tests (test_gpu_parity._assert_trajectory_close: the shard sums
 are the whole-batch sums in another fp32 order, which Adam turns into drift).
 
+Round 5 adds the owner-sharded exchange (dp_mode "owner": gradient rows to their
+owners, dense Adam per owner, the next batch's rows back) at the configs' own rank
+counts: C4 at world 2 and 4 over 100 steps, C3 at world 8 (8,192-row shards, one whole
+fresh epoch through Trainer.fit), and the bench's weak-scaling leg -- world 2 at a
+global batch of 131,072 -- against the oracle at batch_size 131,072.  Past the first
+steps at C4 the late tolerance is 1e-4: the reference's own fp32 loop, perturbed by
+one ulp per step, parts by ~1e-5 to 4e-5 within 100 steps at this shape
+(test_oracle.test_c4_fp32_trajectory_sensitivity).
+
 Every rank builds the same epoch stream: the grouping is canonical for world > 1
 (ncf_prepare_epoch2 NCF_PREP_CANONICAL; without it the rows of an item run sit in
 arrival order, which differs between the processes, and a shard boundary inside a run
@@ -61,7 +70,7 @@ def _flat(model):
     return torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu().numpy()
 
 
-def _c3_run(world, rank, group):
+def _c3_run(world, rank, group, batch=B):
     """Trainer.fit(1) at C3 (train_neumf.py:98-131), seeds 0 as the scripts set them."""
     from torch.utils.data import DataLoader
     from ncf_amd.models import NCF
@@ -70,7 +79,7 @@ def _c3_run(world, rank, group):
     np.random.seed(0)
     torch.manual_seed(0)
     model = NCF(ds["user_num"], ds["item_num"], 16, 3, 0.0, "NeuMF-end").to(DEV)
-    tr = Trainer(model, train, DataLoader(test, batch_size=100, shuffle=False), batch_size=B, lr=1e-3, top_k=10,
+    tr = Trainer(model, train, DataLoader(test, batch_size=100, shuffle=False), batch_size=batch, lr=1e-3, top_k=10,
                  verbose=False, world_size=world, rank=rank, process_group=group)
     tr.fit(1)
     torch.cuda.synchronize()
@@ -79,6 +88,11 @@ def _c3_run(world, rank, group):
     if eng.dp_mode == "zero1":
         assert eng._fact_shard  # the sharded factored expansion ran
     return _flat(model), losses, eng.dp_mode
+
+
+def _c3w_run(world, rank, group):
+    """The bench's weak-scaling leg: the per-GPU batch held at 65,536 (global B x world)."""
+    return _c3_run(world, rank, group, batch=B * world)
 
 
 def _c4_stream(train, item_num, dev):
@@ -97,7 +111,7 @@ def _c4_stream(train, item_num, dev):
 C4_STEPS = 20
 
 
-def _c4_run(world, rank, group):
+def _c4_run(world, rank, group, steps=C4_STEPS):
     from ncf_amd.engine import TrainEngine
     from ncf_amd.models import NCF
     ds, train, _ = _data("ml-20m")
@@ -107,13 +121,21 @@ def _c4_run(world, rank, group):
     eng = TrainEngine(model, lr=1e-3, world_size=world, rank=rank, process_group=group)
     stream = _c4_stream(train, ds["item_num"], DEV)
     eng.set_epoch_stream(stream, B, checked=True)
-    eng.run(C4_STEPS)
+    eng.run(steps)
     torch.cuda.synchronize()
-    losses = eng.epoch_losses()[:C4_STEPS].astype(np.float64).copy()
+    losses = eng.epoch_losses()[:steps].astype(np.float64).copy()
     return _flat(model), losses, eng.dp_mode
 
 
-RUNS = {"c3": _c3_run, "c4": _c4_run}
+def _c4l_run(world, rank, group):
+    """C4 over 100 steps."""
+    return _c4_run(world, rank, group, steps=100)
+
+
+# what dp_mode "auto" resolves to (TrainEngine.auto_dp_mode)
+AUTO_EXPECT = {("c3", 2): "allreduce", ("c3", 4): "allreduce", ("c3", 8): "allreduce", ("c4", 2): "touched"}
+
+RUNS = {"c3": _c3_run, "c4": _c4_run, "c4l": _c4l_run, "c3w": _c3w_run}
 
 
 def _worker(rank, world, port, name, q, dp_mode=None):
@@ -171,14 +193,16 @@ _single = {}
 
 
 def _single_rank(name):
+    """The single-rank run of the same config (the weak-scaling leg: at world 2's global
+    batch)."""
     if name not in _single:
-        _single[name] = RUNS[name](1, 0, None)
+        _single[name] = _c3_run(1, 0, None, batch=2 * B) if name == "c3w" else RUNS[name](1, 0, None)
     return _single[name]
 
 
-def _oracle_losses(name, steps):
+def _oracle_losses(name, steps, batch=B):
     """The reference loop's first `steps` losses from the same seeds (oracle)."""
-    ds, _, _ = _data("ml-20m" if name == "c4" else "ml-1m")
+    ds, _, _ = _data("ml-20m" if name.startswith("c4") else "ml-1m")
     U, I = ds["user_num"], ds["item_num"]
     pu, pi = ds["train_users"], ds["train_items"]
     torch.set_num_threads(min(16, torch.get_num_threads()))
@@ -189,30 +213,33 @@ def _oracle_losses(name, steps):
     items = np.concatenate([pi, neg]).astype(np.int64)
     labels = np.concatenate([np.ones(len(pu), np.int64), np.zeros(len(neg), np.int64)])
     perm = O.epoch_order(len(users))
-    sl = [perm[b * B:(b + 1) * B] for b in range(steps)]
+    sl = [perm[b * batch:(b + 1) * batch] for b in range(steps)]
     opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
     return np.asarray(O.train_steps(ref, opt, [users[s] for s in sl], [items[s] for s in sl],
                                     [labels[s] for s in sl]), dtype=np.float64)
 
 
 @pytest.mark.parametrize("name,world,dp_mode", [("c3", 2, None), ("c3", 4, None), ("c4", 2, None),
-                                                 ("c3", 4, "zero1")])
+                                                 ("c3", 4, "zero1"), ("c4l", 2, "owner"), ("c4l", 4, "owner"),
+                                                 ("c3", 8, "owner"), ("c3", 8, None), ("c3w", 2, "owner")])
 def test_full_shape_ranks_match_single_rank_and_oracle(name, world, dp_mode):
     """dp_mode None: the default ("auto"); "zero1" at C3: reduce-scatter, each rank
     expands the factored layer 0 of its own shard inside its Adam launch
-    (ncf_adam_step_fact), all-gather."""
+    (ncf_adam_step_fact), all-gather; "owner": the owner-sharded exchange."""
     res = _spawn(name, world, dp_mode)
     flat0, loss0, mode0 = res[0]
     for r in range(1, world):
         assert np.array_equal(res[r][1], loss0), f"rank {r} losses differ from rank 0"
         assert np.array_equal(res[r][0], flat0), f"rank {r} parameters differ from rank 0"
         assert res[r][2] == mode0
-    assert mode0 == (dp_mode or {"c3": "allreduce", "c4": "touched"}[name]), mode0
+    want = dp_mode or AUTO_EXPECT[(name, world)]
+    assert mode0 == want, mode0
     flat1, loss1, mode1 = _single_rank(name)
     assert mode1 == "single"
-    nb = {"c3": 76, "c4": C4_STEPS}[name]
+    nb = {"c3": 76, "c4": 20, "c4l": 100, "c3w": 38}[name]
     assert len(loss0) == len(loss1) == nb
-    ref = _oracle_losses(name, 20)
+    batch = 2 * B if name == "c3w" else B
+    ref = _oracle_losses(name, 20, batch)
     rel1 = np.abs(loss0 - loss1) / np.abs(loss1)
     relo = np.abs(loss0[:20] - ref) / np.abs(ref)
     rel1o = np.abs(loss1[:20] - ref) / np.abs(ref)
@@ -220,12 +247,20 @@ def test_full_shape_ranks_match_single_rank_and_oracle(name, world, dp_mode):
             f"{int(np.argmax(rel1 > 1e-5)) if (rel1 > 1e-5).any() else None}); vs oracle (20) {relo.max():.2e}; "
             f"1 rank vs oracle (20) {rel1o.max():.2e}; per step vs 1 rank {np.round(rel1 * 1e6, 2).tolist()} (1e-6)")
     print(info)
-    if name == "c3":
+    if name.startswith("c3"):
         assert relo.max() <= 1e-5, info
+        assert rel1.max() <= 1e-5, info
     else:
         assert relo[:10].max() <= 1e-5 and relo.max() <= 1e-4, info
-    assert rel1.max() <= 1e-5, info
+        # the steps the single rank holds to the oracle at 1e-5: held to the single rank at 1e-5
+        held = rel1o <= 1e-5
+        assert rel1[:20][held].max(initial=0.0) <= 1e-5, info
+        assert rel1.max() <= 1e-4, info
     # parameters after the free-running steps: two fp32 trajectories (shard sums vs
     # whole-batch sums) -- the criterion of the single-rank trajectory tests
     from test_gpu_parity import _assert_trajectory_close
-    _assert_trajectory_close(flat0, flat1, nb, 1e-3, f"{name} world {world}: params vs 1 rank")
+    # 100 steps at C4: the reference's own loop perturbed by one ulp per step leaves 9%
+    # of the elements outside the criterion (0.27% at 50 steps, 0.01% at 20; max dev
+    # 0.011) -- twice that is allowed
+    _assert_trajectory_close(flat0, flat1, nb, 1e-3, f"{name} world {world}: params vs 1 rank",
+                             off_max=0.2 if nb >= 100 else 0.10)

@@ -374,7 +374,7 @@ def test_engine_layered_factored_trajectory_vs_oracle(f, Lyr, T):
     _teacher_forced_steps(ref, m, eng, users, items, labels)
 
 
-def _assert_trajectory_close(got, exp, T, lr, name):
+def _assert_trajectory_close(got, exp, T, lr, name, off_max=0.10):
     """Parameters after T free-running Adam steps.  Two correct fp32 trajectories
     drift apart: Adam turns the summation-order noise of a near-zero gradient into
     up to ~lr of movement, and the drifted parameters later flip ReLU mask bits of
@@ -390,7 +390,7 @@ def _assert_trajectory_close(got, exp, T, lr, name):
     off = dev > tol
     info = f"{name}: max dev {dev.max(initial=0.0):.3g}, {off.mean():.5f} of elements off"
     assert float(dev.max(initial=0.0)) <= 4 * T * lr, info
-    assert off.mean() <= 0.10, info
+    assert off.mean() <= off_max, info
 
 
 def _relu_ties(ref, users, items, tau=1e-7):

@@ -437,3 +437,19 @@ def test_sampler_threads_default(monkeypatch):
     assert sampler_threads(994_169) == 2
     monkeypatch.setenv("NCF_SAMPLER_THREADS", "3")
     assert sampler_threads(994_169) == 3
+
+
+def test_stream_checksum_and_canonical_default():
+    """ops.stream_checksum is order-sensitive (ranks holding the same rows in another
+    order disagree); EpochPrep / EpochPipeline default to the canonical grouping
+    only where torch.distributed runs several ranks (not here)."""
+    from ncf_amd import ops
+    r = torch.arange(1000, dtype=torch.int64) * 7919 + (1 << 40)
+    c0 = int(ops.stream_checksum(r))
+    assert c0 == int(ops.stream_checksum(r.clone()))
+    assert c0 != int(ops.stream_checksum(r.flip(0)))
+    r2 = r.clone()
+    r2[[3, 4]] = r2[[4, 3]]
+    assert c0 != int(ops.stream_checksum(r2))
+    assert ops.default_canonical() is False
+    assert ops.EpochPrep("cpu").canonical is False
