@@ -22,7 +22,8 @@ extern "C" {
 #endif
 
 /* 17: the owner-sharded sparse exchange (dp_mode "owner"): ncf_owner_plan,
- * ncf_owner_plan_init, ncf_owner_lists, ncf_owner_pack, ncf_owner_adam, ncf_owner_unpack.
+ * ncf_owner_plan_init, ncf_owner_lists, ncf_owner_pack, ncf_owner_adam, ncf_owner_unpack;
+ * NCF_LAYOUT_FACT_IN_ADAM (the factored expansion inside ncf_reduce_adam_step).
  * 16: NCF_LAYOUT_USER_STORE (ncf_layout_tune; ncf_uses_user_order covers it),
  * ncf_debug_set_user_store; ncf_adam_step_fact: one launch, clears the local bucket
  * (grads_local, grads_n arguments), gshard may be written.
@@ -89,6 +90,14 @@ typedef struct ncf_layout {
 #define NCF_LAYOUT_FACT_DEFER_DX 0x8 /* factored layer 0: the step forms only the dW0 partials and leaves the
                                         per-entity sums G in grads' Um / Im rows (ncf_adam_step_fact expands them
                                         per shard after the reduce-scatter); set by the caller, kept by tune */
+#define NCF_LAYOUT_FACT_IN_ADAM 0x20 /* factored layer 0 on the fused path, dm in {16, 32, 64}, single process
+                                       (since ABI 17): ncf_train_step leaves the per-entity sums G in grads' Um / Im
+                                       rows and ncf_reduce_adam_step forms dUm, dIm and dW0 itself and applies Adam
+                                       in the same launch (one launch fewer per step).  Set by the caller, kept by
+                                       tune; the train workspace must be zero-filled once before the first step (the
+                                       launch's counters live there and are left zero).  ncf_reduce_slab,
+                                       ncf_lazy_adam_step, ncf_touched_pack, ncf_owner_pack, ncf_adam_step_fact and
+                                       ncf_kd_feature_step refuse such a layout (NCF_E_ARG). */
 #define NCF_LAYOUT_USER_STORE 0x10  /* fused step (set by ncf_layout_tune when ncf_debug_set_user_store
                                        enables it; since ABI 16): the user-side embedding gradients of each
                                        row are stored plainly into the workspace and summed per user by a

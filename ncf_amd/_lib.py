@@ -38,6 +38,7 @@ PREP_CANONICAL = 0x1  # ncf_prepare_epoch2 flags: canonical row order inside ite
 PROBE_BLOCKS = 2048  # include/ncf_hip.h NCF_PROBE_BLOCKS (ncf_probe_gather_scatter's sink: x 256 floats)
 LAYOUT_FACT_DEFER_DX = 0x8  # ncf_layout.flags: factored step leaves G for ncf_adam_step_fact (sharded zero1)
 LAYOUT_USER_STORE = 0x10  # ncf_layout.flags (ncf_layout_tune): user-side gradients stored, summed per user
+LAYOUT_FACT_IN_ADAM = 0x20  # ncf_layout.flags: factored expansion inside ncf_reduce_adam_step (single process)
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
 
 c_i64 = ctypes.c_int64

@@ -292,6 +292,7 @@ class TrainEngine:
             if os.environ.get("NCF_FORCE_LAYERED", "0") == "1":  # A/B: the layered path for any shape
                 self.lay.flags |= L.LAYOUT_LAYERED
             self._set_fact_shard()
+            self._set_fact_in_adam()
             self.ws = ops.new_workspace(self.lay, per, self.device)
         self.batch_size = int(batch_size)
         if self.num_batches > self.loss_hist.numel():
@@ -520,6 +521,23 @@ class TrainEngine:
         if self.group is None or dist.get_world_size(self.group) != self.world_size:
             return  # an emulated world on a smaller group (scripts/dp_modes.py): timing only
         D.owner_gather_rows(self.flat, self._owner_tables(), self.world_size, self.rank, self.group)
+
+    def _set_fact_in_adam(self):
+        """Single-process Adam on the factored fused path (dm 16..64, e.g. C3): the
+        expansion of the per-entity sums (dUm, dIm, dW0) runs inside the optimizer
+        launch (NCF_LAYOUT_FACT_IN_ADAM) -- one launch fewer per step.
+        NCF_FACT_IN_ADAM=0 keeps the separate expansion launch (A/B)."""
+        lay, m = self.lay, self.model
+        dm = m.factor_num << (m.num_layers - 1)
+        on = bool(self._fused_optimizer and self.distill is None and os.environ.get("NCF_LAZY_ADAM", "0") == "0"
+                  and os.environ.get("NCF_FACT_IN_ADAM", "1") == "1"
+                  and not (lay.flags & L.LAYOUT_LAYERED) and lay.dropout == 0.0
+                  and L.supported(m.model_type, m.factor_num, m.num_layers) == L.PATH_FUSED
+                  and dm in (16, 32, 64) and L.hip().ncf_fact_mode(ctypes.byref(lay)) == 1)
+        if on:
+            lay.flags |= L.LAYOUT_FACT_IN_ADAM
+        else:
+            lay.flags &= ~L.LAYOUT_FACT_IN_ADAM
 
     def _order_buf(self, rows):
         """The user-order buffer that goes with epoch-stream buffer `rows`."""
