@@ -220,6 +220,8 @@ class TrainEngine:
         self._ow_lists = {}
         self._ow_bufs = None
         self._ow_max = None
+        self._ow_pre = {}  # owner_prebuild results per stream buffer
+        self._ow_old = []  # replaced list buffers (a side-stream prebuild may still write them)
         if dp_mode == "touched":  # packed gradients of the touched rows + tower, all-reduced
             self._packed = torch.zeros(int(L.hip().ncf_touched_packed_floats(ctypes.byref(self.lay), self._ranges,
                                                                              self._nranges, 1)),
@@ -422,18 +424,43 @@ class TrainEngine:
     # exchange chunks keep one size (and the captured graphs stay valid) across epochs
     OWNER_SLACK = 1.08
 
-    def _owner_plan_for(self, mu, mi):
+    def _owner_plan_for(self, mu, mi, n=None, batch=None):
         P = L.NcfOwnerPlan()
-        L.check(L.hip().ncf_owner_plan_init(ctypes.byref(self.lay), self._ranges, self._nranges, self.n_total,
-                                            self.batch_size, self.world_size, self.rank, int(mu), int(mi),
-                                            ctypes.byref(P)), "ncf_owner_plan_init")
+        L.check(L.hip().ncf_owner_plan_init(ctypes.byref(self.lay), self._ranges, self._nranges,
+                                            self.n_total if n is None else int(n),
+                                            self.batch_size if batch is None else int(batch), self.world_size,
+                                            self.rank, int(mu), int(mi), ctypes.byref(P)), "ncf_owner_plan_init")
         return P
+
+    def owner_prebuild(self, rows, stream):
+        """EpochPipeline.on_built (dp_mode "owner"): the epoch's bucket lists built on
+        the pipeline's side stream right after the stream itself, with the current list
+        slots, and their maxima copied to pinned memory -- so at the epoch boundary
+        set_epoch_stream only reads two numbers of a build that finished long before
+        (the host does not wait for the running epoch).  Lists longer than the slots are
+        rebuilt there, synchronously."""
+        if self.dp_mode != "owner" or self.batch_size is None or self._ow_plan is None:
+            return
+        mu, mi = self._ow_M
+        plan = self._owner_plan_for(mu, mi, n=rows.numel())
+        key = (rows.data_ptr(), rows.numel(), self.batch_size)
+        lists = self._owner_lists_buf(rows, plan)
+        dmax = torch.zeros(2, dtype=torch.int32, device=self.device)
+        L.check(L.hip().ncf_owner_lists(ctypes.byref(plan), ctypes.byref(self.lay), rows.data_ptr(),
+                                        lists.data_ptr(), dmax.data_ptr(), stream.cuda_stream), "ncf_owner_lists")
+        host = torch.empty(2, dtype=torch.int32, pin_memory=True)
+        host.copy_(dmax, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self._ow_pre[key] = ((mu, mi), host, ev, dmax)
 
     def _owner_lists_buf(self, rows, plan):
         key = (rows.data_ptr(), rows.numel(), self.batch_size)
         ints = (int(plan.lists_bytes) + 3) // 4
         buf = self._ow_lists.get(key)
         if buf is None or buf.numel() < ints:
+            if buf is not None:  # a prebuild on the side stream may still write it: kept alive
+                self._ow_old.append(buf)
             buf = self._ow_lists[key] = torch.zeros(ints, dtype=torch.int32, device=self.device)
         return buf
 
@@ -447,6 +474,16 @@ class TrainEngine:
         if self._ow_max is None:
             self._ow_max = torch.zeros(2, dtype=torch.int32, device=self.device)
         mu, mi = self._ow_M
+        key = (rows.data_ptr(), rows.numel(), self.batch_size)
+        pre = self._ow_pre.pop(key, None)
+        if (pre is not None and pre[0] == (mu, mi) and self._ow_plan is not None
+                and int(self._ow_plan.n_total) == rows.numel() and int(self._ow_plan.batch_global) == self.batch_size):
+            _, host, ev, _ = pre
+            ev.synchronize()  # the side-stream build (a prefetched epoch: finished long before)
+            need_u, need_i = (int(x) for x in host.tolist())
+            if need_u <= mu and need_i <= mi:
+                torch.cuda.current_stream(self.device).wait_event(ev)
+                return
         while True:
             plan = self._owner_plan_for(mu, mi)
             lists = self._owner_lists_buf(rows, plan)

@@ -163,6 +163,9 @@ class EpochPipeline:
         self.stats = {"epochs": 0, "prefetch_hits": 0}
         self._wordgen = WordsGen()
         self.events = None  # (start, rows+perm built, grouped) of the last epoch
+        # on_built(rows_out, stream): called after each epoch's build, on the build's
+        # stream (the worker thread for a prefetched epoch), e.g. TrainEngine.owner_prebuild
+        self.on_built = None
 
     # ---------------------------------------------------------------- host part
     def _take_slot(self):
@@ -231,6 +234,10 @@ class EpochPipeline:
             self.prep(self.rows, self.perm, self.batch_size, self.item_num, out=self._out[slot])
         staged.ready = torch.cuda.Event(enable_timing=True)
         staged.ready.record(stream)
+        hook = self.on_built
+        if hook is not None:  # per-stream work of the consumer, on the same stream (e.g. owner lists)
+            with torch.cuda.stream(stream):
+                hook(self._out[slot], stream)
 
     def _launch(self, seed, prev, key=None, pos=None):
         """Stage the epoch after `prev` (or from (key, pos)) on a worker thread."""

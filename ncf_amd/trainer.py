@@ -76,6 +76,7 @@ class Trainer:
                 self._pipe = EpochPipeline(self.ds, self.device, self.batch_size, int(self.model.item_num),
                                            user_num=int(self.model.user_num), canonical=self.world_size > 1)
                 self.engine.stream_buffers = self._pipe.buffers  # step graphs captured for both
+                self._pipe.on_built = self.engine.owner_prebuild  # dp_mode "owner": lists built with each epoch
             # fit() evaluates after every epoch (one torch draw): the next epoch's
             # sampler seed is peeked past it
             return self._pipe.next_epoch(peek_eval_draw=True)
