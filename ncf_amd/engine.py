@@ -105,19 +105,41 @@ class TrainEngine:
             return "auto"
         return "allreduce" if total_floats <= cls.ALLREDUCE_MAX_FLOATS else "zero1"
 
+    # dp_mode "auto" picks the owner-sharded exchange from this many ranks up even where
+    # a global batch touches every row (C3): two all-to-alls of the touched rows over the
+    # point-to-point xGMI links against a ring all-reduce of the whole flat gradient
+    # (the projection of DESIGN.md section 6, from per-rank costs measured at emulated
+    # N = 2 / 4 / 8); at 2 ranks the all-reduce's one collective wins there
+    OWNER_MIN_WORLD = 4
+
     @classmethod
-    def auto_dp_mode(cls, lay, ranges, nranges, batch_size):
-        """("touched" | "allreduce" | "zero1", packed floats) for dp_mode "auto" at this
-        global batch: touched where the packed buffer is small enough, else the
-        size rule of default_dp_mode without deferred Adam (all-reduce up to
+    def auto_dp_mode(cls, lay, ranges, nranges, batch_size, world=2, owner_ok=False):
+        """("owner" | "touched" | "allreduce" | "zero1", packed floats) for dp_mode "auto"
+        at this global batch and world: owner (where it applies) when the batch touches
+        a small part of the tables (packed buffer <= TOUCHED_MAX_FRACTION of the flat
+        gradient, C4) or from OWNER_MIN_WORLD ranks up; else touched where the packed
+        buffer is small enough; else the size rule of default_dp_mode (all-reduce up to
         ALLREDUCE_MAX_FLOATS, zero1 above: the optimizer state stays sharded)."""
         pf = int(L.hip().ncf_touched_packed_floats(ctypes.byref(lay), ranges, nranges, int(batch_size)))
-        if 0 < pf <= cls.TOUCHED_MAX_FRACTION * int(lay.total):
+        sparse = 0 < pf <= cls.TOUCHED_MAX_FRACTION * int(lay.total)
+        if owner_ok and (sparse or int(world) >= cls.OWNER_MIN_WORLD):
+            return "owner", pf
+        if sparse:
             return "touched", pf
         return cls.default_dp_mode(int(lay.total), touched_ok=False), pf
 
+    def _owner_ok(self):
+        """dp_mode "owner" applies: Adam, no distillation, at most 16 ranks, rows of at
+        most 1,024 floats (ncf_owner_plan_init) -- touched_ok's other limits."""
+        if self.optimizer != "adam" or self.distill is not None or self.world_size > 16:
+            return False
+        P = L.NcfOwnerPlan()
+        return L.hip().ncf_owner_plan_init(ctypes.byref(self.lay), self._ranges, self._nranges, 1, 1,
+                                           self.world_size, self.rank, 0, 0, ctypes.byref(P)) == L.NCF_OK
+
     def _resolve_auto(self, batch_size):
-        self.dp_mode, pf = self.auto_dp_mode(self.lay, self._ranges, self._nranges, batch_size)
+        self.dp_mode, pf = self.auto_dp_mode(self.lay, self._ranges, self._nranges, batch_size, self.world_size,
+                                             self._owner_ok())
         if self.dp_mode == "touched":
             self._packed = torch.zeros(pf, dtype=torch.float32, device=self.device)
         elif self.dp_mode == "zero1":

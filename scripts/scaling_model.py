@@ -61,6 +61,13 @@ def main():
     ap.add_argument("--packed", type=json.loads, default={"c3": 790737, "c4": 7400000},
                     help="touched-mode packed floats per step (DESIGN §6 table)")
     ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--local", choices=("events", "graph"), default="events",
+                    help="local part: the event-timed launch groups without the collectives (events), or the "
+                         "graph-replayed step minus the one-rank collectives' kernel time (graph; per-part event "
+                         "pairs add several us each)")
+    ap.add_argument("--coll-us", type=json.loads, default={},
+                    help='graph mode: {"config/mode": us} of one one-rank collective kernel (rocprofv3 trace of '
+                         'the dp_modes run)')
     a = ap.parse_args()
     rows = []
     for path in a.inputs:
@@ -74,6 +81,9 @@ def main():
             local = sum(1e3 * v for k, v in m["launch_groups_ms"].items()
                         if k not in ("allreduce", "reduce_scatter", "all_gather", "all_to_all_grads",
                                      "all_to_all_params"))
+            if a.local == "graph":
+                ncoll = {"allreduce": 1, "touched": 1, "zero1": 2, "owner": 2}[mode]
+                local = 1e3 * m["ms_per_step_graph"] - ncoll * float(a.coll_us.get(f"{cfg}/{mode}", 0.0))
             for bw in (a.link_bw if mode == "owner" else a.bw):
                 for alpha in a.alpha:
                     x = exchange_us(mode, n, a.floats[cfg], a.packed[cfg], bw, alpha, m.get("owner"))

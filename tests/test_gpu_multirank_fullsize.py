@@ -133,7 +133,7 @@ def _c4l_run(world, rank, group):
 
 
 # what dp_mode "auto" resolves to (TrainEngine.auto_dp_mode)
-AUTO_EXPECT = {("c3", 2): "allreduce", ("c3", 4): "allreduce", ("c3", 8): "allreduce", ("c4", 2): "touched"}
+AUTO_EXPECT = {("c3", 2): "allreduce", ("c3", 4): "owner", ("c3", 8): "owner", ("c4", 2): "owner"}
 
 RUNS = {"c3": _c3_run, "c4": _c4_run, "c4l": _c4l_run, "c3w": _c3w_run}
 

@@ -288,6 +288,12 @@ def test_auto_dp_mode_by_global_batch():
         ranges = (ctypes.c_int64 * (2 * len(rng)))(*[x for r in rng for x in r])
         got, pf = TrainEngine.auto_dp_mode(lay, ranges, len(rng), 65536)
         assert got == mode, (U, I, pf, int(lay.total))
+        # with the owner exchange available: owner for the sparse batch at any world and
+        # for every shape from OWNER_MIN_WORLD ranks up
+        for world in (2, 4, 8):
+            got, _ = TrainEngine.auto_dp_mode(lay, ranges, len(rng), 65536, world, owner_ok=True)
+            exp = "owner" if (mode == "touched" or world >= TrainEngine.OWNER_MIN_WORLD) else mode
+            assert got == exp, (U, I, world, got)
 
 
 @pytest.mark.parametrize("bs,k", [(100, 10), (100, 1), (100, 5), (25, 10)])
