@@ -1,6 +1,6 @@
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -u -m pytest tests/test_gpu_fact_adam.py tests/test_gpu_owner.py tests/test_gpu_multirank.py tests/test_gpu_distill.py -k "fact or owner or different or c5_id" -q --maxfail=3 --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r5c_tests.log 2>&1 || { tail -40 gpurun_out/r5c_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fact_adam.py tests/test_gpu_owner.py tests/test_gpu_multirank.py tests/test_gpu_distill.py -k "fact or owner or different or c5_id" -q --maxfail=5 --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r5c_tests.log 2>&1 || { tail -40 gpurun_out/r5c_tests.log; exit 1; }
 tail -2 gpurun_out/r5c_tests.log
 timeout -k 10 300 python bench.py --steps 200 --warmup 20 --skip-cpu-baseline --skip-eval --e2e-epochs 0 > gpurun_out/r5c_bench_c3.log 2>&1 || { tail -20 gpurun_out/r5c_bench_c3.log; exit 1; }
 python3 -c "import json; d=[json.loads(l) for l in open('gpurun_out/r5c_bench_c3.log') if l.startswith('{')][-1]; print('C3', round(d['value']/1e6,1), 'M/s', round(d['ms_per_step']*1000,2), 'us/step', {k: (round(v*1e3,2) if isinstance(v,float) else v) for k,v in d['kernel_ms'].items() if not isinstance(v, dict)})"
