@@ -405,9 +405,6 @@ class TrainEngine:
         import torch.distributed as dist
         if dist.get_world_size(self.group) != self.world_size:
             return  # an emulated world (scripts/dp_modes.py)
-        pend = getattr(self, "_stream_checks", None)
-        if pend is None:
-            pend = self._stream_checks = []
         self._poll_stream_checks(block=False)
         c = ops.stream_checksum(rows)
         t = torch.stack([c, -c])
@@ -422,7 +419,7 @@ class TrainEngine:
         flag.copy_(bad.view(1), non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        pend.append((flag, ev))
+        self._stream_checks = getattr(self, "_stream_checks", []) + [(flag, ev)]
         if not getattr(self, "_stream_checked_once", False):
             self._stream_checked_once = True
             self._poll_stream_checks(block=True)

@@ -104,7 +104,7 @@ def test_device_plan_at_c5_id_space_vs_cpu_modules(strategy):
     rng = np.random.default_rng(11)
     u = rng.integers(0, 6041, T * B)
     i = rng.integers(0, 3707, T * B)
-    y = (rng.random(T * B) < 0.2).astype(np.int64)
+    y = (rng.random(T * B) < 0.2).astype(np.float32)  # the reference loader's float labels
     # CPU reference run
     teacher, student, d = _build_ml1m(strategy)
     opt = torch.optim.Adam(student.parameters(), lr=1e-3)
