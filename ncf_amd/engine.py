@@ -579,14 +579,16 @@ class TrainEngine:
         D.owner_gather_rows(self.flat, self._owner_tables(), self.world_size, self.rank, self.group)
 
     def _set_fact_in_adam(self):
-        """Single-process Adam on the factored fused path (dm 16..64, e.g. C3): the
-        expansion of the per-entity sums (dUm, dIm, dW0) runs inside the optimizer
-        launch (NCF_LAYOUT_FACT_IN_ADAM) -- one launch fewer per step.
-        NCF_FACT_IN_ADAM=0 keeps the separate expansion launch (A/B)."""
+        """Single-process Adam on the factored fused path (dm 16..64, e.g. C3): with
+        NCF_FACT_IN_ADAM=1 the expansion of the per-entity sums (dUm, dIm, dW0) runs
+        inside the optimizer launch (NCF_LAYOUT_FACT_IN_ADAM) -- one launch fewer per
+        step, but its in-launch hand-off of the dW0 partials measured slower than the
+        launch boundary it replaces (C3 optimizer 36 us against 7.4 + 9.3 us for
+        fact_expand + reduce_adam): off by default (A/B)."""
         lay, m = self.lay, self.model
         dm = m.factor_num << (m.num_layers - 1)
         on = bool(self._fused_optimizer and self.distill is None and os.environ.get("NCF_LAZY_ADAM", "0") == "0"
-                  and os.environ.get("NCF_FACT_IN_ADAM", "1") == "1"
+                  and os.environ.get("NCF_FACT_IN_ADAM", "0") == "1"
                   and not (lay.flags & L.LAYOUT_LAYERED) and lay.dropout == 0.0
                   and L.supported(m.model_type, m.factor_num, m.num_layers) == L.PATH_FUSED
                   and dm in (16, 32, 64) and L.hip().ncf_fact_mode(ctypes.byref(lay)) == 1)
