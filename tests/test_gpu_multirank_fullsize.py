@@ -259,8 +259,31 @@ def test_full_shape_ranks_match_single_rank_and_oracle(name, world, dp_mode):
     # parameters after the free-running steps: two fp32 trajectories (shard sums vs
     # whole-batch sums) -- the criterion of the single-rank trajectory tests
     from test_gpu_parity import _assert_trajectory_close
-    # 100 steps at C4: the reference's own loop perturbed by one ulp per step leaves 9%
-    # of the elements outside the criterion (0.27% at 50 steps, 0.01% at 20; max dev
-    # 0.011) -- twice that is allowed
-    _assert_trajectory_close(flat0, flat1, nb, 1e-3, f"{name} world {world}: params vs 1 rank",
-                             off_max=0.2 if nb >= 100 else 0.10)
+    if nb < 100:
+        _assert_trajectory_close(flat0, flat1, nb, 1e-3, f"{name} world {world}: params vs 1 rank")
+        return
+    # 100 free-running steps at C4: the element-wise criterion stops meaning much -- the
+    # reference's own loop perturbed by one ulp per step leaves 9% of the elements
+    # outside it (0.27% at 50 steps, 0.01% at 20; test_oracle.py), two GPU runs 11-30%
+    # (Adam turns near-zero gradients of rarely touched rows into +-lr moves).  Checked
+    # instead: every element within 4 T lr, and the two parameter sets give the same
+    # loss on a held-out batch (the oracle model, CPU) to 1e-5 relative
+    dev = np.abs(flat0.astype(np.float64) - flat1.astype(np.float64))
+    assert dev.max() <= 4 * nb * 1e-3, dev.max()
+    ds, _, _ = _data("ml-20m")
+    rng = np.random.default_rng(123)
+    hu = rng.integers(0, ds["user_num"], B)
+    hi = rng.integers(0, ds["item_num"], B)
+    hy = (rng.random(B) < 0.2).astype(np.int64)
+    held = []
+    for flat in (flat0, flat1):
+        m = O.OracleNCF(ds["user_num"], ds["item_num"], 16, 3, 0.0, "NeuMF-end")
+        off = 0
+        with torch.no_grad():
+            for p in m.parameters():
+                p.copy_(torch.from_numpy(flat[off:off + p.numel()].reshape(p.shape)))
+                off += p.numel()
+            held.append(float(O.bce_mean(m(torch.from_numpy(hu), torch.from_numpy(hi)), torch.from_numpy(hy))))
+    print(f"{name} world {world}: held-out loss {held[0]:.8f} vs 1 rank {held[1]:.8f}; "
+          f"{(dev > 1e-4 * np.abs(flat1) + 1e-6 * np.abs(flat1).max()).mean():.3f} of elements off element-wise")
+    assert abs(held[0] - held[1]) <= 1e-5 * abs(held[1]), held
