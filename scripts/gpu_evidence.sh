@@ -64,6 +64,9 @@ if has profile; then
         mkdir -p "gpurun_out/prof_$cfg"
         cp gpurun_out/prof_summary.md gpurun_out/prof_summary.json gpurun_out/prof/run_kernel_stats.csv \
             "gpurun_out/prof_$cfg/"
+        # the box's copy of the tree: later stages of this call (bench, configs) read the
+        # newest committed summary of their config for the roofline's traffic field
+        cp gpurun_out/prof_summary.json "profiles/${PROF_TAG:-r05}_${cfg}_prof_summary.json"
     done
 fi
 if has multirank; then
