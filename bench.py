@@ -744,6 +744,33 @@ def newest_profile(config, kernel_names):
     return None, None
 
 
+LAYERED_STEP_PREFIXES = ("ncf::lyr_", "ncf::fact_expand_kernel")
+
+
+def layered_profile(config):
+    """(HBM bytes per step, MFMA-busy fraction, source) of the layered path's step from
+    the newest committed rocprofv3 summary of this config: every kernel of
+    ncf_train_step (LAYERED_STEP_PREFIXES), each weighted by its launches per step
+    (calls / the calls of lyr_proj_kernel, the step's first launch); the busy fraction
+    time-weighted over those kernels.  (None, None, None) if there is none."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_prof_summary.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("config") != config:
+            continue
+        ks = [k for k in d.get("kernels", []) if str(k.get("kernel", "")).startswith(LAYERED_STEP_PREFIXES)]
+        steps = max((k.get("calls") or 0 for k in ks if k["kernel"].startswith("ncf::lyr_proj_kernel")), default=0)
+        if not steps or not all(k.get("hbm_bytes_corrected") for k in ks):
+            continue
+        traffic = sum(k["hbm_bytes_corrected"] * k["calls"] / steps for k in ks)
+        t = [(k["avg_us"] * k["calls"] / steps, k.get("mfma_busy_frac")) for k in ks]
+        busy = (sum(a * b for a, b in t) / sum(a for a, _ in t)) if all(b is not None for _, b in t) else None
+        return float(traffic), busy, os.path.relpath(path, ROOT)
+    return None, None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -851,7 +878,9 @@ def main():
         traffic, traffic_src = pmc_traffic(args.config, names) if world == 1 else (None, None)
         busy, busy_src = newest_profile(args.config, names) if world == 1 else (None, None)
     else:
-        names, traffic, traffic_src, busy, busy_src = [], None, None, None, None
+        names = []
+        traffic, busy, traffic_src = layered_profile(args.config) if world == 1 else (None, None, None)
+        busy_src = traffic_src
         kname = ("layered path: all kernels of ncf_train_step (fwd/predict/bwd GEMMs); the fp32 GEMMs with "
                  "16-byte loads run as exact three-plane bf16 splits on v_mfma_f32_16x16x32_bf16 (six bf16 "
                  "products per fp32 product; peak kept at the fp32 MFMA figure)")
