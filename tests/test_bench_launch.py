@@ -57,3 +57,22 @@ def test_failed_rank_stops_the_others():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu-harness",
                         "--config", "c3"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+def test_roofline_traffic_sources_in_committed_profiles():
+    """Every bench config's roofline finds its counter traffic in a committed
+    rocprofv3 summary: the fused path by its launch group's kernel names, the layered
+    path (CLI, stress) by every kernel of its step weighted per step."""
+    sys.path.insert(0, ROOT)
+    import bench
+    t, busy, src = bench.layered_profile("stress")
+    assert src is not None and t > 1e9 and 0 < busy < 1, (t, busy, src)
+    # weights per step: the step's three forward GEMM launches count three times
+    d = json.load(open(os.path.join(ROOT, src)))
+    ks = {k["kernel"]: k for k in d["kernels"]}
+    fwd = ks["ncf::lyr_fwd_kernel<false, false, true>"]
+    assert fwd["calls"] == 3 * ks["ncf::lyr_proj_kernel"]["calls"]
+    assert bench.layered_profile("cli")[0] is not None
+    tr, src3 = bench.pmc_traffic("c3", ["ncf::ncf_step_kernel<16, 3, 2, false, true, 8>",
+                                        "ncf::fact_expand_kernel<64>"])
+    assert tr is not None and tr > 1e6, src3
