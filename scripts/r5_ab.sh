@@ -11,7 +11,7 @@ for cfg in ${AB_CONFIGS:-c2 c5 c3}; do
             timeout -k 10 300 env "$AB_VAR=$v" python bench.py --config "$cfg" --steps "${AB_STEPS:-400}" --warmup 20 \
                 --skip-cpu-baseline --skip-eval --e2e-epochs 0 > "gpurun_out/ab/${cfg}_${v}_$r.log" 2>&1 || {
                 tail -20 "gpurun_out/ab/${cfg}_${v}_$r.log"; exit 1; }
-            python3 -c "import json; d=[json.loads(l) for l in open('gpurun_out/ab/${cfg}_${v}_$r.log') if l.startswith('{')][-1]; print('$cfg $AB_VAR=$v', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step']*1000,2), 'us/step')"
+            python3 -c "import json; d=[json.loads(l) for l in open('gpurun_out/ab/${cfg}_${v}_$r.log') if l.startswith('{')][-1]; print('$cfg $AB_VAR=$v', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step']*1000,2), 'us/step', 'sustained', round((d.get('sustained') or {}).get('value', 0)/1e6,2), round((d.get('sustained') or {}).get('ms_per_step', 0)*1000,2))"
         done
     done
 done
