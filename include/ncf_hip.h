@@ -21,7 +21,9 @@
 extern "C" {
 #endif
 
-/* 17: the owner-sharded sparse exchange (dp_mode "owner"): ncf_owner_plan,
+/* 18: in-step Adam for small batches: ncf_ais_bufs, ncf_ais_supported, ncf_ais_begin,
+ * ncf_train_step_ais, ncf_ais_bump, ncf_ais_flush.
+ * 17: the owner-sharded sparse exchange (dp_mode "owner"): ncf_owner_plan,
  * ncf_owner_plan_init, ncf_owner_lists, ncf_owner_pack, ncf_owner_adam, ncf_owner_unpack;
  * NCF_LAYOUT_FACT_IN_ADAM (the factored expansion inside ncf_reduce_adam_step).
  * 16: NCF_LAYOUT_USER_STORE (ncf_layout_tune; ncf_uses_user_order covers it),
@@ -30,7 +32,7 @@ extern "C" {
  * 15: ncf_layout.flags gains the fused step's workgroup geometry (NCF_LAYOUT_GEO_*) and
  * NCF_LAYOUT_FACT_DEFER_DX; new ncf_adam_step_fact, ncf_prepare_epoch2
  * (NCF_PREP_CANONICAL), ncf_probe_gather_scatter, ncf_debug_set_geometry. */
-#define NCF_ABI_VERSION 17
+#define NCF_ABI_VERSION 18
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -201,6 +203,38 @@ int ncf_train_step_kd(const ncf_layout *lay, const float *params, float *grads, 
                       int rank, float w_task, float w_resp, float temperature, void *workspace,
                       int64_t workspace_bytes,
                       float *logits_out, void *stream);
+
+/* ---- In-step Adam for small batches (ABI 18) ----------------------------------
+ * The previous step's dense Adam (torch.optim.Adam, train_neumf.py:90,115) runs inside
+ * the next training launch: the launch's training workgroups apply it on the fly to
+ * every tower float and embedding row they read, its extra workgroups write it for
+ * every active float, so a small-batch step is ONE launch (fused path, per-row layer 0,
+ * the 4-wave geometry; single process).  Two state buffers (params / exp_avg /
+ * exp_avg_sq: the caller's and `*_b`) and three gradient buffers (the caller's grads,
+ * grads_1, grads_2) rotate: state S_n (after update n) lives in buffer (n + par) & 1,
+ * update n's gradient (tower partials and loss slot included) in buffer n % 3.
+ * Sequence: ncf_ais_begin; per chunk of k launches ncf_train_step_ais with step_i =
+ * 0 .. k-1 (capturable), then ncf_ais_bump(k); ncf_ais_flush writes the last update
+ * into the caller's buffers and advances ctl->adam_t -- the parameters, moments and
+ * ctl are then exactly the two-launch form's.  All buffers hold ncf_layout.total
+ * floats; `state` is 4 device int64. */
+typedef struct ncf_ais_bufs {
+    float *params_b, *exp_avg_b, *exp_avg_sq_b;
+    float *grads_1, *grads_2;
+    int64_t *state;
+} ncf_ais_bufs;
+int ncf_ais_supported(const ncf_layout *lay);
+int ncf_ais_begin(const ncf_layout *lay, float *params, float *grads, float *exp_avg, float *exp_avg_sq,
+                  const ncf_ais_bufs *b, const int64_t *ranges, int nranges, ncf_step_ctl *ctl, void *stream);
+int ncf_train_step_ais(const ncf_layout *lay, float *params, float *grads, float *exp_avg, float *exp_avg_sq,
+                       const ncf_ais_bufs *b, const int64_t *ranges, int nranges, const uint64_t *rows,
+                       const float *dlogit, ncf_step_ctl *ctl, int64_t batch_global, int dz_mode, float kd_wt,
+                       float kd_wr, float kd_temp, double lr, double beta1, double beta2, double eps,
+                       float *loss_hist, int64_t hist_len, int64_t step_i, void *stream);
+int ncf_ais_bump(ncf_step_ctl *ctl, const ncf_ais_bufs *b, int64_t k, void *stream);
+int ncf_ais_flush(const ncf_layout *lay, float *params, float *grads, float *exp_avg, float *exp_avg_sq,
+                  const ncf_ais_bufs *b, const int64_t *ranges, int nranges, ncf_step_ctl *ctl, double lr,
+                  double beta1, double beta2, double eps, float *loss_hist, int64_t hist_len, void *stream);
 
 /*
  * Feature distillation terms (src/distillation/feature.py:51-123) of the same batch

@@ -29,7 +29,7 @@ NCF_E_ARG = -2
 NCF_E_LAUNCH = -3
 MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
 DZ_BCE, DZ_DLOGIT, DZ_KD = 0, 1, 2
-ABI_VERSION = 17  # include/ncf_hip.h NCF_ABI_VERSION
+ABI_VERSION = 18  # include/ncf_hip.h NCF_ABI_VERSION
 PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 LAYOUT_PER_ROW_L0, LAYOUT_WG_SHIFT, LAYOUT_WG_MASK = 0x1, 8, 0xFFF  # ncf_layout.flags (ncf_layout_tune)
 LAYOUT_LAYERED = 0x2  # ncf_layout.flags: training on the layered path even where a fused kernel exists
@@ -73,7 +73,14 @@ class NcfOwnerPlan(ctypes.Structure):
                 ("send_floats", c_i64), ("param_floats", c_i64), ("tail_offset", c_i64), ("off", c_i64 * 4)]
 
 
+class NcfAisBufs(ctypes.Structure):
+    """include/ncf_hip.h ncf_ais_bufs (in-step Adam, ABI 18)."""
+    _fields_ = [("params_b", c_vp), ("exp_avg_b", c_vp), ("exp_avg_sq_b", c_vp), ("grads_1", c_vp),
+                ("grads_2", c_vp), ("state", c_vp)]
+
+
 _OWNER = ctypes.POINTER(NcfOwnerPlan)
+_AIS = ctypes.POINTER(NcfAisBufs)
 _LAY = ctypes.POINTER(NcfLayout)
 _HIP_PROTOS = {
     "ncf_abi_version": (ctypes.c_int, []),
@@ -157,6 +164,17 @@ _HIP_PROTOS = {
                                       ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_vp, c_i64,
                                       c_vp, c_vp, c_vp]),
     "ncf_owner_unpack": (ctypes.c_int, [_OWNER, _LAY, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "ncf_ais_supported": (ctypes.c_int, [_LAY]),
+    "ncf_ais_begin": (ctypes.c_int, [_LAY, c_vp, c_vp, c_vp, c_vp, _AIS, ctypes.POINTER(c_i64), ctypes.c_int, c_vp,
+                                     c_vp]),
+    "ncf_train_step_ais": (ctypes.c_int, [_LAY, c_vp, c_vp, c_vp, c_vp, _AIS, ctypes.POINTER(c_i64), ctypes.c_int,
+                                          c_vp, c_vp, c_vp, c_i64, ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                          ctypes.c_float, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                          ctypes.c_double, c_vp, c_i64, c_i64, c_vp]),
+    "ncf_ais_bump": (ctypes.c_int, [c_vp, _AIS, c_i64, c_vp]),
+    "ncf_ais_flush": (ctypes.c_int, [_LAY, c_vp, c_vp, c_vp, c_vp, _AIS, ctypes.POINTER(c_i64), ctypes.c_int, c_vp,
+                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_vp, c_i64,
+                                     c_vp]),
 }
 
 _SAMPLER_PROTOS = {

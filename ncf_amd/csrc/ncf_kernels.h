@@ -1,5 +1,6 @@
 // Internal (C++) declarations shared by the kernel translation units and the C ABI.
 #pragma once
+#include "ncf_adam.h"
 #include "ncf_common.h"
 
 namespace ncf {
@@ -91,6 +92,29 @@ struct Shape {
     static_assert(L >= 1 && L <= 4, "num_layers must be 1..4");
 };
 
+// NCF_LAYOUT_ADAM_IN_STEP (ncf_train_step_ais): the previous step's dense Adam runs
+// inside this launch -- its training workgroups apply it on the fly to every tower
+// float and embedding row they read, its extra workgroups write it for every float --
+// so a small-batch step is one launch.  State S_n (after update n) lives in buffer
+// (n + st[1]) & 1; update n's gradient in g[n % 3], its tower partials in slab[n & 1].
+struct AisArgs {
+    float* p[2];
+    float* m[2];
+    float* v[2];
+    float* g[3];
+    float* slab[2];
+    int64_t* st;  // device: [0] an update is pending at the chunk's first launch, [1] parity
+    Ranges R, RE;  // active float4 ranges; their embedding part (below the tower)
+    double lr, beta1, beta2;
+    float eps;
+    float* loss_hist;
+    int64_t hist_len;
+    ScCache* scc;
+    int64_t step_i;  // this launch's index in its chunk (ncf_ais_bump closes the chunk)
+    int ntrain;      // training workgroups; workgroups [ntrain, grid) run the dense update
+    int lo, stride, rows;  // tower slab: first column, row stride, rows (the ntrain workgroups)
+};
+
 struct TrainArgs {
     ncf_layout lay;
     const float* params;
@@ -111,6 +135,7 @@ struct TrainArgs {
     // atomics into grads; user_sum_kernel (ncf_ops.hip) sums them per user afterwards.
     float* ustore;
     int uw;
+    AisArgs ais;  // ncf_step_kernel<..., AIS = true> only
 };
 
 constexpr int NSTAMP = 64;  // stamps per workgroup
@@ -134,6 +159,7 @@ struct KernelEntry {
     const void* train[NGEO];       // per geometry; nullptr where it has no instantiation
     const void* fwd;               // GEO_8
     const void* train_fact[NGEO];  // factored layer 0 (MLP shapes; see ncf_train.hip), else nullptr
+    const void* train_ais[NGEO];   // the previous step's Adam inside the launch (per-row layer 0), else nullptr
     int w_total;                   // LDS floats
     int misc[NGEO], stage[NGEO];   // LDS floats per geometry
 };

@@ -7,6 +7,7 @@
 #include <mutex>
 #include <unordered_map>
 
+#include "ncf_adam.h"
 #include "ncf_kernels.h"
 #include "ncf_layered.h"
 
@@ -93,21 +94,6 @@ __global__ __launch_bounds__(256) void reduce_slab_kernel(const float* __restric
 
 // ---------------------------------------------------------------------------
 // Dense Adam (torch.optim.Adam, single-tensor path) + fused grad zeroing.
-struct Ranges {
-    int64_t begin[8];
-    int64_t prefix[9];  // prefix sums of float4 counts
-    int n;
-};
-
-__device__ __forceinline__ int64_t range_locate(const Ranges& R, int64_t q, int* which) {
-    int k = 0;
-#pragma unroll
-    for (int i = 1; i < 8; ++i)
-        if (i < R.n && q >= R.prefix[i]) k = i;
-    *which = k;
-    return R.begin[k] + (q - R.prefix[k]) * 4;
-}
-
 // Loss bookkeeping of the step: done by one thread, no cross-block protocol.
 __device__ __forceinline__ void record_loss(const ncf_step_ctl* ctl, const float* grads, int64_t loss_slot,
                                             float* loss_hist, int64_t hist_len) {
@@ -117,87 +103,7 @@ __device__ __forceinline__ void record_loss(const ncf_step_ctl* ctl, const float
     }
 }
 
-__device__ __forceinline__ void adam_f4(f4& p, f4& m, f4& v, const f4& g, float w1, float b2, float omb2,
-                                        float bc2s, float eps, float neg_step) {
-#pragma clang fp contract(off)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const float gr = lane_get(g, r);
-        float mr = lane_get(m, r), vr = lane_get(v, r), pr = lane_get(p, r);
-        mr = fmaf(w1, gr - mr, mr);          // exp_avg.lerp_(grad, 1 - beta1)   (fmadd form)
-        vr = vr * b2 + omb2 * gr * gr;       // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
-        const float den = sqrtf(vr) / bc2s + eps;  // (exp_avg_sq.sqrt() / bias_correction2_sqrt).add_(eps)
-        pr = pr + neg_step * mr / den;       // param.addcdiv_(exp_avg, denom, value=-step_size)
-        if (r == 0) { m.x = mr; v.x = vr; p.x = pr; }
-        else if (r == 1) { m.y = mr; v.y = vr; p.y = pr; }
-        else if (r == 2) { m.z = mr; v.z = vr; p.z = pr; }
-        else { m.w = mr; v.w = vr; p.w = pr; }
-    }
-}
-
-// Step-t scalars in double like torch's Python scalars, by thread 0 of the block:
-// sc[0] = -(lr / (1 - beta1^t)), sc[1] = sqrt(1 - beta2^t) (torch _single_tensor_adam).
-// The two double pows take ~2.5 us on one lane -- longer than the launch's loads --
-// so each optimizer launch also computes step t + 1's pair (one lane of block 0,
-// beside its other work) into a per-control-block cache entry, and step t + 1's
-// launch reads it instead: entry [t & 1] is only written by the launch of step t - 1
-// (a finished kernel), never by the launch that reads it.  The entry holds its
-// inputs (t, lr, beta1, beta2); any mismatch -- first step, a reloaded or
-// teacher-forced state, another optimizer on the same control block -- computes
-// the pair again, so the cached value is always the one pow gives.
-struct ScCache {
-    int64_t t;
-    double lr, beta1, beta2;
-    float sc0, sc1;
-    int64_t pad;
-};
-constexpr int SC_SLOTS = 1024;
 __device__ ScCache g_sc_cache[SC_SLOTS][2];
-
-__device__ __forceinline__ void step_pair(int64_t t_step, double lr, double beta1, double beta2, float* a, float* b) {
-    const double t = (double)t_step;
-    *a = (float)(-(lr / (1.0 - pow(beta1, t))));
-    *b = (float)sqrt(1.0 - pow(beta2, t));
-}
-
-// thread 0: the cache entry of step t, requested (issue early, resolve late)
-__device__ __forceinline__ ScCache sc_peek(const ScCache* cache, int64_t t_step) {
-    ScCache e;
-    e.t = -1;
-    if (threadIdx.x == 0 && cache != nullptr) e = cache[t_step & 1];
-    return e;
-}
-
-__device__ __forceinline__ void sc_resolve(const ScCache& e, int64_t t_step, double lr, double beta1, double beta2,
-                                           float* sc) {
-    if (threadIdx.x == 0) {
-        if (e.t == t_step && e.lr == lr && e.beta1 == beta1 && e.beta2 == beta2) {
-            sc[0] = e.sc0;
-            sc[1] = e.sc1;
-        } else {
-            step_pair(t_step, lr, beta1, beta2, &sc[0], &sc[1]);
-        }
-    }
-}
-
-__device__ __forceinline__ void step_scalars(const ScCache* cache, int64_t t_step, double lr, double beta1,
-                                             double beta2, float* sc) {
-    sc_resolve(sc_peek(cache, t_step), t_step, lr, beta1, beta2, sc);
-}
-
-// step t + 1's entry, by lane 0 of wave 1 of block 0 (vector stores)
-__device__ __forceinline__ void step_scalars_ahead(ScCache* cache, int64_t t_step, double lr, double beta1,
-                                                   double beta2) {
-    if (cache == nullptr || blockIdx.x != 0 || threadIdx.x != 64) return;
-    ScCache e;
-    e.t = t_step + 1;
-    e.lr = lr;
-    e.beta1 = beta1;
-    e.beta2 = beta2;
-    e.pad = 0;
-    step_pair(t_step + 1, lr, beta1, beta2, &e.sc0, &e.sc1);
-    cache[(t_step + 1) & 1] = e;
-}
 
 // The step-scalar cache entry pair of a control block (see ScCache): one slot per
 // (device, ctl pointer) seen, for the life of the process; null (always recompute)
@@ -308,12 +214,6 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* 
 // reduce_slab_kernel) and apply Adam to the active ones in place; blocks
 // [nA, grid) run the plain Adam over the embedding ranges RE.  t and the batch
 // come from the snapshot the train step wrote; block 0 commits them.
-__device__ __forceinline__ bool in_ranges(const Ranges& R, int64_t i) {
-    for (int k = 0; k < R.n; ++k)
-        if (i >= R.begin[k] && i < R.begin[k] + (R.prefix[k + 1] - R.prefix[k]) * 4) return true;
-    return false;
-}
-
 // Block of the tower part (blockIdx.x < nA): reduce 64 slab columns (W0's from the
 // expansion's partials), apply Adam to the active ones in place; the loss column
 // goes to the history.  sc[0..1] = (-step size, sqrt(bias correction 2)) of step t,
@@ -2296,6 +2196,239 @@ int ncf_train_step_kd(const ncf_layout* lay, const float* params, float* grads, 
     if (!teacher_logits) return NCF_E_ARG;
     return train_step_impl(lay, params, grads, rows, user_order, teacher_logits, ctl, batch_global, world, rank, NCF_DZ_KD,
                            w_task, w_resp, temperature, workspace, workspace_bytes, logits_out, stream);
+}
+
+// ---- the previous step's Adam inside the training launch (ABI 18, NCF_LAYOUT_ADAM_IN_STEP)
+}  // extern "C"
+
+namespace ncf {
+
+// The fused kernel with the in-step optimizer for this layout and its geometry, or null.
+static const void* ais_kernel(const ncf_layout* lay, int* geo) {
+    const KernelEntry* e = train_fused(lay);
+    if (!e || fact_mode(lay) || us_on(lay) || fa_applies(lay)) return nullptr;
+    const int g = train_geo(e, lay);
+    *geo = g;
+    return e->train_ais[g];
+}
+
+// ncf_ais_begin: no update pending, S_{adam_t} in buffer 0; the three gradient buffers
+// cleared over the active ranges and the loss slot.
+__global__ __launch_bounds__(256) void ais_begin_kernel(ncf_step_ctl* ctl, int64_t* st, float* g0, float* g1, float* g2,
+                                                        Ranges R, int64_t loss_i) {
+    const int64_t total = R.prefix[R.n];
+    const f4 z = f4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
+        int which;
+        const int64_t i = range_locate(R, q, &which);
+        *reinterpret_cast<f4*>(g0 + i) = z;
+        *reinterpret_cast<f4*>(g1 + i) = z;
+        *reinterpret_cast<f4*>(g2 + i) = z;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        g0[loss_i] = g1[loss_i] = g2[loss_i] = 0.f;
+        st[0] = 0;
+        st[1] = ctl->adam_t & 1;
+    }
+}
+
+// ncf_ais_bump: a chunk of k launches done -- k batches, k - 1 + pending updates applied,
+// one pending for the next launch.
+__global__ void ais_bump_kernel(ncf_step_ctl* ctl, int64_t* st, int64_t k) {
+    if (threadIdx.x == 0) {
+        const int64_t pend0 = st[0];
+        ctl->adam_t = ctl->adam_t + k - 1 + pend0;
+        ctl->batch = ctl->batch + k;
+        st[0] = 1;
+    }
+}
+
+// ncf_ais_flush, first launch: the pending update written into buffer 0 (or, with
+// none pending, S_{adam_t} copied there from buffer 1), its loss recorded, its gradient
+// cleared; reads ctl / st only (the second launch advances them).
+__global__ __launch_bounds__(256) void ais_flush_kernel(AisArgs x, ncf_step_ctl* ctl, int64_t loss_i) {
+#pragma clang fp contract(off)
+    __shared__ float sc[2];
+    const int64_t pend = x.st[0], par = x.st[1];
+    const int64_t n = ctl->adam_t + 1;
+    const int rb = (int)((pend ? n - 1 + par : ctl->adam_t + par) & 1);
+    const ScCache sce = sc_peek(x.scc, n);
+    float* gr = x.g[n % 3];
+    if (pend) {
+        if (blockIdx.x == 0 && threadIdx.x == 0 && x.loss_hist != nullptr && x.hist_len > 0) {
+            const int64_t b = ctl->batch - 1;
+            x.loss_hist[((b % x.hist_len) + x.hist_len) % x.hist_len] = gr[loss_i];
+        }
+        sc_resolve(sce, n, x.lr, x.beta1, x.beta2, sc);
+        step_scalars_ahead(x.scc, n, x.lr, x.beta1, x.beta2);
+    }
+    __syncthreads();
+    if (!pend && rb == 0) return;  // block-uniform: already in buffer 0
+    const float neg_step = sc[0], bc2s = sc[1];
+    const float w1 = (float)(1.0 - x.beta1), b2 = (float)x.beta2, omb2 = (float)(1.0 - x.beta2);
+    const int64_t total = x.R.prefix[x.R.n];
+    const f4 z = f4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
+        int which;
+        const int64_t i = range_locate(x.R, q, &which);
+        f4 pp = *reinterpret_cast<const f4*>(x.p[rb] + i), mm = *reinterpret_cast<const f4*>(x.m[rb] + i),
+           vv = *reinterpret_cast<const f4*>(x.v[rb] + i);
+        if (pend) {
+            const f4 gg = *reinterpret_cast<const f4*>(gr + i);
+            adam_f4(pp, mm, vv, gg, w1, b2, omb2, bc2s, x.eps, neg_step);
+            *reinterpret_cast<f4*>(gr + i) = z;
+        }
+        *reinterpret_cast<f4*>(x.p[0] + i) = pp;
+        *reinterpret_cast<f4*>(x.m[0] + i) = mm;
+        *reinterpret_cast<f4*>(x.v[0] + i) = vv;
+    }
+    if (pend && blockIdx.x == 0 && threadIdx.x == 0) gr[loss_i] = 0.f;
+}
+
+__global__ void ais_flush_done_kernel(ncf_step_ctl* ctl, int64_t* st) {
+    if (threadIdx.x == 0) {
+        const int64_t t = ctl->adam_t + st[0];
+        ctl->adam_t = t;
+        st[0] = 0;
+        st[1] = t & 1;
+    }
+}
+
+static int ais_args(const ncf_layout* lay, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                    const ncf_ais_bufs* b, const int64_t* ranges, int nranges, AisArgs* x) {
+    if (!lay || !params || !grads || !exp_avg || !exp_avg_sq || !b || !ranges) return NCF_E_ARG;
+    if (!b->params_b || !b->exp_avg_b || !b->exp_avg_sq_b || !b->grads_1 || !b->grads_2 || !b->state) return NCF_E_ARG;
+    memset(x, 0, sizeof(*x));
+    int err = 0;
+    x->R = make_ranges(ranges, nranges, &err);
+    if (err) return NCF_E_ARG;
+    for (int i = 0; i < nranges; ++i)  // every active float inside the flat buffers
+        if (ranges[2 * i + 1] > lay->total) return NCF_E_ARG;
+    x->p[0] = params;
+    x->p[1] = b->params_b;
+    x->m[0] = exp_avg;
+    x->m[1] = b->exp_avg_b;
+    x->v[0] = exp_avg_sq;
+    x->v[1] = b->exp_avg_sq_b;
+    x->g[0] = grads;
+    x->g[1] = b->grads_1;
+    x->g[2] = b->grads_2;
+    x->st = b->state;
+    return NCF_OK;
+}
+
+static unsigned ais_grid(const Ranges& R, int64_t cap) {
+    int64_t g = (R.prefix[R.n] + 255) / 256;
+    if (g > cap) g = cap;
+    return (unsigned)(g < 1 ? 1 : g);
+}
+
+}  // namespace ncf
+
+extern "C" {
+
+int ncf_ais_supported(const ncf_layout* lay) {
+    int geo = 0;
+    return (lay && ais_kernel(lay, &geo) != nullptr) ? 1 : 0;
+}
+
+int ncf_ais_begin(const ncf_layout* lay, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                  const ncf_ais_bufs* b, const int64_t* ranges, int nranges, ncf_step_ctl* ctl, void* stream) {
+    AisArgs x;
+    const int rc = ais_args(lay, params, grads, exp_avg, exp_avg_sq, b, ranges, nranges, &x);
+    if (rc != NCF_OK) return rc;
+    if (!ctl) return NCF_E_ARG;
+    const hipStream_t st = (hipStream_t)stream;
+    const size_t bytes = (size_t)lay->total * 4;  // buffer 1 = buffer 0 (inactive floats stay equal)
+    if (hipMemcpyAsync(b->params_b, params, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(b->exp_avg_b, exp_avg, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(b->exp_avg_sq_b, exp_avg_sq, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return NCF_E_LAUNCH;
+    hipLaunchKernelGGL(ais_begin_kernel, dim3(ais_grid(x.R, 1024)), dim3(256), 0, st, ctl, b->state, grads, b->grads_1,
+                       b->grads_2, x.R, lay->tower_begin + lay->tower_len);
+    return launch_status();
+}
+
+int ncf_train_step_ais(const ncf_layout* lay, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                       const ncf_ais_bufs* b, const int64_t* ranges, int nranges, const uint64_t* rows,
+                       const float* dlogit, ncf_step_ctl* ctl, int64_t batch_global, int dz_mode, float kd_wt,
+                       float kd_wr, float kd_temp, double lr, double beta1, double beta2, double eps,
+                       float* loss_hist, int64_t hist_len, int64_t step_i, void* stream) {
+    AisArgs x;
+    int rc = ais_args(lay, params, grads, exp_avg, exp_avg_sq, b, ranges, nranges, &x);
+    if (rc != NCF_OK) return rc;
+    if (!rows || !ctl || batch_global <= 0 || step_i < 0) return NCF_E_ARG;
+    if (dz_mode != NCF_DZ_BCE && dz_mode != NCF_DZ_DLOGIT && dz_mode != NCF_DZ_KD) return NCF_E_ARG;
+    if (dz_mode != NCF_DZ_BCE && !dlogit) return NCF_E_ARG;
+    int geo = 0;
+    const void* fn = ais_kernel(lay, &geo);
+    if (!fn) return NCF_E_UNSUPPORTED;
+    const KernelEntry* e = train_fused(lay);
+    const int64_t lds = train_lds_floats(e, lay, geo) * 4;
+    if (lds > LDS_LIMIT_BYTES) return NCF_E_UNSUPPORTED;
+    if (ensure_lds(fn, lds) != NCF_OK) return NCF_E_LAUNCH;
+    x.lr = lr;
+    x.beta1 = beta1;
+    x.beta2 = beta2;
+    x.eps = (float)eps;
+    x.loss_hist = loss_hist;
+    x.hist_len = hist_len;
+    x.scc = sc_cache_for(ctl, stream);
+    x.step_i = step_i;
+    x.ntrain = slab_rows_of(lay);
+    TrainArgs a;
+    memset(&a, 0, sizeof(a));
+    a.lay = *lay;
+    a.params = params;
+    a.grads = grads;
+    a.rows = rows;
+    a.dlogit = dz_mode != NCF_DZ_BCE ? dlogit : reinterpret_cast<const float*>(rows);
+    a.ctl = ctl;
+    a.batch_global = batch_global;
+    a.world = 1;
+    a.rank = 0;
+    a.dz_mode = dz_mode;
+    a.kd_wt = kd_wt;
+    a.kd_wr = kd_wr;
+    a.kd_temp = kd_temp;
+    a.diag = g_diag;
+    a.stamps = g_stamps;
+    a.ais = x;
+    // the dense update over every active float by the workgroups past the training ones
+    const unsigned extra = ais_grid(x.R, 4 * 256);
+    void* args[] = {&a};
+    if (hipLaunchKernel(fn, dim3((unsigned)x.ntrain + (extra < 2 ? 2 : extra)), dim3(geo_waves(geo) * WAVE), args,
+                        (size_t)lds, (hipStream_t)stream) != hipSuccess)
+        return NCF_E_LAUNCH;
+    return launch_status();
+}
+
+int ncf_ais_bump(ncf_step_ctl* ctl, const ncf_ais_bufs* b, int64_t k, void* stream) {
+    if (!ctl || !b || !b->state || k < 1) return NCF_E_ARG;
+    hipLaunchKernelGGL(ais_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ctl, b->state, k);
+    return launch_status();
+}
+
+int ncf_ais_flush(const ncf_layout* lay, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                  const ncf_ais_bufs* b, const int64_t* ranges, int nranges, ncf_step_ctl* ctl, double lr,
+                  double beta1, double beta2, double eps, float* loss_hist, int64_t hist_len, void* stream) {
+    AisArgs x;
+    const int rc = ais_args(lay, params, grads, exp_avg, exp_avg_sq, b, ranges, nranges, &x);
+    if (rc != NCF_OK) return rc;
+    if (!ctl) return NCF_E_ARG;
+    x.lr = lr;
+    x.beta1 = beta1;
+    x.beta2 = beta2;
+    x.eps = (float)eps;
+    x.loss_hist = loss_hist;
+    x.hist_len = hist_len;
+    x.scc = sc_cache_for(ctl, stream);
+    const hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(ais_flush_kernel, dim3(ais_grid(x.R, 1024)), dim3(256), 0, st, x, ctl,
+                       lay->tower_begin + lay->tower_len);
+    if (launch_status() != NCF_OK) return NCF_E_LAUNCH;
+    hipLaunchKernelGGL(ais_flush_done_kernel, dim3(1), dim3(64), 0, st, ctl, b->state);
+    return launch_status();
 }
 
 int ncf_kd_feature_step(const ncf_layout* student, const float* s_params, float* s_grads, const ncf_layout* teacher,

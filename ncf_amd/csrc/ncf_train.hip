@@ -88,7 +88,54 @@ __device__ __forceinline__ void set_r(f4& v, int r, float x) {
 // fact_expand_kernel (ncf_ops.hip) turns those sums into dUm, dIm, dW0 with
 // (U + I) / 16 tile GEMMs instead of B / 16.  Every wave then touches only its own
 // rows of LDS after the weight prologue, so tiles need no workgroup barrier.
-template <int F, int L, int MODE, bool FWD_ONLY, bool FACT, int NW>
+// NCF_LAYOUT_ADAM_IN_STEP, workgroups [ntrain, grid) of a training launch: update n
+// (pending) written for every active float -- S_n into buffer wb from S_{n-1} in rb
+// with the gradient g[n % 3], exactly the values the training workgroups compute on
+// the fly for what they read -- and g[(n + 2) % 3] cleared for the next launch's
+// accumulation.  Block 0 of them also records update n's loss and computes update
+// n + 1's step scalars (two double pows) into the cache.
+__device__ __forceinline__ void ais_dense_block(const TrainArgs& a, int64_t n, bool pending, int rb, float* sc) {
+#pragma clang fp contract(off)
+    const AisArgs& x = a.ais;
+    const int e = (int)blockIdx.x - x.ntrain, ne = (int)gridDim.x - x.ntrain;
+    const int64_t tb = a.lay.tower_begin, loss_i = tb + a.lay.tower_len;
+    float* gz = x.g[(n + 2) % 3];
+    const float* gr = x.g[n % 3];
+    const float *pr = x.p[rb], *mr = x.m[rb], *vr = x.v[rb];
+    float *pw = x.p[rb ^ 1], *mw = x.m[rb ^ 1], *vw = x.v[rb ^ 1];
+    const int64_t total = x.R.prefix[x.R.n];
+    const int64_t nthr = (int64_t)ne * blockDim.x;
+    const ScCache sce = sc_peek(x.scc, n);
+    if (e == 0 && threadIdx.x == 0) {
+        gz[loss_i] = 0.f;
+        if (pending && x.loss_hist != nullptr && x.hist_len > 0) {
+            const int64_t b = a.ctl->batch + x.step_i - 1;  // the batch whose gradient is update n's
+            x.loss_hist[((b % x.hist_len) + x.hist_len) % x.hist_len] = gr[loss_i];
+        }
+    }
+    if (e == 0) step_scalars_ahead_lane(x.scc, n, x.lr, x.beta1, x.beta2);
+    sc_resolve(sce, n, x.lr, x.beta1, x.beta2, sc);
+    __syncthreads();
+    const float neg_step = sc[0], bc2s = sc[1];
+    const float w1 = (float)(1.0 - x.beta1), b2 = (float)x.beta2, omb2 = (float)(1.0 - x.beta2);
+    const f4 z4 = f4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t q = (int64_t)e * blockDim.x + threadIdx.x; q < total; q += nthr) {
+        int which;
+        const int64_t i = range_locate(x.R, q, &which);
+        if (pending) {
+            f4 pp = *reinterpret_cast<const f4*>(pr + i), mm = *reinterpret_cast<const f4*>(mr + i),
+               vv = *reinterpret_cast<const f4*>(vr + i);
+            const f4 gg = *reinterpret_cast<const f4*>(gr + i);
+            adam_f4(pp, mm, vv, gg, w1, b2, omb2, bc2s, x.eps, neg_step);
+            *reinterpret_cast<f4*>(pw + i) = pp;
+            *reinterpret_cast<f4*>(mw + i) = mm;
+            *reinterpret_cast<f4*>(vw + i) = vv;
+        }
+        *reinterpret_cast<f4*>(gz + i) = z4;
+    }
+}
+
+template <int F, int L, int MODE, bool FWD_ONLY, bool FACT, int NW, bool AIS = false>
 __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     using S_ = Shape<F, L, MODE, NW>;
     // workgroup geometry: NW waves, 16 rows each, per tile (NW = 8, or 4 for small batches)
@@ -115,6 +162,86 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     const int g0 = l0 >> 4;
     const ncf_layout& lay = a.lay;
     const float* __restrict__ prm = a.params;
+    float* __restrict__ grads = a.grads;
+
+    // NCF_LAYOUT_ADAM_IN_STEP: the state this launch reads (S_{n-1}, with update n
+    // pending, applied on the fly), the gradient it accumulates (update n + 1's)
+    static_assert(!AIS || (!FACT && !FWD_ONLY), "in-step Adam: per-row layer 0, training launches");
+    const float* mrd = nullptr;
+    const float* vrd = nullptr;
+    const float* gread = nullptr;
+    bool ais_pend = false;
+    float* ais_sc = smem + S_::W_TOTAL + 10 * TRW;  // = sB below, written after the scalars are read
+    if constexpr (AIS) {
+        const int64_t pend0 = a.ais.st[0], par = a.ais.st[1];
+        const int64_t n = a.ctl->adam_t + a.ais.step_i + pend0;
+        ais_pend = a.ais.step_i > 0 || pend0 != 0;
+        const int rb = (int)((ais_pend ? n - 1 + par : n + par) & 1);
+        prm = a.ais.p[rb];
+        mrd = a.ais.m[rb];
+        vrd = a.ais.v[rb];
+        gread = a.ais.g[n % 3];
+        grads = a.ais.g[(n + 1) % 3];
+        if ((int)blockIdx.x >= a.ais.ntrain) {
+            ais_dense_block(a, n, ais_pend, rb, ais_sc);
+            return;
+        }
+        const ScCache sce = sc_peek(a.ais.scc, n);
+        if (ais_pend) sc_resolve(sce, n, a.ais.lr, a.ais.beta1, a.ais.beta2, ais_sc);
+    }
+    float ais_w1 = 0.f, ais_b2 = 0.f, ais_omb2 = 0.f, ais_ns = 0.f, ais_bc = 1.f;
+    if constexpr (AIS) {
+        ais_w1 = (float)(1.0 - a.ais.beta1);
+        ais_b2 = (float)a.ais.beta2;
+        ais_omb2 = (float)(1.0 - a.ais.beta2);
+    }
+    // one parameter float4 / float as this launch sees it
+    auto pval4 = [&](int64_t i) -> f4 {
+        f4 pp = *reinterpret_cast<const f4*>(prm + i);
+        if constexpr (AIS) {
+            if (ais_pend) {
+                f4 mm = *reinterpret_cast<const f4*>(mrd + i), vv = *reinterpret_cast<const f4*>(vrd + i);
+                const f4 gg = *reinterpret_cast<const f4*>(gread + i);
+                adam_f4(pp, mm, vv, gg, ais_w1, ais_b2, ais_omb2, ais_bc, a.ais.eps, ais_ns);
+            }
+        }
+        return pp;
+    };
+    auto pval = [&](int64_t i) -> float {
+        float pp = prm[i];
+        if constexpr (AIS) {
+            if (ais_pend) {
+                float mm = mrd[i], vv = vrd[i];
+                pp = adam_1(pp, mm, vv, gread[i], ais_w1, ais_b2, ais_omb2, ais_bc, a.ais.eps, ais_ns);
+            }
+        }
+        return pp;
+    };
+    // AIS: the tower after update n, built into the (idle) staging region before the
+    // weights are read: in_ranges floats updated, the others as stored
+    const float* tw = prm;  // tower floats: tw[i - toff]
+    int64_t toff = 0;
+    float* sstage_ = smem + S_::W_TOTAL + S_::MISC;  // = sstage below
+    if constexpr (AIS) {
+        __syncthreads();  // ais_sc
+        ais_ns = ais_sc[0];
+        ais_bc = ais_sc[1];
+        const int64_t tb = lay.tower_begin;
+        const int n4 = (int)((lay.tower_len + 3) / 4);
+        for (int q = tid; q < n4; q += NTH) {
+            const int64_t i = tb + 4 * q;
+            f4 v;
+            if (ais_pend && in_ranges(a.ais.R, i)) {
+                v = pval4(i);
+            } else {
+                v = *reinterpret_cast<const f4*>(prm + i);
+            }
+            *reinterpret_cast<f4*>(sstage_ + 4 * q) = v;
+        }
+        __syncthreads();
+        tw = sstage_;
+        toff = tb;
+    }
 
     // Tower weight / bias loads first: they depend on nothing, so they fly while
     // the control block and the row indices make their round trips.
@@ -127,7 +254,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
             constexpr int k = decltype(kk)::value;
             constexpr int rows = 16 * S_::MT(k), cols4 = S_::S(k) / 4, outs = S_::S(k + 1);
             constexpr int PER = (rows * cols4 + NTH - 1) / NTH;
-            const f4* Wg = reinterpret_cast<const f4*>(prm + lay.w[k]);
+            const f4* Wg = reinterpret_cast<const f4*>(tw + (lay.w[k] - toff));
 #pragma unroll
             for (int q = 0; q < PER; ++q) {
                 const int e = tid + q * NTH;
@@ -137,7 +264,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
             for (int q = 0; q < BPER; ++q) {
                 const int e = tid + q * NTH;
-                breg[k][q] = e < outs ? prm[lay.b[k] + e] : 0.f;
+                breg[k][q] = e < outs ? tw[lay.b[k] - toff + e] : 0.f;
             }
         });
     }
@@ -151,7 +278,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     } else {
         const int64_t ntot = a.ctl->n_total;
         const int64_t nbatch = (ntot + a.batch_global - 1) / a.batch_global;
-        const int64_t b = nbatch > 0 ? a.ctl->batch % nbatch : 0;  // epochs repeat past the end
+        const int64_t b = nbatch > 0 ? (a.ctl->batch + (AIS ? a.ais.step_i : 0)) % nbatch : 0;  // epochs repeat past the end
         const int64_t b0 = b * a.batch_global;
         int64_t gb = ntot - b0;
         if (gb > a.batch_global) gb = a.batch_global;
@@ -164,12 +291,13 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         base = b0 + lo;
         nloc = hi - lo;
         gb_f = (float)gb;
-        if (blockIdx.x == 0 && tid == 0) {  // step snapshot for ncf_reduce_adam_step (fields no WG reads here)
+        if (!AIS && blockIdx.x == 0 && tid == 0) {  // step snapshot for ncf_reduce_adam_step (fields no WG reads here)
             a.ctl->snap_batch = a.ctl->batch;
             a.ctl->snap_t = a.ctl->adam_t + 1;
         }
     }
     const int64_t ntiles = (nloc + TRW - 1) / TRW;
+    const int64_t gtrain = AIS ? (int64_t)a.ais.ntrain : (int64_t)gridDim.x;  // training workgroups
     stamp(a, 0);
 
     // Row prefetch: every thread issues the same loads (clamped row), so the
@@ -215,7 +343,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         }
     };
     if ((int64_t)blockIdx.x < ntiles) load_idx((int64_t)blockIdx.x * TRW);
-    if constexpr (FACT && !FWD_ONLY) load_idx2(((int64_t)blockIdx.x + gridDim.x) * TRW);
+    if constexpr (FACT && !FWD_ONLY) load_idx2(((int64_t)blockIdx.x + gtrain) * TRW);
 
     // ---- tower weights, biases, predict weights -> LDS (zero-padded) ---------
     if constexpr (S_::MLP) {
@@ -237,7 +365,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                 if (tid + q * NTH < 16 * S_::MT(k)) sB[S_::boff(k) + tid + q * NTH] = breg[k][q];
         });
     }
-    for (int e = tid; e < 128; e += NTH) sWP[e] = e < S_::P ? prm[lay.wp + e] : 0.f;
+    for (int e = tid; e < 128; e += NTH) sWP[e] = e < S_::P ? tw[lay.wp - toff + e] : 0.f;
 
     // ---- per-lane persistent accumulators ----------------------------------
     constexpr int MT0 = S_::MLP ? S_::MT(0) : 1;
@@ -274,8 +402,8 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
 
     constexpr int RPI = S_::GMF ? 64 / F : 1;  // GMF rows per wave-instruction
     constexpr int NI = S_::GMF ? 16 / RPI : 1;
-    const float bpv = prm[lay.bp];
-    const float wpf = S_::GMF ? prm[lay.wp + l0 % F] : 0.f;
+    const float bpv = tw[lay.bp - toff];
+    const float wpf = S_::GMF ? tw[lay.wp - toff + l0 % F] : 0.f;
     publish(0);
     if constexpr (FACT && !FWD_ONLY) {
         npr = npr2;
@@ -300,7 +428,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                 const int j0 = 16 * t + 4 * g;
                 const bool isu = j0 < DM;
                 const int64_t off = isu ? lay.um + (int64_t)uc * DM + j0 : lay.im + (int64_t)ic * DM + (j0 - DM);
-                X0[t] = *reinterpret_cast<const f4*>(prm + off);
+                X0[t] = pval4(off);
             }
         }
     };
@@ -311,8 +439,8 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
             for (int j = 0; j < NI; ++j) {
                 const int q = wr + j * RPI + gq0;
-                ugv[j] = prm[lay.ug + (int64_t)max(su[q], 0) * F + gf];
-                igv[j] = prm[lay.ig + (int64_t)max(si[q], 0) * F + gf];
+                ugv[j] = pval(lay.ug + (int64_t)max(su[q], 0) * F + gf);
+                igv[j] = pval(lay.ig + (int64_t)max(si[q], 0) * F + gf);
             }
         }
     };
@@ -374,7 +502,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                     sum += v[row];
                     if (row == 15 || ids[row + 1] != ids[row]) {
                         if (ids[row] >= 0 && f < DM && !DIAG_ON(a, DIAG_NO_ITEM_SCATTER))
-                            atomicAdd(a.grads + lay.im + (int64_t)ids[row] * DM + f, sum);
+                            atomicAdd(grads + lay.im + (int64_t)ids[row] * DM + f, sum);
                         sum = 0.f;
                     }
                 }
@@ -392,7 +520,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                 sum += v[row];
                 if (row == 15 || ids[row + 1] != ids[row]) {
                     if (ids[row] >= 0 && l < F && !DIAG_ON(a, DIAG_NO_GMF_SCATTER))
-                        atomicAdd(a.grads + lay.ig + (int64_t)ids[row] * F + l, sum);
+                        atomicAdd(grads + lay.ig + (int64_t)ids[row] * F + l, sum);
                     sum = 0.f;
                 }
             }
@@ -417,13 +545,13 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     stamp(a, 1);
     int titer = 0;
 
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gtrain) {
         const int64_t row0 = tile * TRW;
         const int buf = titer & 1;
         const int* su = su2 + buf * TRW;
         const int* si = si2 + buf * TRW;
         const float* slab_ = slab2 + buf * TRW;
-        const bool has_next = tile + gridDim.x < ntiles;
+        const bool has_next = tile + gtrain < ntiles;
         const int sb = 2 + 14 * titer;  // stamp base of this tile
         stamp(a, sb + 0);
         const int wr = w * 16;  // first tile row of this wave
@@ -436,9 +564,9 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
 
         // (a) next tile's indices
         if constexpr (EARLY) {
-            load_idx2(row0 + 2 * (int64_t)gridDim.x * TRW);
+            load_idx2(row0 + 2 * gtrain * TRW);
         } else {
-            load_idx(row0 + (int64_t)gridDim.x * TRW);
+            load_idx(row0 + gtrain * TRW);
             nok = nok && has_next;
         }
 
@@ -542,7 +670,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
                         for (int s = 0; s < 4; ++s) {
                             const int id = max(ids[ws * 16 + 4 * g + s], 0);
-                            bx[j][ws * 4 + s] = prm[tab + (int64_t)id * DM];
+                            bx[j][ws * 4 + s] = pval(tab + (int64_t)id * DM);
                         }
                     }
                 }
@@ -586,7 +714,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                     if (a.ustore != nullptr)  // NCF_LAYOUT_USER_STORE: [Um part][Ug part] of row q
                         a.ustore[(row0 + q) * a.uw + (S_::MLP ? S_::DM : 0) + gf] = dgm * igv[j];
                     else if (!DIAG_ON(a, DIAG_NO_GMF_SCATTER))
-                        atomicAdd(a.grads + lay.ug + (int64_t)max(su[q], 0) * F + gf, dgm * igv[j]);
+                        atomicAdd(grads + lay.ug + (int64_t)max(su[q], 0) * F + gf, dgm * igv[j]);
                     gIg[j] = dgm * ugv[j];
                 }
                 if constexpr (EARLY) load_gmf(su2 + (buf ^ 1) * TRW, si2 + (buf ^ 1) * TRW, l);
@@ -658,7 +786,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                                 if (a.ustore != nullptr)
                                     a.ustore[(row0 + wr + qi * RPW + l / FPI) * a.uw + f] = uv[qi][fi];
                                 else if (!DIAG_ON(a, DIAG_NO_USER_SCATTER))
-                                    atomicAdd(a.grads + lay.um + (int64_t)uid[qi] * DM + f, uv[qi][fi]);
+                                    atomicAdd(grads + lay.um + (int64_t)uid[qi] * DM + f, uv[qi][fi]);
                             }
                         }
                     } else {  // DM == 8: one 16-column tile, lanes c < 8 user, c >= 8 item
@@ -672,7 +800,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                             if (c < DM && a.ustore != nullptr)
                                 a.ustore[(row0 + wr + 4 * g + r) * a.uw + c] = lane_get(acc[0], r);
                             else if (c < DM)
-                                atomicAdd(a.grads + lay.um + (int64_t)uu * DM + c, lane_get(acc[0], r));
+                                atomicAdd(grads + lay.um + (int64_t)uu * DM + c, lane_get(acc[0], r));
                         }
                     }
                 };
@@ -794,7 +922,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                                 if (a.ustore != nullptr)
                                     a.ustore[(row0 + wr + qi * RPW + l / FPI) * a.uw + f] = uv[qi][fi];
                                 else if (!DIAG_ON(a, DIAG_NO_USER_SCATTER))
-                                    atomicAdd(a.grads + lay.um + (int64_t)uid[qi] * DM + f, uv[qi][fi]);
+                                    atomicAdd(grads + lay.um + (int64_t)uid[qi] * DM + f, uv[qi][fi]);
                             }
                         }
                         stamp(a, sb + 5 + 3 * (L - 1));
@@ -986,6 +1114,14 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         const int64_t tb = lay.tower_begin;
         const int len = (int)lay.tower_len + 64;  // slab stride (ncf_slab_stride); loss at tower_len
         float* out = a.slab + (int64_t)blockIdx.x * len;
+        // AIS: no slab -- the tower partials (and the loss at tower_len) are added into the
+        // gradient buffer, which the next launch reads like the embedding rows
+        auto put = [&](int64_t pos, float v) {
+            if constexpr (AIS)
+                atomicAdd(grads + tb + pos, v);
+            else
+                out[pos] = v;
+        };
         const int l = l0, c = c0, g = g0;
         // layer-0 wgrad: this wave's 16-column block, already summed over the rows
         // (FACT: formed after the step by fact_expand_kernel; its slab columns unused;
@@ -1000,7 +1136,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int o = 16 * mt + 4 * g + r;
-                        if (o < S_::S(1)) out[(lay.w[0] - tb) + o * S_::S(0) + 16 * ntj + c] = lane_get(accW0[j][mt], r);
+                        if (o < S_::S(1)) put((lay.w[0] - tb) + o * S_::S(0) + 16 * ntj + c, lane_get(accW0[j][mt], r));
                     }
                 }
             }
@@ -1065,7 +1201,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                 const int64_t pos = e < S1 ? (lay.b[0] - tb) + e
                                   : e < S1 + S_::P ? (lay.wp - tb) + (e - S1)
                                   : e == S1 + S_::P ? (lay.bp - tb) : (int64_t)lay.tower_len;
-                out[pos] = ts;
+                put(pos, ts);
             }
         };
         // every wave past its last tile: the staging is free.  FACT: a wave's staging
@@ -1115,14 +1251,14 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                             float s = 0.f;
 #pragma unroll
                             for (int ws = 0; ws < NWV; ++ws) s += sstage[ws * S_::WAVE_STAGE + e];
-                            out[(lay.w[k] - tb) + e] = s;
+                            put((lay.w[k] - tb) + e, s);
                         } else if (BIAS && e < SO * SK + SO) {
                             float s = 0.f;
 #pragma unroll
                             for (int ws = 0; ws < NWV; ++ws)
 #pragma unroll
                                 for (int gg = 0; gg < 4; ++gg) s += sstage[ws * S_::WAVE_STAGE + SO * SK + gg * SO + (e - SO * SK)];
-                            out[(lay.b[k] - tb) + (e - SO * SK)] = s;
+                            put((lay.b[k] - tb) + (e - SO * SK), s);
                         }
                     }
                     if constexpr (TAIL_MERGED && k == L - 1)
@@ -1141,7 +1277,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         // alignment gaps of the 64-float segments (ncf_layout_init)
         auto zero_gap = [&](int64_t seg, int n) {
             const int gap = ((n + 63) & ~63) - n;
-            if (tid < gap) out[(seg - tb) + n + tid] = 0.f;
+            if (!AIS && tid < gap) out[(seg - tb) + n + tid] = 0.f;
         };
         if constexpr (S_::MLP) {
             static_for<L>([&](auto kk) {
@@ -1185,6 +1321,11 @@ static void set_geo(KernelEntry& e) {
         e.train_fact[G] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, true, NW>);
     else
         e.train_fact[G] = nullptr;
+    // in-step Adam (NCF_LAYOUT_ADAM_IN_STEP): the small-batch geometry only
+    if constexpr (G == GEO_4 && regs_ok && (!S8::MLP || S8::MT(0) * S8::KT(0) <= 8))
+        e.train_ais[G] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, false, NW, true>);
+    else
+        e.train_ais[G] = nullptr;
     e.misc[G] = SG::MISC;
     e.stage[G] = NW * SG::WAVE_STAGE;
 }

@@ -641,9 +641,18 @@ class TrainEngine:
 
     def flush(self):
         """Deferred Adam: every embedding row brought up to the current step (the
-        parameters and moments are then the dense optimizer's).  No-op otherwise."""
+        parameters and moments are then the dense optimizer's).  In-step Adam: the
+        pending update written (ncf_ais_flush).  No-op otherwise."""
         if self.dp_mode == "owner":
             self.owner_sync()
+        if getattr(self, "_ais_live", False):
+            b = self._ais_bufs()
+            L.check(L.hip().ncf_ais_flush(ctypes.byref(self.lay), self.flat.data_ptr(), self.grads.data_ptr(),
+                                          self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), ctypes.byref(b),
+                                          self._ranges, self._nranges, self.ctl.data_ptr(), self.lr,
+                                          self.betas[0], self.betas[1], self.eps, self.loss_hist.data_ptr(),
+                                          self.num_batches, L.stream_ptr(self.device)), "ncf_ais_flush")
+            self._ais_live = False
         if not self.lazy:
             return
         L.check(L.hip().ncf_lazy_adam_flush(ctypes.byref(self.lay), self.flat.data_ptr(), self.grads.data_ptr(),
@@ -790,8 +799,66 @@ class TrainEngine:
         (ncf_reduce_adam_step); otherwise reduce, [all-reduce], optimizer."""
         return self.dp_mode == "single" and self.optimizer == "adam" and os.environ.get("NCF_FUSED_ADAM", "1") == "1"
 
+    # NCF_ADAM_IN_STEP=0 turns the in-step optimizer off (two launches per step)
+    ADAM_IN_STEP = os.environ.get("NCF_ADAM_IN_STEP", "1") != "0"
+
+    @property
+    def _ais_active(self):
+        """In-step Adam (ABI 18, ncf_train_step_ais): single process, dense Adam, the fused
+        small-batch kernel with per-row layer 0; response distillation only (its logits
+        ride in the launch, feature terms would add into the gradient separately)."""
+        if not (self.ADAM_IN_STEP and self._fused_optimizer) or self.lazy:
+            return False
+        if self.distill is not None and self.distill.keys:
+            return False
+        return bool(L.hip().ncf_ais_supported(ctypes.byref(self.lay)))
+
+    def _ais_bufs(self):
+        if getattr(self, "_ais_b", None) is None:
+            n = int(self.lay.total)
+            z = lambda: torch.zeros(n, dtype=torch.float32, device=self.device)  # noqa: E731
+            self._ais_t = [z() for _ in range(5)] + [torch.zeros(4, dtype=torch.int64, device=self.device)]
+            self._ais_b = L.NcfAisBufs(*[t.data_ptr() for t in self._ais_t])
+        return self._ais_b
+
+    def _ais_begin(self):
+        if getattr(self, "_ais_live", False):
+            return
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("in-step Adam: ncf_ais_begin must run before graph capture")
+        b = self._ais_bufs()
+        L.check(L.hip().ncf_ais_begin(ctypes.byref(self.lay), self.flat.data_ptr(), self.grads.data_ptr(),
+                                      self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), ctypes.byref(b),
+                                      self._ranges, self._nranges, self.ctl.data_ptr(), L.stream_ptr(self.device)),
+                "ncf_ais_begin")
+        self._ais_live = True
+
+    def _ais_launch(self, step_i):
+        st = L.stream_ptr(self.device)
+        b = self._ais_bufs()
+        if self.distill is not None:
+            d = self.distill
+            dl, dz, kd = d.tlog.data_ptr(), L.DZ_KD, (d.w_task, d.w_resp, d.temperature)
+        else:
+            dl, dz, kd = None, L.DZ_BCE, (0.0, 0.0, 0.0)
+        L.check(L.hip().ncf_train_step_ais(ctypes.byref(self.lay), self.flat.data_ptr(), self.grads.data_ptr(),
+                                           self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), ctypes.byref(b),
+                                           self._ranges, self._nranges, self.rows.data_ptr(), dl, self.ctl.data_ptr(),
+                                           self.batch_size, dz, kd[0], kd[1], kd[2], self.lr, self.betas[0],
+                                           self.betas[1], self.eps, self.loss_hist.data_ptr(), self.num_batches,
+                                           step_i, st), "ncf_train_step_ais")
+
+    def _ais_bump(self, k):
+        L.check(L.hip().ncf_ais_bump(self.ctl.data_ptr(), ctypes.byref(self._ais_bufs()), k,
+                                     L.stream_ptr(self.device)), "ncf_ais_bump")
+
     def _train_launch(self):
         st = L.stream_ptr(self.device)
+        if self._ais_active:  # one whole step: the previous step's Adam rides in this launch
+            self._ais_begin()
+            self._ais_launch(0)
+            self._ais_bump(1)
+            return
         if self.distill is not None:
             self.distill.launch(self, st)
             return
@@ -803,6 +870,8 @@ class TrainEngine:
 
     def _reduce_adam(self):
         st = L.stream_ptr(self.device)
+        if self._ais_active:  # inside the next training launch (or ncf_ais_flush)
+            return
         if self.lazy:
             L.check(L.hip().ncf_lazy_adam_step(ctypes.byref(self.lay), self.ws.data_ptr(), self.flat.data_ptr(),
                                                self.grads.data_ptr(), self.exp_avg.data_ptr(),
@@ -902,6 +971,8 @@ class TrainEngine:
     def step(self):
         """One optimizer step on global batch ctl.batch (eager launches)."""
         self._step_body()
+        if getattr(self, "_ais_live", False):
+            self.flush()  # in-step Adam: the update written now, not in the next launch
 
     @property
     def _capture_collective(self):
@@ -949,9 +1020,15 @@ class TrainEngine:
             k = self.graph_steps
             self._graph_k = None
             if k > 1:
-                def body():
-                    for _ in range(k):
-                        self._step_body()
+                if self._ais_active:
+                    def body():  # k launches, one bump: each launch applies its predecessor's Adam
+                        for j in range(k):
+                            self._ais_launch(j)
+                        self._ais_bump(k)
+                else:
+                    def body():
+                        for _ in range(k):
+                            self._step_body()
                 self._graph_k = (self._graph_of(body), k)  # the k-step graph and its step count
         elif self.dp_mode == "owner":
             # (compute, optimize, unpack + next compute, unpack): the collectives between
@@ -1018,6 +1095,8 @@ class TrainEngine:
         (ncf_lazy_adam_flush: a pass over the per-row step counters; rows the last
         batch of an epoch already caught up cost nothing), so the parameters are the
         dense optimizer's whenever run() returns."""
+        if self._ais_active:
+            self._ais_begin()  # eager: the step graphs may replay without an eager step first
         self._run(n_steps, use_graph)
         self.flush()
 
