@@ -2394,10 +2394,20 @@ int ncf_train_step_ais(const ncf_layout* lay, float* params, float* grads, float
     a.diag = g_diag;
     a.stamps = g_stamps;
     a.ais = x;
-    // the dense update over every active float by the workgroups past the training ones
-    const unsigned extra = ais_grid(x.R, 4 * 256);
-    void* args[] = {&a};
-    if (hipLaunchKernel(fn, dim3((unsigned)x.ntrain + (extra < 2 ? 2 : extra)), dim3(geo_waves(geo) * WAVE), args,
+    // the dense update over every active float by the workgroups past the training ones:
+    // a few, so their bursts of loads do not queue ahead of the training workgroups'
+    // dependent round trips (NCF_AIS_EXTRA, default 64)
+    static const int extra_cap = [] {
+        const char* e = getenv("NCF_AIS_EXTRA");
+        const int v = e ? atoi(e) : 192;
+        return v < 1 ? 1 : (v > 1024 ? 1024 : v);
+    }();
+    const int64_t t4 = x.R.prefix[x.R.n];  // float4 of the update; two per thread
+    int64_t extra = (t4 + 2 * 256 - 1) / (2 * 256);
+    if (extra > extra_cap) extra = extra_cap;
+    if (extra < 1) extra = 1;
+    void* args[] = {&a};  // + 1: the step-scalar workgroup (ais_dense_block)
+    if (hipLaunchKernel(fn, dim3((unsigned)(x.ntrain + extra + 1)), dim3(geo_waves(geo) * WAVE), args,
                         (size_t)lds, (hipStream_t)stream) != hipSuccess)
         return NCF_E_LAUNCH;
     return launch_status();

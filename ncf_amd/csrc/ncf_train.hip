@@ -97,7 +97,13 @@ __device__ __forceinline__ void set_r(f4& v, int r, float x) {
 __device__ __forceinline__ void ais_dense_block(const TrainArgs& a, int64_t n, bool pending, int rb, float* sc) {
 #pragma clang fp contract(off)
     const AisArgs& x = a.ais;
-    const int e = (int)blockIdx.x - x.ntrain, ne = (int)gridDim.x - x.ntrain;
+    // the last extra workgroup only computes update n + 1's step scalars (two double
+    // pows, ~2.5 us on one lane) -- beside the others, not ahead of a barrier of theirs
+    if ((int)blockIdx.x == (int)gridDim.x - 1) {
+        step_scalars_ahead_lane(x.scc, n, x.lr, x.beta1, x.beta2);
+        return;
+    }
+    const int e = (int)blockIdx.x - x.ntrain, ne = (int)gridDim.x - 1 - x.ntrain;
     const int64_t tb = a.lay.tower_begin, loss_i = tb + a.lay.tower_len;
     float* gz = x.g[(n + 2) % 3];
     const float* gr = x.g[n % 3];
@@ -113,25 +119,38 @@ __device__ __forceinline__ void ais_dense_block(const TrainArgs& a, int64_t n, b
             x.loss_hist[((b % x.hist_len) + x.hist_len) % x.hist_len] = gr[loss_i];
         }
     }
-    if (e == 0) step_scalars_ahead_lane(x.scc, n, x.lr, x.beta1, x.beta2);
     sc_resolve(sce, n, x.lr, x.beta1, x.beta2, sc);
     __syncthreads();
     const float neg_step = sc[0], bc2s = sc[1];
     const float w1 = (float)(1.0 - x.beta1), b2 = (float)x.beta2, omb2 = (float)(1.0 - x.beta2);
     const f4 z4 = f4{0.f, 0.f, 0.f, 0.f};
-    for (int64_t q = (int64_t)e * blockDim.x + threadIdx.x; q < total; q += nthr) {
+    // two float4 per thread and pass, all loads of a pass issued before its stores
+    for (int64_t q0 = (int64_t)e * blockDim.x + threadIdx.x; q0 < total; q0 += 2 * nthr) {
+        const int64_t q1 = q0 + nthr;
+        const bool has1 = q1 < total;
         int which;
-        const int64_t i = range_locate(x.R, q, &which);
+        const int64_t i0 = range_locate(x.R, q0, &which);
+        const int64_t i1 = has1 ? range_locate(x.R, q1, &which) : i0;
         if (pending) {
-            f4 pp = *reinterpret_cast<const f4*>(pr + i), mm = *reinterpret_cast<const f4*>(mr + i),
-               vv = *reinterpret_cast<const f4*>(vr + i);
-            const f4 gg = *reinterpret_cast<const f4*>(gr + i);
-            adam_f4(pp, mm, vv, gg, w1, b2, omb2, bc2s, x.eps, neg_step);
-            *reinterpret_cast<f4*>(pw + i) = pp;
-            *reinterpret_cast<f4*>(mw + i) = mm;
-            *reinterpret_cast<f4*>(vw + i) = vv;
+            f4 p0 = *reinterpret_cast<const f4*>(pr + i0), m0 = *reinterpret_cast<const f4*>(mr + i0),
+               v0 = *reinterpret_cast<const f4*>(vr + i0);
+            const f4 g0 = *reinterpret_cast<const f4*>(gr + i0);
+            f4 p1 = *reinterpret_cast<const f4*>(pr + i1), m1 = *reinterpret_cast<const f4*>(mr + i1),
+               v1 = *reinterpret_cast<const f4*>(vr + i1);
+            const f4 g1 = *reinterpret_cast<const f4*>(gr + i1);
+            adam_f4(p0, m0, v0, g0, w1, b2, omb2, bc2s, x.eps, neg_step);
+            *reinterpret_cast<f4*>(pw + i0) = p0;
+            *reinterpret_cast<f4*>(mw + i0) = m0;
+            *reinterpret_cast<f4*>(vw + i0) = v0;
+            if (has1) {
+                adam_f4(p1, m1, v1, g1, w1, b2, omb2, bc2s, x.eps, neg_step);
+                *reinterpret_cast<f4*>(pw + i1) = p1;
+                *reinterpret_cast<f4*>(mw + i1) = m1;
+                *reinterpret_cast<f4*>(vw + i1) = v1;
+            }
         }
-        *reinterpret_cast<f4*>(gz + i) = z4;
+        *reinterpret_cast<f4*>(gz + i0) = z4;
+        if (has1) *reinterpret_cast<f4*>(gz + i1) = z4;
     }
 }
 
@@ -173,6 +192,14 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     bool ais_pend = false;
     float* ais_sc = smem + S_::W_TOTAL + 10 * TRW;  // = sB below, written after the scalars are read
     if constexpr (AIS) {
+        // both cache entries requested with the control block (the entry of update n
+        // is picked once n is known: one round trip, not two dependent ones)
+        ScCache sce2[2];
+        sce2[0].t = sce2[1].t = -1;
+        if (threadIdx.x == 0 && a.ais.scc != nullptr) {
+            sce2[0] = a.ais.scc[0];
+            sce2[1] = a.ais.scc[1];
+        }
         const int64_t pend0 = a.ais.st[0], par = a.ais.st[1];
         const int64_t n = a.ctl->adam_t + a.ais.step_i + pend0;
         ais_pend = a.ais.step_i > 0 || pend0 != 0;
@@ -186,8 +213,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
             ais_dense_block(a, n, ais_pend, rb, ais_sc);
             return;
         }
-        const ScCache sce = sc_peek(a.ais.scc, n);
-        if (ais_pend) sc_resolve(sce, n, a.ais.lr, a.ais.beta1, a.ais.beta2, ais_sc);
+        if (ais_pend) sc_resolve((n & 1) ? sce2[1] : sce2[0], n, a.ais.lr, a.ais.beta1, a.ais.beta2, ais_sc);
     }
     float ais_w1 = 0.f, ais_b2 = 0.f, ais_omb2 = 0.f, ais_ns = 0.f, ais_bc = 1.f;
     if constexpr (AIS) {
@@ -195,18 +221,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         ais_b2 = (float)a.ais.beta2;
         ais_omb2 = (float)(1.0 - a.ais.beta2);
     }
-    // one parameter float4 / float as this launch sees it
-    auto pval4 = [&](int64_t i) -> f4 {
-        f4 pp = *reinterpret_cast<const f4*>(prm + i);
-        if constexpr (AIS) {
-            if (ais_pend) {
-                f4 mm = *reinterpret_cast<const f4*>(mrd + i), vv = *reinterpret_cast<const f4*>(vrd + i);
-                const f4 gg = *reinterpret_cast<const f4*>(gread + i);
-                adam_f4(pp, mm, vv, gg, ais_w1, ais_b2, ais_omb2, ais_bc, a.ais.eps, ais_ns);
-            }
-        }
-        return pp;
-    };
+    // one parameter float as this launch sees it (the per-row layer-0 wgrad operand)
     auto pval = [&](int64_t i) -> float {
         float pp = prm[i];
         if constexpr (AIS) {
@@ -222,33 +237,58 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     const float* tw = prm;  // tower floats: tw[i - toff]
     int64_t toff = 0;
     float* sstage_ = smem + S_::W_TOTAL + S_::MISC;  // = sstage below
-    if constexpr (AIS) {
-        __syncthreads();  // ais_sc
-        ais_ns = ais_sc[0];
-        ais_bc = ais_sc[1];
+    // (issued after the row indices: its loads fly with theirs)
+    auto build_image = [&]() {
+        // the tower's loads issued before the scalar barrier (AIS_TQ float4 per thread
+        // in flight; more in a second pass)
+        constexpr int AIS_TQ = 4;
         const int64_t tb = lay.tower_begin;
         const int n4 = (int)((lay.tower_len + 3) / 4);
-        for (int q = tid; q < n4; q += NTH) {
-            const int64_t i = tb + 4 * q;
-            f4 v;
-            if (ais_pend && in_ranges(a.ais.R, i)) {
-                v = pval4(i);
-            } else {
-                v = *reinterpret_cast<const f4*>(prm + i);
+        for (int q0 = 0; q0 < n4; q0 += AIS_TQ * NTH) {
+            f4 pp[AIS_TQ], mm[AIS_TQ], vv[AIS_TQ], gg[AIS_TQ];
+#pragma unroll
+            for (int u = 0; u < AIS_TQ; ++u) {
+                const int q = q0 + u * NTH + tid;
+                const int64_t i = tb + 4 * (int64_t)(q < n4 ? q : 0);
+                pp[u] = *reinterpret_cast<const f4*>(prm + i);
+                if (ais_pend) {
+                    mm[u] = *reinterpret_cast<const f4*>(mrd + i);
+                    vv[u] = *reinterpret_cast<const f4*>(vrd + i);
+                    gg[u] = *reinterpret_cast<const f4*>(gread + i);
+                }
             }
-            *reinterpret_cast<f4*>(sstage_ + 4 * q) = v;
+            if (q0 == 0) {
+                __syncthreads();  // ais_sc
+                ais_ns = ais_sc[0];
+                ais_bc = ais_sc[1];
+            }
+#pragma unroll
+            for (int u = 0; u < AIS_TQ; ++u) {
+                const int q = q0 + u * NTH + tid;
+                if (q >= n4) continue;
+                if (ais_pend && in_ranges(a.ais.R, tb + 4 * (int64_t)q))
+                    adam_f4(pp[u], mm[u], vv[u], gg[u], ais_w1, ais_b2, ais_omb2, ais_bc, a.ais.eps, ais_ns);
+                *reinterpret_cast<f4*>(sstage_ + 4 * q) = pp[u];
+            }
+        }
+        if (n4 == 0) {  // (every layout has the predict weights: not reached)
+            __syncthreads();
+            ais_ns = ais_sc[0];
+            ais_bc = ais_sc[1];
         }
         __syncthreads();
         tw = sstage_;
         toff = tb;
-    }
+    };
 
     // Tower weight / bias loads first: they depend on nothing, so they fly while
-    // the control block and the row indices make their round trips.
+    // the control block and the row indices make their round trips (AIS: from the
+    // image, after the row indices are requested).
     constexpr int PERMAX = S_::MLP ? (16 * S_::MT(0) * (S_::S(0) / 4) + NTH - 1) / NTH : 1;
     f4 wreg[L][PERMAX];
     constexpr int BPER = (128 + NTH - 1) / NTH;  // bias entries per thread (16 * MT(k) <= 128)
     float breg[L][BPER];
+    auto load_wregs = [&]() {
     if constexpr (S_::MLP) {
         static_for<L>([&](auto kk) {
             constexpr int k = decltype(kk)::value;
@@ -268,6 +308,8 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
             }
         });
     }
+    };
+    if constexpr (!AIS) load_wregs();
 
     // ---- rows of this rank -------------------------------------------------
     int64_t base, nloc;
@@ -343,6 +385,12 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         }
     };
     if ((int64_t)blockIdx.x < ntiles) load_idx((int64_t)blockIdx.x * TRW);
+    if constexpr (AIS) {
+        stamp(a, 58);  // diag: AIS row indices requested
+        build_image();
+        stamp(a, 59);  // diag: AIS tower image built
+        load_wregs();
+    }
     if constexpr (FACT && !FWD_ONLY) load_idx2(((int64_t)blockIdx.x + gtrain) * TRW);
 
     // ---- tower weights, biases, predict weights -> LDS (zero-padded) ---------
@@ -417,6 +465,39 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     //   ugv/igv: GMF rows, row-major lanes (feature l % F, rows j*RPI + l / F)
     f4 X0[KT0];
     float ugv[NI], igv[NI];
+    // AIS: the optimizer state of the fragments rides with them; the pending update is
+    // applied where the fragments are first used (ais_finish at the top of the tile),
+    // so the early loads keep their distance from their use (and from the waits that
+    // would also drain the scatter atomics issued after them)
+    constexpr int AKT = AIS ? KT0 : 1, ANI = AIS ? NI : 1;
+    f4 Xm[AKT], Xv[AKT], Xg[AKT];
+    float um_[ANI], uv_[ANI], ug_[ANI], im_[ANI], iv_[ANI], ig_[ANI];
+    auto raw4 = [&](int64_t off, f4& pp, f4& mm, f4& vv, f4& gg) {
+        pp = *reinterpret_cast<const f4*>(prm + off);
+        if constexpr (AIS) {
+            mm = *reinterpret_cast<const f4*>(mrd + off);
+            vv = *reinterpret_cast<const f4*>(vrd + off);
+            gg = *reinterpret_cast<const f4*>(gread + off);
+        }
+    };
+    auto ais_finish = [&]() {
+        if constexpr (AIS) {
+            if (ais_pend) {
+                if constexpr (S_::MLP) {
+#pragma unroll
+                    for (int t = 0; t < KT0; ++t)
+                        adam_f4(X0[t], Xm[t], Xv[t], Xg[t], ais_w1, ais_b2, ais_omb2, ais_bc, a.ais.eps, ais_ns);
+                }
+                if constexpr (S_::GMF) {
+#pragma unroll
+                    for (int j = 0; j < NI; ++j) {
+                        ugv[j] = adam_1(ugv[j], um_[j], uv_[j], ug_[j], ais_w1, ais_b2, ais_omb2, ais_bc, a.ais.eps, ais_ns);
+                        igv[j] = adam_1(igv[j], im_[j], iv_[j], ig_[j], ais_w1, ais_b2, ais_omb2, ais_bc, a.ais.eps, ais_ns);
+                    }
+                }
+            }
+        }
+    };
     auto load_mlp = [&](const int* su, const int* si, int c, int g) {
         const int wr = w * 16;
         if constexpr (S_::MLP) {
@@ -428,7 +509,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                 const int j0 = 16 * t + 4 * g;
                 const bool isu = j0 < DM;
                 const int64_t off = isu ? lay.um + (int64_t)uc * DM + j0 : lay.im + (int64_t)ic * DM + (j0 - DM);
-                X0[t] = pval4(off);
+                raw4(off, X0[t], Xm[AIS ? t : 0], Xv[AIS ? t : 0], Xg[AIS ? t : 0]);
             }
         }
     };
@@ -439,8 +520,18 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
 #pragma unroll
             for (int j = 0; j < NI; ++j) {
                 const int q = wr + j * RPI + gq0;
-                ugv[j] = pval(lay.ug + (int64_t)max(su[q], 0) * F + gf);
-                igv[j] = pval(lay.ig + (int64_t)max(si[q], 0) * F + gf);
+                const int64_t ou = lay.ug + (int64_t)max(su[q], 0) * F + gf;
+                const int64_t oi = lay.ig + (int64_t)max(si[q], 0) * F + gf;
+                ugv[j] = prm[ou];
+                igv[j] = prm[oi];
+                if constexpr (AIS) {
+                    um_[j] = mrd[ou];
+                    uv_[j] = vrd[ou];
+                    ug_[j] = gread[ou];
+                    im_[j] = mrd[oi];
+                    iv_[j] = vrd[oi];
+                    ig_[j] = gread[oi];
+                }
             }
         }
     };
@@ -546,6 +637,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     int titer = 0;
 
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gtrain) {
+        ais_finish();  // AIS: this tile's fragments after the pending update
         const int64_t row0 = tile * TRW;
         const int buf = titer & 1;
         const int* su = su2 + buf * TRW;

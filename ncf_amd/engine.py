@@ -799,19 +799,30 @@ class TrainEngine:
         (ncf_reduce_adam_step); otherwise reduce, [all-reduce], optimizer."""
         return self.dp_mode == "single" and self.optimizer == "adam" and os.environ.get("NCF_FUSED_ADAM", "1") == "1"
 
-    # NCF_ADAM_IN_STEP=0 turns the in-step optimizer off (two launches per step)
-    ADAM_IN_STEP = os.environ.get("NCF_ADAM_IN_STEP", "1") != "0"
+    # NCF_ADAM_IN_STEP: "auto" (default) -- the in-step optimizer where the step has at most
+    # AIS_MAX_WG training workgroups (C5's 256-row batch: 11.7 against 12.0 us/step; at
+    # C2's 16 workgroups the on-the-fly update quadruples each CU's gather loads and the
+    # step takes 22.7 against 18.4 us, profiles/r05_evidence/ais_ab/); "1" wherever the
+    # kernel exists, "0" never
+    ADAM_IN_STEP = os.environ.get("NCF_ADAM_IN_STEP", "auto")
+    AIS_MAX_WG = int(os.environ.get("NCF_AIS_MAX_WG", "4"))
 
     @property
     def _ais_active(self):
         """In-step Adam (ABI 18, ncf_train_step_ais): single process, dense Adam, the fused
         small-batch kernel with per-row layer 0; response distillation only (its logits
         ride in the launch, feature terms would add into the gradient separately)."""
-        if not (self.ADAM_IN_STEP and self._fused_optimizer) or self.lazy:
+        mode = {True: "1", False: "0"}.get(self.ADAM_IN_STEP, self.ADAM_IN_STEP)
+        if mode == "0" or not self._fused_optimizer or self.lazy:
             return False
         if self.distill is not None and self.distill.keys:
             return False
-        return bool(L.hip().ncf_ais_supported(ctypes.byref(self.lay)))
+        if not L.hip().ncf_ais_supported(ctypes.byref(self.lay)):
+            return False
+        if mode == "auto":
+            wg = (int(self.lay.flags) >> L.LAYOUT_WG_SHIFT) & L.LAYOUT_WG_MASK
+            return 0 < wg <= self.AIS_MAX_WG
+        return True
 
     def _ais_bufs(self):
         if getattr(self, "_ais_b", None) is None:

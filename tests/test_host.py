@@ -459,3 +459,17 @@ def test_stream_checksum_and_canonical_default():
     assert c0 != int(ops.stream_checksum(r2))
     assert ops.default_canonical() is False
     assert ops.EpochPrep("cpu").canonical is False
+
+
+def test_in_step_adam_kernel_availability():
+    """ncf_ais_supported (host logic, no GPU): the fused small-batch geometry with a
+    per-row layer 0 has the in-step kernel; the factored C3 shape does not."""
+    import ctypes
+    import ncf_amd._lib as L
+    lib = L.hip()
+    small = L.layout(6041, 3707, 8, 2, "MLP")
+    assert lib.ncf_layout_tune(ctypes.byref(small), 256) == L.NCF_OK
+    assert lib.ncf_ais_supported(ctypes.byref(small)) == 1
+    c3 = L.layout(6041, 3707, 16, 3, "NeuMF-end")
+    assert lib.ncf_layout_tune(ctypes.byref(c3), 65536) == L.NCF_OK
+    assert lib.ncf_ais_supported(ctypes.byref(c3)) == 0
