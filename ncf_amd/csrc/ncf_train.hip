@@ -192,6 +192,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     bool ais_pend = false;
     float* ais_sc = smem + S_::W_TOTAL + 10 * TRW;  // = sB below, written after the scalars are read
     if constexpr (AIS) {
+        if ((int)blockIdx.x < a.ais.ntrain) stamp(a, 63);  // diag: kernel entry
         // both cache entries requested with the control block (the entry of update n
         // is picked once n is known: one round trip, not two dependent ones)
         ScCache sce2[2];
@@ -1413,8 +1414,8 @@ static void set_geo(KernelEntry& e) {
         e.train_fact[G] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, true, NW>);
     else
         e.train_fact[G] = nullptr;
-    // in-step Adam (NCF_LAYOUT_ADAM_IN_STEP): the small-batch geometry only
-    if constexpr (G == GEO_4 && regs_ok && (!S8::MLP || S8::MT(0) * S8::KT(0) <= 8))
+    // in-step Adam (NCF_LAYOUT_ADAM_IN_STEP): the small-batch geometries
+    if constexpr (G != GEO_8 && regs_ok && (!S8::MLP || S8::MT(0) * S8::KT(0) <= 8))
         e.train_ais[G] = reinterpret_cast<const void*>(&ncf_step_kernel<F, L, MODE, false, false, NW, true>);
     else
         e.train_ais[G] = nullptr;

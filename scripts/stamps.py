@@ -23,7 +23,7 @@ for t in range(4):
     NAMES.update({b + 10: f"t{t}:L0:dgrad_mfma", b + 11: f"t{t}:L0:scatter", b + 13: f"t{t}:L0:wgrad+end-barrier"})
     NAMES[b + 13] = f"t{t}:end-barrier"
 NAMES.update({62: "epilogue:first barrier", 60: "epilogue:sums+stores", 61: "epilogue:drain",
-              58: "ais:row indices requested", 59: "ais:tower image built"})
+              58: "ais:row indices requested", 59: "ais:tower image built", 63: "ais:kernel entry"})
 for t in range(2):  # sub-phases of loss+gmf_bwd (slots of tiles 3-4, unused at bench size)
     NAMES.update({44 + 3 * t: f"t{t}:  bx-gather-issued", 45 + 3 * t: f"t{t}:  loss+dz"})
 
