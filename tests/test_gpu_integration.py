@@ -23,7 +23,8 @@ def _binding():
     text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     sec = text.split("## 2.", 1)[1].split("\n## 3.", 1)[0]
     blocks = re.findall(r"```python\n(.*?)```", sec, re.S)
-    assert len(blocks) == 3, "INTEGRATION.md section 2 must hold the train, distill and deferred-Adam stubs"
+    assert len(blocks) == 4, ("INTEGRATION.md section 2 must hold the train, in-step-Adam, distill and "
+                              "deferred-Adam stubs")
     lib = os.path.join(ROOT, "ncf_amd", "libncf_hip.so")
     ns = {}
     for b in blocks:
@@ -154,3 +155,41 @@ def test_documented_deferred_adam_steps_vs_oracle():
         np.testing.assert_allclose(v.cpu().numpy(), r.numpy(), rtol=1e-4, atol=2e-5, err_msg=k)
     assert ctl.cpu().tolist()[:2] == [T - 1, T - 1]
     assert int(last.min()) == T - 1 and float(grads.abs().max()) == 0.0
+
+
+def test_documented_in_step_adam_steps_vs_oracle():
+    """The section-2 in-step-Adam stub (ncf_ais_begin, ncf_train_step_ais, ncf_ais_bump,
+    ncf_ais_flush) on a C2-shaped stream (ml-1m ids, bs 1,024): 6 steps in one chunk,
+    flushed, vs 6 steps of the oracle's torch.optim.Adam on the same batches."""
+    from ncf_amd import ops
+    from ncf_amd.models import NCF
+    ns = _binding()
+    U, I, f, Lyr, B, T = 6041, 3707, 8, 3, 1024, 6
+    torch.manual_seed(9)
+    ref = O.OracleNCF(U, I, f, Lyr, 0.0, "NeuMF-end")
+    torch.manual_seed(9)
+    m = NCF(U, I, f, Lyr, 0.0, "NeuMF-end").to(DEV)
+    flat, _ = ops.ensure_flat(m)
+    lay = ns["layout"](m)
+    ns["_lib"].ncf_layout_tune(ctypes.byref(lay), B)
+    assert ns["_lib"].ncf_ais_supported(ctypes.byref(lay)) == 1
+    rng = np.random.default_rng(29)
+    n = B * T
+    users = rng.integers(0, U, n)
+    items = np.minimum(rng.zipf(1.3, n) - 1, I - 1)
+    labels = (rng.random(n) < 0.2).astype(np.int64)
+    rows = ns["pack"](torch.as_tensor(users, device=DEV), torch.as_tensor(items, device=DEV),
+                      torch.as_tensor(labels, device=DEV))
+    grads = torch.zeros(int(lay.total), device=DEV)
+    mom, vel = torch.zeros_like(grads), torch.zeros_like(grads)
+    ctl = torch.tensor([0, 0, n, 0, 0, 0], dtype=torch.int64, device=DEV)
+    keep, bufs = ns["ais_buffers"](lay, DEV)
+    ns["train_steps_ais"](flat, grads, mom, vel, lay, rows, ctl, B, _ranges(m, lay), bufs, T)
+    torch.cuda.synchronize()
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    O.train_steps(ref, opt, [users[k * B:(k + 1) * B] for k in range(T)],
+                  [items[k * B:(k + 1) * B] for k in range(T)], [labels[k * B:(k + 1) * B] for k in range(T)])
+    for (k, v), (_, r) in zip(m.state_dict().items(), ref.state_dict().items()):
+        np.testing.assert_allclose(v.cpu().numpy(), r.numpy(), rtol=1e-4, atol=2e-5, err_msg=k)
+    assert ctl.cpu().tolist()[:2] == [T, T]
+    del keep
