@@ -473,3 +473,20 @@ def test_in_step_adam_kernel_availability():
     c3 = L.layout(6041, 3707, 16, 3, "NeuMF-end")
     assert lib.ncf_layout_tune(ctypes.byref(c3), 65536) == L.NCF_OK
     assert lib.ncf_ais_supported(ctypes.byref(c3)) == 0
+
+
+def test_integration_section2_binding_loads_on_cpu():
+    """INTEGRATION.md section 2's code blocks exec as written on the CPU (the library
+    loads, every argtypes line names a real export); the GPU tests call them."""
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    text = open(os.path.join(root, "INTEGRATION.md")).read()
+    sec = text.split("## 2.", 1)[1].split("\n## 3.", 1)[0]
+    blocks = re.findall(r"```python\n(.*?)```", sec, re.S)
+    lib = os.path.join(root, "ncf_amd", "libncf_hip.so")
+    ns = {}
+    for b in blocks:
+        exec(compile(b.replace("/path/to/ncf_amd/libncf_hip.so", lib), "INTEGRATION.md", "exec"), ns)
+    for fn in ("train_step", "train_steps_ais", "ais_buffers", "distill_step", "train_step_lazy", "flush"):
+        assert callable(ns[fn]), fn
+    assert len(ns["_lib"].ncf_train_step_ais.argtypes) == 24
