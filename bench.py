@@ -867,16 +867,13 @@ def main():
     if path == L.PATH_FUSED:
         mode = {"GMF": 0, "MLP": 1}.get(mtype, 2)
         waves = (8, 4, 2, 1)[(int(eng.lay.flags) >> L.LAYOUT_GEO_SHIFT) & L.LAYOUT_GEO_MASK]
-        ais = bool(eng._ais_active)  # in-step Adam: the launch carries the optimizer
-        names = [f"ncf::ncf_step_kernel<{f}, {nl}, {mode}, false, {'true' if fact else 'false'}, {waves}"
-                 + (", true>" if ais else ">")]
+        names = [f"ncf::ncf_step_kernel<{f}, {nl}, {mode}, false, {'true' if fact else 'false'}, {waves}>"]
         if fact and not in_adam:
             names.append(f"ncf::fact_expand_kernel<{dm}>")
         kname = (f"ncf_step_kernel<{f},{nl},{mtype.split('-')[0]},FACT={str(fact).lower()}>"
                  + ((" (factored layer 0; its expansion GEMMs run in the optimizer launch, "
                      f"fact_reduce_adam_kernel<{dm}>)" if in_adam else
                      f" + fact_expand_kernel<{dm}> (factored layer 0)") if fact else " (per-row layer 0)")
-                 + ("; the previous step's Adam inside the launch (in-step Adam)" if ais else "")
                  + "; launch group timed back to back")
         traffic, traffic_src = pmc_traffic(args.config, names) if world == 1 else (None, None)
         busy, busy_src = newest_profile(args.config, names) if world == 1 else (None, None)
