@@ -582,10 +582,6 @@ int ncf_uses_user_order(const ncf_layout *lay);
  * rounds; see ncf_epoch.hip), always complete.  Since ABI 9 (was: a `rounds`
  * count and a device `remaining` report of the round-based version).
  *
- * ncf_randperm_gather (ABI 18): the same permutation applied to an epoch's packed rows
- * in the same pass: rows_out[k] = rows[perm[k]] (perm also written when non-null);
- * ncf_prepare_epoch2 with perm = NULL then groups rows_out as it stands.
- *
  * ncf_build_rows: rows_out = NCF_ROW_PACK of features_fill / labels_fill
  * (datasets.py:65-69): positives in file order, then positive p's num_ng
  * negatives neg[p*num_ng .. (p+1)*num_ng).
@@ -593,8 +589,6 @@ int ncf_uses_user_order(const ncf_layout *lay);
 int64_t ncf_randperm_workspace(int64_t n);
 int ncf_randperm(const uint32_t *words, int64_t n, int64_t *perm, void *workspace, int64_t workspace_bytes,
                  void *stream);
-int ncf_randperm_gather(const uint32_t *words, int64_t n, const uint64_t *rows, uint64_t *rows_out, int64_t *perm,
-                        void *workspace, int64_t workspace_bytes, void *stream);
 int ncf_build_rows(const int32_t *pos_users, const int32_t *pos_items, int64_t n_pos, const int32_t *neg, int num_ng,
                    uint64_t *rows_out, void *stream);
 

@@ -136,7 +136,6 @@ _HIP_PROTOS = {
     "ncf_fact_partials_bytes": (c_i64, [c_vp]),
     "ncf_randperm_workspace": (c_i64, [c_i64]),
     "ncf_randperm": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
-    "ncf_randperm_gather": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "ncf_build_rows": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, ctypes.c_int, c_vp, c_vp]),
     "ncf_user_order": (ctypes.c_int, [c_vp, c_i64, c_i64, ctypes.c_int, ctypes.c_int, c_vp, c_vp]),
     "ncf_uses_user_order": (ctypes.c_int, [c_vp]),

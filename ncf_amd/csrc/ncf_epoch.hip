@@ -29,10 +29,6 @@
 //   sorted order each step's predecessor is its left neighbour, and the last of
 //   each run is P(q).  Then one gather pass follows each chain to its root
 //   (a few hops: chains are ~log n long for MT19937 words; any input is correct).
-//   Since round 5 that pass walks the sorted order itself (step j = vs[t], its
-//   predecessor vs[t - 1] in the same run), so no per-step predecessor array is
-//   scattered first, and it can write the permuted epoch row (rows[A[j]]) instead of
-//   A[j] (ncf_randperm_gather: the grouping then reads the epoch in order).
 // * ncf_build_rows -- features_fill / labels_fill (datasets.py:65-69) packed
 //   (NCF_ROW_PACK): positives in file order, then positive p's num_ng negatives.
 #include <string.h>
@@ -71,15 +67,17 @@ __global__ __launch_bounds__(EP_THREADS) void fy_keys_kernel(const uint32_t* __r
     }
 }
 
-// Sorted by (H, j): P(q) = the last step of q's run (written in key order: the
-// stores of a wave fall on nearby q).
+// Sorted by (H, j): K[j] = left neighbour in the same run (-1 for the first),
+// P(q) = the run's last step.
 __global__ __launch_bounds__(EP_THREADS) void fy_runs_kernel(const uint32_t* __restrict__ ks,
                                                              const int32_t* __restrict__ vs, int64_t n,
-                                                             int32_t* __restrict__ P) {
+                                                             int32_t* __restrict__ P, int32_t* __restrict__ K) {
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
         const uint32_t q = ks[t];
         if (q == (uint32_t)n) continue;
-        if (t + 1 == n || ks[t + 1] != q) P[q] = vs[t];
+        const int j = vs[t];
+        K[j] = (t > 0 && ks[t - 1] == q) ? vs[t - 1] : -1;
+        if (t + 1 == n || ks[t + 1] != q) P[q] = j;
     }
 }
 
@@ -88,28 +86,13 @@ __device__ __forceinline__ int fy_root(const int32_t* __restrict__ P, int x) {
     return x;
 }
 
-// In sorted order: step j = vs[t] leaves at position j the root of its
-// predecessor's chain (vs[t - 1] in the same run), its own when H[j] = j (key n), or
-// H[j] itself as the first step into H[j].  A[j] = that value; with `rows`, the
-// epoch row rows[A[j]] is written to R[j] instead (A may be null then).
-__global__ __launch_bounds__(EP_THREADS) void fy_final_kernel(const uint32_t* __restrict__ ks,
-                                                              const int32_t* __restrict__ vs, int64_t n,
-                                                              const int32_t* __restrict__ P, int64_t* __restrict__ A,
-                                                              const uint64_t* __restrict__ rows,
-                                                              uint64_t* __restrict__ R) {
-    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-        const uint32_t q = ks[t];
-        const int j = vs[t];
-        int v;
-        if (q == (uint32_t)n) {
-            v = fy_root(P, j);
-        } else if (t > 0 && ks[t - 1] == q) {
-            v = fy_root(P, vs[t - 1]);
-        } else {
-            v = (int)q;
-        }
-        if (A) A[j] = v;
-        if (R) R[j] = rows[v];
+__global__ __launch_bounds__(EP_THREADS) void fy_final_kernel(const uint32_t* __restrict__ words, int64_t n,
+                                                              const int32_t* __restrict__ P,
+                                                              const int32_t* __restrict__ K, int64_t* __restrict__ A) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int h = fy_target(words, n, i);
+        const int x = h == i ? i : K[i];
+        A[i] = x < 0 ? h : fy_root(P, x);
     }
 }
 
@@ -130,7 +113,7 @@ __global__ __launch_bounds__(EP_THREADS) void build_rows_kernel(const int32_t* _
 
 struct FyLayout {
     uint32_t *keys, *keys_sorted;
-    int32_t *steps_sorted, *P, *K;  // K: unused since round 5 (the layout keeps its slot)
+    int32_t *steps_sorted, *P, *K;
     void* sort_tmp;
     size_t sort_bytes;
 };
@@ -171,36 +154,24 @@ int64_t ncf_randperm_workspace(int64_t n) {
     return 5 * al256e(n * 4) + al256e((int64_t)sb);
 }
 
-static int randperm_impl(const uint32_t* words, int64_t n, int64_t* perm, const uint64_t* rows, uint64_t* rows_out,
-                         void* workspace, int64_t workspace_bytes, hipStream_t st) {
-    if (!workspace || n <= 0 || n > 0x7fffffff) return NCF_E_ARG;
+int ncf_randperm(const uint32_t* words, int64_t n, int64_t* perm, void* workspace, int64_t workspace_bytes,
+                 void* stream) {
+    if (!perm || !workspace || n <= 0 || n > 0x7fffffff) return NCF_E_ARG;
     if (n > 1 && !words) return NCF_E_ARG;
     const int64_t need = ncf_randperm_workspace(n);
     if (need < 0 || workspace_bytes < need) return NCF_E_ARG;
     FyLayout F;
     if (!fy_layout(workspace, n, &F)) return NCF_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
     const unsigned g = ep_grid(n, 8192);
     hipLaunchKernelGGL(fy_keys_kernel, dim3(g), dim3(EP_THREADS), 0, st, words, n, F.keys, F.P);
     size_t sb = F.sort_bytes;
     if (rocprim::radix_sort_pairs(F.sort_tmp, sb, F.keys, F.keys_sorted, rocprim::counting_iterator<int32_t>(0),
                                   F.steps_sorted, (size_t)n, 0, fy_key_bits(n), st) != hipSuccess)
         return NCF_E_LAUNCH;
-    hipLaunchKernelGGL(fy_runs_kernel, dim3(g), dim3(EP_THREADS), 0, st, F.keys_sorted, F.steps_sorted, n, F.P);
-    hipLaunchKernelGGL(fy_final_kernel, dim3(g), dim3(EP_THREADS), 0, st, F.keys_sorted, F.steps_sorted, n, F.P, perm,
-                       rows, rows_out);
+    hipLaunchKernelGGL(fy_runs_kernel, dim3(g), dim3(EP_THREADS), 0, st, F.keys_sorted, F.steps_sorted, n, F.P, F.K);
+    hipLaunchKernelGGL(fy_final_kernel, dim3(g), dim3(EP_THREADS), 0, st, words, n, F.P, F.K, perm);
     return ep_status();
-}
-
-int ncf_randperm(const uint32_t* words, int64_t n, int64_t* perm, void* workspace, int64_t workspace_bytes,
-                 void* stream) {
-    if (!perm) return NCF_E_ARG;
-    return randperm_impl(words, n, perm, nullptr, nullptr, workspace, workspace_bytes, (hipStream_t)stream);
-}
-
-int ncf_randperm_gather(const uint32_t* words, int64_t n, const uint64_t* rows, uint64_t* rows_out, int64_t* perm,
-                        void* workspace, int64_t workspace_bytes, void* stream) {
-    if (!rows || !rows_out || rows == rows_out) return NCF_E_ARG;
-    return randperm_impl(words, n, perm, rows, rows_out, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 int ncf_build_rows(const int32_t* pos_users, const int32_t* pos_items, int64_t n_pos, const int32_t* neg, int num_ng,

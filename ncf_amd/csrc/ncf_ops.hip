@@ -756,7 +756,7 @@ __global__ __launch_bounds__(SH_THREADS) void shuffle_hist_kernel(const uint64_t
 #pragma unroll
     for (int k = 0; k < SH_UNROLL; ++k) {
         const int64_t j = j0 + k * SH_THREADS;
-        const int64_t s = j < n ? (perm ? perm[j] : j) : 0;
+        const int64_t s = j < n ? perm[j] : 0;
         src[k] = s < 0 ? 0 : (s >= n ? n - 1 : s);
     }
 #pragma unroll
@@ -765,7 +765,7 @@ __global__ __launch_bounds__(SH_THREADS) void shuffle_hist_kernel(const uint64_t
     for (int k = 0; k < SH_UNROLL; ++k) {
         const int64_t j = j0 + k * SH_THREADS;
         if (j < n) {
-            if (perm) shuf[j] = r[k];
+            shuf[j] = r[k];
             atomicAdd(hist + (j / B) * item_num + min(row_item(r[k]), item_num - 1), 1);
         }
     }
@@ -797,8 +797,7 @@ __global__ __launch_bounds__(SH2_THREADS) void shuffle_hist_lds_kernel(const uin
 #pragma unroll
         for (int k = 0; k < SH2_UNROLL; ++k) {
             const int q = q0 + k * SH2_THREADS + tid;
-            // perm null: the rows are the epoch in order already (ncf_randperm_gather)
-            const int64_t s = q < r1 ? (perm ? perm[b0 + q] : b0 + q) : b0;
+            const int64_t s = q < r1 ? perm[b0 + q] : 0;
             src[k] = s < 0 ? 0 : (s >= n ? n - 1 : s);
         }
 #pragma unroll
@@ -807,7 +806,7 @@ __global__ __launch_bounds__(SH2_THREADS) void shuffle_hist_lds_kernel(const uin
         for (int k = 0; k < SH2_UNROLL; ++k) {
             const int q = q0 + k * SH2_THREADS + tid;
             if (q < r1) {
-                if (perm) shuf[b0 + q] = r[k];
+                shuf[b0 + q] = r[k];
                 atomicAdd(&lh[min(row_item(r[k]), item_num - 1)], 1);
             }
         }
@@ -3027,19 +3026,13 @@ int ncf_prepare_epoch(const uint64_t* rows, const int64_t* perm, int64_t n, int6
 
 int ncf_prepare_epoch2(const uint64_t* rows, const int64_t* perm, int64_t n, int64_t batch_global, int item_num,
                        int flags, uint64_t* rows_out, void* workspace, int64_t workspace_bytes, void* stream) {
-    // perm null (since ABI 18): `rows` is the epoch stream in order already (ncf_randperm_gather)
-    if (!rows || !rows_out || !workspace || n < 0 || batch_global <= 0 || item_num <= 0) return NCF_E_ARG;
-    if (!perm && rows == rows_out) return NCF_E_ARG;
+    if (!rows || !perm || !rows_out || !workspace || n < 0 || batch_global <= 0 || item_num <= 0) return NCF_E_ARG;
     if (flags & ~NCF_PREP_CANONICAL) return NCF_E_ARG;
     if (batch_global > 0x7fffffff) return NCF_E_ARG;
     if (workspace_bytes < ncf_prepare_epoch_workspace(n, batch_global, item_num)) return NCF_E_ARG;
     if (n == 0) return NCF_OK;
     hipStream_t st = (hipStream_t)stream;
     if (batch_global < PREP_GROUP_MIN) {  // small batches: item runs ~1 row, grouping buys nothing
-        if (!perm)
-            return hipMemcpyAsync(rows_out, rows, (size_t)n * 8, hipMemcpyDeviceToDevice, st) == hipSuccess
-                       ? NCF_OK
-                       : NCF_E_LAUNCH;
         int64_t grid = (n + 255) / 256;
         if (grid > 8192) grid = 8192;
         hipLaunchKernelGGL(gather_epoch_kernel, dim3((int)grid), dim3(256), 0, st, rows, perm, n, rows_out);
@@ -3067,9 +3060,8 @@ int ncf_prepare_epoch2(const uint64_t* rows, const int64_t* perm, int64_t n, int
                        item_num, P, parts);
     if (ensure_lds(reinterpret_cast<const void*>(&sort_part_kernel), SORT_LDS) != NCF_OK) return NCF_E_LAUNCH;
     const int64_t g3 = P >= 8 ? ((nb + 7) / 8) * 8 * P : nb * P;
-    hipLaunchKernelGGL(sort_part_kernel, dim3((unsigned)g3), dim3(SORT_THREADS), (size_t)SORT_LDS, st,
-                       perm ? shuf : rows, hist, parts, n, batch_global, item_num, P, nb, rows_out,
-                       (flags & NCF_PREP_CANONICAL) ? 1 : 0);
+    hipLaunchKernelGGL(sort_part_kernel, dim3((unsigned)g3), dim3(SORT_THREADS), (size_t)SORT_LDS, st, shuf, hist,
+                       parts, n, batch_global, item_num, P, nb, rows_out, (flags & NCF_PREP_CANONICAL) ? 1 : 0);
     return launch_status();
 }
 

@@ -185,8 +185,7 @@ class EpochPrep:
         self.canonical = default_canonical() if canonical is None else bool(canonical)
 
     def __call__(self, rows, perm, batch_size, item_num, out=None):
-        """On the current stream; into `out` (n int64 on the device) if given.  perm None:
-        `rows` is the epoch in order already (ncf_randperm_gather)."""
+        """On the current stream; into `out` (n int64 on the device) if given."""
         n = rows.numel()
         need = int(L.hip().ncf_prepare_epoch_workspace(n, int(batch_size), int(item_num)))
         if need < 0:
@@ -199,8 +198,7 @@ class EpochPrep:
             out = self.out
         elif out.numel() != n or out.dtype != torch.int64 or not out.is_contiguous():
             raise ValueError("prepare_epoch out: n contiguous int64")
-        pp = None if perm is None else perm.data_ptr()  # None: rows already in epoch order
-        L.check(L.hip().ncf_prepare_epoch2(rows.data_ptr(), pp, n, int(batch_size), int(item_num),
+        L.check(L.hip().ncf_prepare_epoch2(rows.data_ptr(), perm.data_ptr(), n, int(batch_size), int(item_num),
                                            L.PREP_CANONICAL if self.canonical else 0, out.data_ptr(),
                                            self.ws.data_ptr(), self.ws.numel(), L.stream_ptr(self.device)),
                 "ncf_prepare_epoch2")

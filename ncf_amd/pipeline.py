@@ -226,15 +226,12 @@ class EpochPipeline:
         L.check(lib.ncf_build_rows(self.pu.data_ptr(), self.pi.data_ptr(), self.P,
                                    self._neg_dev[slot].data_ptr() if self.S else None, self.ng,
                                    self.rows.data_ptr(), st), "ncf_build_rows")
-        # the permutation applied in its own last pass: self.perm holds the epoch's rows
-        # in order (same size as the int64 permutation), which the grouping reads as is
-        L.check(lib.ncf_randperm_gather(self._words_dev[slot].data_ptr(), self.n, self.rows.data_ptr(),
-                                        self.perm.data_ptr(), None, self.fy_ws.data_ptr(), self.fy_ws.numel(), st),
-                "ncf_randperm_gather")
+        L.check(lib.ncf_randperm(self._words_dev[slot].data_ptr(), self.n, self.perm.data_ptr(),
+                                 self.fy_ws.data_ptr(), self.fy_ws.numel(), st), "ncf_randperm")
         staged.built = torch.cuda.Event(enable_timing=True)
         staged.built.record(stream)
         with torch.cuda.stream(stream):
-            self.prep(self.perm, None, self.batch_size, self.item_num, out=self._out[slot])
+            self.prep(self.rows, self.perm, self.batch_size, self.item_num, out=self._out[slot])
         staged.ready = torch.cuda.Event(enable_timing=True)
         staged.ready.record(stream)
         hook = self.on_built

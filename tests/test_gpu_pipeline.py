@@ -168,41 +168,3 @@ def test_engine_captures_every_pipeline_buffer_once():
     torch.cuda.synchronize()
     assert seen == {b.data_ptr() for b in pipe.buffers}
     assert np.isfinite(eng.epoch_losses()).all()
-
-
-@pytest.mark.parametrize("n,B,canon", [(1000, 256, False), (4970845, 65536, True), (4970845, 65536, False),
-                                       (300000, 2048, True)])
-def test_randperm_gather_and_grouping_without_perm(n, B, canon):
-    """ncf_randperm_gather (the permutation applied in its last pass) == rows[randperm],
-    its optional perm output == ncf_randperm; ncf_prepare_epoch2 with perm NULL on those
-    rows == with the permutation."""
-    import ncf_amd._lib as L
-    from ncf_amd import ops
-    from ncf_amd.pipeline import torch_words
-    rng = np.random.default_rng(n)
-    I = 3706
-    u, i = rng.integers(0, 6040, n), rng.integers(0, I, n)
-    y = (rng.random(n) < 0.2).astype(np.float32)
-    rows = torch.as_tensor(ops.pack_rows_host(u, i, y), device=DEV)
-    w = np.empty(max(1, n - 1), dtype=np.uint32)
-    torch_words(77, n - 1, w)
-    perm = _randperm(w, n).to(DEV)
-    words = torch.from_numpy(np.ascontiguousarray(w).view(np.int32)).to(DEV)
-    ws = torch.empty(int(L.hip().ncf_randperm_workspace(n)), dtype=torch.uint8, device=DEV)
-    out = torch.empty(n, dtype=torch.int64, device=DEV)
-    perm2 = torch.empty(n, dtype=torch.int64, device=DEV)
-    L.check(L.hip().ncf_randperm_gather(words.data_ptr(), n, rows.data_ptr(), out.data_ptr(), perm2.data_ptr(),
-                                        ws.data_ptr(), ws.numel(), L.stream_ptr()), "ncf_randperm_gather")
-    assert torch.equal(perm2, perm)
-    assert torch.equal(out, rows[perm])
-    prep = ops.EpochPrep(torch.device(DEV), canonical=canon)
-    a = prep(rows, perm, B, I).clone()
-    b = prep(out, None, B, I).clone()
-    if canon or B < 4096:
-        assert torch.equal(a, b)
-    else:  # arrival order inside an item run may differ: same rows per batch and item
-        nb = (n + B - 1) // B
-        for k in range(0, nb, max(1, nb // 7)):
-            sa = np.sort(a[k * B:(k + 1) * B].cpu().numpy())
-            sb = np.sort(b[k * B:(k + 1) * B].cpu().numpy())
-            assert np.array_equal(sa, sb), k
