@@ -996,6 +996,8 @@ class TrainEngine:
         if self.dp_mode == "sparse":  # bucket sizes go through the host every step
             return False
         if self.dp_mode == "owner":  # RCCL: both all-to-alls inside the step graph unless turned off
+            if getattr(self, "_owner_capture_failed", False):
+                return False
             default = "1" if D.capturable(self.grads, self.group) else "0"
             return os.environ.get("NCF_CAPTURE_ALLREDUCE", default) == "1"
         return os.environ.get("NCF_CAPTURE_ALLREDUCE", "0") == "1"
@@ -1025,7 +1027,20 @@ class TrainEngine:
         return self.num_batches if self.num_batches <= 128 else 32
 
     def capture(self):
-        """Capture the step into hipGraph(s) (after at least one eager step)."""
+        """Capture the step into hipGraph(s) (after at least one eager step).  dp_mode
+        "owner": if capturing the all-to-alls raises, the collectives go eager between
+        graphs from then on (a warning says so) instead of failing the run."""
+        if self.dp_mode == "owner" and self._capture_collective:
+            try:
+                return self._capture()
+            except RuntimeError as e:
+                import warnings
+                warnings.warn(f"owner exchange: capturing the all-to-alls failed ({e}); eager collectives")
+                self._owner_capture_failed = True
+                torch.cuda.synchronize(self.device)
+        return self._capture()
+
+    def _capture(self):
         if self._capture_collective:
             self._graph = (self._graph_of(self._step_body),)
             k = self.graph_steps

@@ -163,6 +163,17 @@ def _rccl_worker(port, dp_mode, q):
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1)
+    if dp_mode == "owner-fallback":  # the first capture (the one with the all-to-alls) raises
+        from ncf_amd.engine import TrainEngine
+        orig, calls = TrainEngine._graph_of, []
+
+        def failing(self, fn):
+            calls.append(1)
+            if len(calls) == 1:
+                raise RuntimeError("simulated capture failure")
+            return orig(self, fn)
+        TrainEngine._graph_of = failing
+        dp_mode = "owner"
     try:
         flat, losses = _run(1, 0, dist.group.WORLD, "NeuMF-end", 16, 3, True, dp_mode)
         q.put((flat, losses))
@@ -170,13 +181,14 @@ def _rccl_worker(port, dp_mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dp_mode", ["zero1", "allreduce", "touched", "owner"])
+@pytest.mark.parametrize("dp_mode", ["zero1", "allreduce", "touched", "owner", "owner-fallback"])
 def test_rccl_collective_captured_in_step_graph(dp_mode):
     """NCF_CAPTURE_ALLREDUCE=1 on backend nccl (RCCL): the gradient exchange is
     captured inside the step graphs.  One GPU holds one RCCL rank, so a one-rank
     group with an explicit dp_mode runs the real RCCL reduce-scatter / all-gather /
     all-reduce kernels through the captured graph; the result must equal the
-    single-process engine (no collective) to fp32 summation order."""
+    single-process engine (no collective) to fp32 summation order.  owner-fallback: the
+    capture with the all-to-alls raises; the engine continues with eager collectives."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_rccl_worker, args=(_free_port(), dp_mode, q))
