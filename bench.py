@@ -208,8 +208,23 @@ def adam_info(kt, eng, model, in_adam=False):
                                           "of lists A, B, C (every row on the epoch's last batch), the gradient read "
                                           "+ cleared (8 B) for list A's rows, the tower as ncf_reduce_adam_step",
                 "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}
+    if "ncf_owner_adam" in kt:
+        # dp_mode "owner": dense Adam on this rank's 1/W of the embedding rows (p, m, v read +
+        # written), the W received contributions read and the next slices' rows written
+        # (the two all-to-all buffers), the tower replicated
+        ms = kt["ncf_owner_adam"]
+        W = max(1, eng.world_size)
+        P = eng._ow_plan
+        xfer = 4 * W * (int(P.send_floats) + int(P.param_floats))
+        b = 24 * emb / W + xfer + 24 * tower
+        return {"kernel": "ncf_owner_adam (owned rows' dense Adam, tower Adam, next rows packed)",
+                "params": emb / W + tower, "bytes": b,
+                "bytes_detail": {"owned_adam": 24 * emb / W, "exchange_buffers": xfer, "tower_adam": 24 * tower},
+                "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}
     b = 32 * (emb + tower)
-    ms = kt["optimizer"]
+    ms = kt.get("optimizer")
+    if ms is None:  # an optimizer this accounting does not know: report the launch groups only
+        return {"kernel": "optimizer", "params": emb + tower, "launch_groups_ms": dict(kt)}
     return {"kernel": "ncf_adam_step", "params": emb + tower, "bytes": b, "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}
 
 
