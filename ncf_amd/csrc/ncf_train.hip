@@ -475,6 +475,9 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
     float um_[ANI], uv_[ANI], ug_[ANI], im_[ANI], iv_[ANI], ig_[ANI];
     auto raw4 = [&](int64_t off, f4& pp, f4& mm, f4& vv, f4& gg) {
         pp = *reinterpret_cast<const f4*>(prm + off);
+#ifdef NCF_AIS_NO_EMB_STATE  // timing experiment only (wrong results): no optimizer-state loads
+        return;
+#endif
         if constexpr (AIS) {
             mm = *reinterpret_cast<const f4*>(mrd + off);
             vv = *reinterpret_cast<const f4*>(vrd + off);
@@ -525,6 +528,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                 const int64_t oi = lay.ig + (int64_t)max(si[q], 0) * F + gf;
                 ugv[j] = prm[ou];
                 igv[j] = prm[oi];
+#ifndef NCF_AIS_NO_EMB_STATE
                 if constexpr (AIS) {
                     um_[j] = mrd[ou];
                     uv_[j] = vrd[ou];
@@ -533,6 +537,7 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
                     iv_[j] = vrd[oi];
                     ig_[j] = gread[oi];
                 }
+#endif
             }
         }
     };
