@@ -168,6 +168,11 @@ def adam_info(kt, eng, model, in_adam=False):
     slab_cols = stride
     if ops.fact_mode(lay):
         slab_cols = stride - (int(lay.b[0]) - int(lay.w[0]))  # W0's columns come from the partials
+    if "ncf_train_step_ais" in kt:  # in-step Adam: no optimizer launch of its own
+        return {"kernel": "in-step Adam inside ncf_train_step_ais (the previous step's update, on the fly for "
+                          "the launch's reads, written by its extra workgroups)", "params": emb + tower,
+                "bytes": 32 * (emb + tower), "ms": None,
+                "note": "no separate launch: the step's launch time is kernel_ms.ncf_train_step_ais"}
     if "ncf_reduce_adam_step" in kt:
         b = 32 * emb + 24 * tower + slab_rows * slab_cols * 4 + partial
         ms = kt["ncf_reduce_adam_step"]

@@ -914,7 +914,9 @@ class TrainEngine:
         """Run n_steps eager steps with HIP events between the launches (on the
         stream they run on) and return mean milliseconds per launch group."""
         st = torch.cuda.current_stream(self.device)
-        if self._fused_optimizer:
+        if self._ais_active:  # one launch per step: the previous step's Adam rides in it
+            parts = [("ncf_train_step_ais", self._train_launch)]
+        elif self._fused_optimizer:
             parts = [("ncf_train_step", self._train_launch),
                      ("ncf_lazy_adam_step" if self.lazy else "ncf_reduce_adam_step", self._reduce_adam)]
         else:
