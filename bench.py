@@ -233,6 +233,13 @@ def adam_info(kt, eng, model, in_adam=False):
     return {"kernel": "ncf_adam_step", "params": emb + tower, "bytes": b, "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}
 
 
+def _kname(n):
+    """Kernel name as the summaries key it: the fused step's template gained a trailing
+    AIS flag in round 5 (`..., NW, false>`), older summaries lack it -- both match."""
+    n = str(n)
+    return n[:-len(", false>")] + ">" if n.endswith(", false>") and "ncf_step_kernel<" in n else n
+
+
 def pmc_traffic(config, names):
     """HBM bytes per launch of `names` from the newest committed rocprofv3 PMC summary
     of THIS config (profiles/r*_prof_summary.json with "config" == config, written by
@@ -246,9 +253,9 @@ def pmc_traffic(config, names):
             continue
         if d.get("config") != config:
             continue
-        got = {k.get("kernel"): k.get("hbm_bytes_corrected") for k in d.get("kernels", [])}
-        if all(got.get(n) for n in names):
-            return float(sum(got[n] for n in names)), os.path.relpath(path, ROOT)
+        got = {_kname(k.get("kernel")): k.get("hbm_bytes_corrected") for k in d.get("kernels", [])}
+        if all(got.get(_kname(n)) for n in names):
+            return float(sum(got[_kname(n)] for n in names)), os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -759,7 +766,7 @@ def newest_profile(config, kernel_names):
         if d.get("config") != config:
             continue
         for k in d.get("kernels", []):
-            if k.get("kernel") == kernel_names[0] and k.get("mfma_busy_frac") is not None:
+            if _kname(k.get("kernel")) == _kname(kernel_names[0]) and k.get("mfma_busy_frac") is not None:
                 return float(k["mfma_busy_frac"]), os.path.relpath(path, ROOT)
     return None, None
 
