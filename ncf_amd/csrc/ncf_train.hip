@@ -1215,10 +1215,13 @@ __global__ __launch_bounds__(NW * WAVE, 2) void ncf_step_kernel(TrainArgs a) {
         // AIS: no slab -- the tower partials (and the loss at tower_len) are added into the
         // gradient buffer, which the next launch reads like the embedding rows
         auto put = [&](int64_t pos, float v) {
-            if constexpr (AIS)
+            if constexpr (AIS) {
+#ifndef NCF_AIS_NO_TOWER_ATOMICS  // timing experiment only (wrong results)
                 atomicAdd(grads + tb + pos, v);
-            else
+#endif
+            } else {
                 out[pos] = v;
+            }
         };
         const int l = l0, c = c0, g = g0;
         // layer-0 wgrad: this wave's 16-column block, already summed over the rows
