@@ -2396,7 +2396,7 @@ int ncf_train_step_ais(const ncf_layout* lay, float* params, float* grads, float
     a.ais = x;
     // the dense update over every active float by the workgroups past the training ones:
     // a few, so their bursts of loads do not queue ahead of the training workgroups'
-    // dependent round trips (NCF_AIS_EXTRA, default 64)
+    // dependent round trips (NCF_AIS_EXTRA, default 192)
     static const int extra_cap = [] {
         const char* e = getenv("NCF_AIS_EXTRA");
         const int v = e ? atoi(e) : 192;

@@ -160,6 +160,12 @@ class TrainEngine:
         epoch by ncf_forward) plus ncf_kd_feature_step for the feature terms."""
         self.model = model
         self.distill = distill
+        if process_group is None and int(world_size) > 1:
+            # no group given: the collectives run over the default group, so the
+            # owner all-gather and the stream agreement check must use it too
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                process_group = dist.group.WORLD
         self.world_size, self.rank, self.group = int(world_size), int(rank), process_group
         lay = L.layout(model.user_num, model.item_num, model.factor_num, model.num_layers, model.model_type)
         touched_ok = (optimizer == "adam" and model.factor_num % 4 == 0 and model.user_num <= (1 << 19)
@@ -478,8 +484,10 @@ class TrainEngine:
         ints = (int(plan.lists_bytes) + 3) // 4
         buf = self._ow_lists.get(key)
         if buf is None or buf.numel() < ints:
-            if buf is not None:  # a prebuild on the side stream may still write it: kept alive
-                self._ow_old.append(buf)
+            if buf is not None:  # work already queued may still use it: kept until it is done
+                ev = torch.cuda.Event()
+                ev.record()  # the current stream (the side stream inside a prebuild)
+                self._ow_old.append((buf, [ev], False))
             buf = self._ow_lists[key] = torch.zeros(ints, dtype=torch.int32, device=self.device)
         return buf
 
@@ -490,6 +498,7 @@ class TrainEngine:
         all hold the same stream.  One host read of the two maxima per epoch."""
         lib = L.hip()
         st = L.stream_ptr(self.device)
+        self._owner_retire()
         if self._ow_max is None:
             self._ow_max = torch.zeros(2, dtype=torch.int32, device=self.device)
         mu, mi = self._ow_M
@@ -522,6 +531,20 @@ class TrainEngine:
             mk = lambda n: torch.zeros(W * int(n), dtype=torch.float32, device=self.device)  # noqa: E731
             self._ow_bufs = (mk(plan.send_floats), mk(plan.send_floats), mk(plan.param_floats), mk(plan.param_floats))
             self._drop_graphs()
+
+    def _owner_retire(self):
+        """Free replaced list buffers once the work queued before their replacement is
+        done: an event from the stream that replaced them, one from this (the step)
+        stream at the first epoch boundary after it."""
+        keep = []
+        for buf, evs, main in self._ow_old:
+            if not main:
+                ev = torch.cuda.Event()
+                ev.record()
+                evs = evs + [ev]
+            if not all(e.query() for e in evs):
+                keep.append((buf, evs, True))
+        self._ow_old = keep
 
     def owner_bytes_per_step(self):
         """(sent, received) bytes of this rank per step in the two all-to-alls (the chunk

@@ -157,16 +157,29 @@ _CHECK_W = {}
 
 
 def stream_checksum(rows):
-    """Order-sensitive int64 checksum of a device epoch stream (one launch group, no
-    host sync): sum_k rows[k] * w_k (mod 2^64), w_k = odd hash of k."""
+    """Order-sensitive int64 checksum of a device epoch stream (a few launches per
+    chunk, no host sync): sum_k rows[k] * w_k (mod 2^64), w_k = (k * K) | 1.  Chunked:
+    w of a chunk at offset o is (j * K + o * K) | 1 from one cached chunk-sized j * K,
+    so no stream-length temporary is kept or allocated (C4: 99M rows)."""
     n = rows.numel()
-    key = (n, rows.device)
-    w = _CHECK_W.get(key)
-    if w is None:
-        w = (torch.arange(n, dtype=torch.int64, device=rows.device) * -7046029254386353131) | 1
+    K = -7046029254386353131
+    c = min(n, _CHECK_CHUNK)
+    key = (c, rows.device)
+    base = _CHECK_W.get(key)
+    if base is None:
+        base = torch.arange(c, dtype=torch.int64, device=rows.device) * K
         _CHECK_W.clear()
-        _CHECK_W[key] = w
-    return (rows * w).sum()
+        _CHECK_W[key] = base
+    total = torch.zeros((), dtype=torch.int64, device=rows.device)
+    for o in range(0, n, c):
+        m = min(c, n - o)
+        # o * K wraps in int64 like the device product does
+        ok = ((o * K + (1 << 63)) % (1 << 64)) - (1 << 63)
+        total += (rows[o:o + m] * ((base[:m] + ok) | 1)).sum()
+    return total
+
+
+_CHECK_CHUNK = 1 << 22
 
 
 class EpochPrep:

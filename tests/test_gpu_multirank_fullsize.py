@@ -95,6 +95,13 @@ def _c3w_run(world, rank, group):
     return _c3_run(world, rank, group, batch=B * world)
 
 
+def _c3n_run(world, rank, group):
+    """C3 with no process group handed to Trainer (its default): the engine must run its
+    owner all-gather and stream check over the default group (without it the
+    replicas kept stale rows after fit)."""
+    return _c3_run(world, rank, None)
+
+
 def _c4_stream(train, item_num, dev):
     """One epoch stream as the host path of Trainer._epoch_stream builds it:
     ng_sample (NumPy global stream), the DataLoader's permutation (torch global
@@ -138,7 +145,7 @@ def _c4l_run(world, rank, group):
 # what dp_mode "auto" resolves to (TrainEngine.auto_dp_mode)
 AUTO_EXPECT = {("c3", 2): "allreduce", ("c3", 4): "owner", ("c3", 8): "owner", ("c4", 2): "owner"}
 
-RUNS = {"c3": _c3_run, "c4": _c4_run, "c4l": _c4l_run, "c3w": _c3w_run}
+RUNS = {"c3": _c3_run, "c4": _c4_run, "c4l": _c4l_run, "c3w": _c3w_run, "c3n": _c3n_run}
 
 
 def _worker(rank, world, port, name, q, dp_mode=None):
@@ -224,7 +231,8 @@ def _oracle_losses(name, steps, batch=B):
 
 @pytest.mark.parametrize("name,world,dp_mode", [("c3", 2, None), ("c3", 4, None), ("c4", 2, None),
                                                  ("c3", 4, "zero1"), ("c4l", 2, "owner"), ("c4l", 4, "owner"),
-                                                 ("c3", 8, "owner"), ("c3", 8, None), ("c3w", 2, "owner")])
+                                                 ("c3", 8, "owner"), ("c3", 8, None), ("c3w", 2, "owner"),
+                                                 ("c3n", 2, "owner")])
 def test_full_shape_ranks_match_single_rank_and_oracle(name, world, dp_mode):
     """dp_mode None: the default ("auto"); "zero1" at C3: reduce-scatter, each rank
     expands the factored layer 0 of its own shard inside its Adam launch
@@ -239,7 +247,7 @@ def test_full_shape_ranks_match_single_rank_and_oracle(name, world, dp_mode):
     assert mode0 == want, mode0
     flat1, loss1, mode1 = _single_rank(name)[:3]
     assert mode1 == "single"
-    nb = {"c3": 76, "c4": 20, "c4l": 100, "c3w": 38}[name]
+    nb = {"c3": 76, "c4": 20, "c4l": 100, "c3w": 38, "c3n": 76}[name]
     assert len(loss0) == len(loss1) == nb
     batch = 2 * B if name == "c3w" else B
     ref = _oracle_losses(name, 20, batch)
