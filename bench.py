@@ -149,7 +149,7 @@ def cache_probe(eng, rows_n, reps=50):
     return out
 
 
-def adam_info(kt, eng, model, in_adam=False):
+def adam_info(kt, eng, model):
     """The optimizer launch and the bytes it moves.  Dense Adam over the embedding
     tables: 32 B/param (read p, g, m, v; write p, m, v, g = 0).  ncf_reduce_adam_step
     also reads the tower slab (ncf_reduce_rows rows: the fused step's workgroups, or
@@ -180,14 +180,6 @@ def adam_info(kt, eng, model, in_adam=False):
                "bytes_detail": {"embedding_adam": 32 * emb, "tower_adam": 24 * tower,
                                 "slab_read": slab_rows * slab_cols * 4, "w0_partials_read": partial},
                "ms": ms, "GB/s": b / (ms * 1e-3) / 1e9}
-        if in_adam:  # + the expansion: dW0 partials written and read back, dX / dW0 GEMMs
-            b += partial
-            dm = model.factor_num << (model.num_layers - 1)
-            out.update({"kernel": "ncf_reduce_adam_step (NCF_LAYOUT_FACT_IN_ADAM: factored expansion + slab "
-                                  "reduce + Adam, fact_reduce_adam_kernel)", "bytes": b,
-                        "GB/s": b / (ms * 1e-3) / 1e9,
-                        "expansion_flops": 4 * (model.user_num + model.item_num) * dm * dm})
-            out["bytes_detail"]["w0_partials_written"] = partial
         return out
     if "ncf_lazy_adam_step" in kt or "ncf_lazy_adam_step_packed" in kt:
         # deferred Adam: the rows of lists A, B, C per step (include/ncf_hip.h
@@ -878,16 +870,13 @@ def main():
     from ncf_amd import ops
     import ncf_amd._lib as L
     fact = ops.fact_mode(eng.lay)
-    # NCF_LAYOUT_FACT_IN_ADAM: the factored expansion runs inside the optimizer launch,
-    # so the step's launch group is the step kernel alone
-    in_adam = bool(int(eng.lay.flags) & L.LAYOUT_FACT_IN_ADAM)
     path = L.supported(mtype, f, nl)
     dm = f * 2 ** (nl - 1)
     rows_per_launch = per_gpu
     ms = kt["ncf_train_step_per_launch_b2b"]
     alg_flops = tower_flops_per_row(f, nl, mtype) * rows_per_launch
     alg_tf = alg_flops / (ms * 1e-3) / 1e12
-    xflops = executed_flops(f, nl, mtype, rows_per_launch, 0 if in_adam else U + I, fact, path == L.PATH_FUSED)
+    xflops = executed_flops(f, nl, mtype, rows_per_launch, U + I, fact, path == L.PATH_FUSED)
     executed_tf = xflops / (ms * 1e-3) / 1e12
     bytes_launch = gather_scatter_bytes_per_row(f, nl) * rows_per_launch
     achieved_gbs = bytes_launch / (ms * 1e-3) / 1e9
@@ -895,12 +884,10 @@ def main():
         mode = {"GMF": 0, "MLP": 1}.get(mtype, 2)
         waves = (8, 4, 2, 1)[(int(eng.lay.flags) >> L.LAYOUT_GEO_SHIFT) & L.LAYOUT_GEO_MASK]
         names = [f"ncf::ncf_step_kernel<{f}, {nl}, {mode}, false, {'true' if fact else 'false'}, {waves}>"]
-        if fact and not in_adam:
+        if fact:
             names.append(f"ncf::fact_expand_kernel<{dm}>")
         kname = (f"ncf_step_kernel<{f},{nl},{mtype.split('-')[0]},FACT={str(fact).lower()}>"
-                 + ((" (factored layer 0; its expansion GEMMs run in the optimizer launch, "
-                     f"fact_reduce_adam_kernel<{dm}>)" if in_adam else
-                     f" + fact_expand_kernel<{dm}> (factored layer 0)") if fact else " (per-row layer 0)")
+                 + (f" + fact_expand_kernel<{dm}> (factored layer 0)" if fact else " (per-row layer 0)")
                  + "; launch group timed back to back")
         traffic, traffic_src = pmc_traffic(args.config, names) if world == 1 else (None, None)
         busy, busy_src = newest_profile(args.config, names) if world == 1 else (None, None)
@@ -1011,7 +998,7 @@ def main():
                                       else "gather+scatter algorithmic bytes over all layered-path kernels")},
             "roofline_cache": roofline_cache,
             "kernel_ms": kt,
-            "adam": adam_info(kt, eng, model, in_adam),
+            "adam": adam_info(kt, eng, model),
             "quality": {"HR@10": hr10, "NDCG@10": ndcg10, "epochs_trained": round(eng.state_step() / eng.num_batches, 2),
                         "last_batch_loss": m["final_loss"]},
             "e2e": e2e,

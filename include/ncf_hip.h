@@ -21,7 +21,10 @@
 extern "C" {
 #endif
 
-/* 18: in-step Adam for small batches: ncf_ais_bufs, ncf_ais_supported, ncf_ais_begin,
+/* 19: NCF_LAYOUT_FACT_IN_ADAM (0x20) removed -- measured slower than the two launches it
+ * replaced; the bit is retired (NCF_LAYOUT_RETIRED_0X20: rejected by
+ * ncf_reduce_adam_step).
+ * 18: in-step Adam for small batches: ncf_ais_bufs, ncf_ais_supported, ncf_ais_begin,
  * ncf_train_step_ais, ncf_ais_bump, ncf_ais_flush.
  * 17: the owner-sharded sparse exchange (dp_mode "owner"): ncf_owner_plan,
  * ncf_owner_plan_init, ncf_owner_lists, ncf_owner_pack, ncf_owner_adam, ncf_owner_unpack;
@@ -32,7 +35,7 @@ extern "C" {
  * 15: ncf_layout.flags gains the fused step's workgroup geometry (NCF_LAYOUT_GEO_*) and
  * NCF_LAYOUT_FACT_DEFER_DX; new ncf_adam_step_fact, ncf_prepare_epoch2
  * (NCF_PREP_CANONICAL), ncf_probe_gather_scatter, ncf_debug_set_geometry. */
-#define NCF_ABI_VERSION 18
+#define NCF_ABI_VERSION 19
 
 #define NCF_OK 0
 #define NCF_E_UNSUPPORTED (-1) /* (model_type, factor_num, num_layers) has no compiled kernel */
@@ -92,14 +95,7 @@ typedef struct ncf_layout {
 #define NCF_LAYOUT_FACT_DEFER_DX 0x8 /* factored layer 0: the step forms only the dW0 partials and leaves the
                                         per-entity sums G in grads' Um / Im rows (ncf_adam_step_fact expands them
                                         per shard after the reduce-scatter); set by the caller, kept by tune */
-#define NCF_LAYOUT_FACT_IN_ADAM 0x20 /* factored layer 0 on the fused path, dm in {16, 32, 64}, single process
-                                       (since ABI 17): ncf_train_step leaves the per-entity sums G in grads' Um / Im
-                                       rows and ncf_reduce_adam_step forms dUm, dIm and dW0 itself and applies Adam
-                                       in the same launch (one launch fewer per step).  Set by the caller, kept by
-                                       tune; the train workspace must be zero-filled once before the first step (the
-                                       launch's counters live there and are left zero).  ncf_reduce_slab,
-                                       ncf_lazy_adam_step, ncf_touched_pack, ncf_owner_pack, ncf_adam_step_fact and
-                                       ncf_kd_feature_step refuse such a layout (NCF_E_ARG). */
+#define NCF_LAYOUT_RETIRED_0X20 0x20 /* was NCF_LAYOUT_FACT_IN_ADAM (ABI 17-18); rejected since ABI 19 */
 #define NCF_LAYOUT_USER_STORE 0x10  /* fused step (set by ncf_layout_tune when ncf_debug_set_user_store
                                        enables it; since ABI 16): the user-side embedding gradients of each
                                        row are stored plainly into the workspace and summed per user by a

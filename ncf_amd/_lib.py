@@ -29,7 +29,7 @@ NCF_E_ARG = -2
 NCF_E_LAUNCH = -3
 MODEL_GMF, MODEL_MLP, MODEL_NEUMF = 0, 1, 2
 DZ_BCE, DZ_DLOGIT, DZ_KD = 0, 1, 2
-ABI_VERSION = 18  # include/ncf_hip.h NCF_ABI_VERSION
+ABI_VERSION = 19  # include/ncf_hip.h NCF_ABI_VERSION
 PATH_FUSED, PATH_LAYERED = 1, 2  # ncf_supported()
 LAYOUT_PER_ROW_L0, LAYOUT_WG_SHIFT, LAYOUT_WG_MASK = 0x1, 8, 0xFFF  # ncf_layout.flags (ncf_layout_tune)
 LAYOUT_LAYERED = 0x2  # ncf_layout.flags: training on the layered path even where a fused kernel exists
@@ -38,7 +38,6 @@ PREP_CANONICAL = 0x1  # ncf_prepare_epoch2 flags: canonical row order inside ite
 PROBE_BLOCKS = 2048  # include/ncf_hip.h NCF_PROBE_BLOCKS (ncf_probe_gather_scatter's sink: x 256 floats)
 LAYOUT_FACT_DEFER_DX = 0x8  # ncf_layout.flags: factored step leaves G for ncf_adam_step_fact (sharded zero1)
 LAYOUT_USER_STORE = 0x10  # ncf_layout.flags (ncf_layout_tune): user-side gradients stored, summed per user
-LAYOUT_FACT_IN_ADAM = 0x20  # ncf_layout.flags: factored expansion inside ncf_reduce_adam_step (single process)
 MODEL_CODES = {"GMF": MODEL_GMF, "MLP": MODEL_MLP, "NeuMF-end": MODEL_NEUMF, "NeuMF-pre": MODEL_NEUMF}
 
 c_i64 = ctypes.c_int64

@@ -1916,14 +1916,6 @@ static int launch_fact_dx(const ncf_layout* lay, const float* w0snap, float* gsh
     return launch_fx(fe, lds, A, (int)(nb[0] + nb[1]), st);
 }
 
-// NCF_LAYOUT_FACT_IN_ADAM (ncf_fact_adam.inc): the expansion inside ncf_reduce_adam_step
-static int64_t fa_state_floats(const ncf_layout* lay);
-static bool fa_applies(const ncf_layout* lay);
-static int launch_fact_reduce_adam(const ncf_layout* lay, const void* workspace, float* params, float* grads,
-                                   float* exp_avg, float* exp_avg_sq, const int64_t* ranges, int nranges,
-                                   ncf_step_ctl* ctl, double lr, double beta1, double beta2, double eps,
-                                   float* loss_hist, int64_t hist_len, hipStream_t st);
-
 }  // namespace ncf
 
 using namespace ncf;
@@ -2056,7 +2048,7 @@ int ncf_supported(int mode, int F, int L) {
 // fused-path workspace: slab rows, [factored: dW0 partials, W0 snapshot], [user store]
 static int64_t us_base_floats(const ncf_layout* lay) {
     return (int64_t)SLAB_ROWS * ncf_slab_stride(lay) +
-           (fact_mode(lay) ? fact_partials_floats(lay) + fact_w0_snap_floats(lay) + fa_state_floats(lay) : 0);
+           (fact_mode(lay) ? fact_partials_floats(lay) + fact_w0_snap_floats(lay) : 0);
 }
 
 int64_t ncf_workspace_bytes(const ncf_layout* lay, int64_t rows) {
@@ -2172,7 +2164,7 @@ static int train_step_impl(const ncf_layout* lay, const float* params, float* gr
         rc = launch_status();
         if (rc != NCF_OK) return rc;
     }
-    if (!fact_mode(lay) || fa_applies(lay)) return rc;  // FACT_IN_ADAM: ncf_reduce_adam_step expands
+    if (!fact_mode(lay)) return rc;
     // factored layer 0: the per-user / per-item D0 sums -> dUm, dIm, dW0 partials
     return launch_fact_expand(lay, params, grads, fact_partials(lay, workspace), fact_w0_snap(lay, workspace),
                               (hipStream_t)stream);
@@ -2206,7 +2198,7 @@ namespace ncf {
 // The fused kernel with the in-step optimizer for this layout and its geometry, or null.
 static const void* ais_kernel(const ncf_layout* lay, int* geo) {
     const KernelEntry* e = train_fused(lay);
-    if (!e || fact_mode(lay) || us_on(lay) || fa_applies(lay)) return nullptr;
+    if (!e || fact_mode(lay) || us_on(lay)) return nullptr;
     const int g = train_geo(e, lay);
     *geo = g;
     return e->train_ais[g];
@@ -2446,7 +2438,7 @@ int ncf_kd_feature_step(const ncf_layout* student, const float* s_params, float*
                         int world, int rank, const float* gmf_w, const float* gmf_b, float gmf_coef,
                         const float* mlp_w, const float* mlp_b, float mlp_coef, void* workspace, void* stream) {
     if (!student || !s_params || !s_grads || !teacher || !t_params || !rows || !ctl || !workspace) return NCF_E_ARG;
-    if (batch_global <= 0 || world < 1 || rank < 0 || rank >= world || fa_applies(student)) return NCF_E_ARG;
+    if (batch_global <= 0 || world < 1 || rank < 0 || rank >= world) return NCF_E_ARG;
     KdFeatArgs a;
     memset(&a, 0, sizeof(a));
     a.sl = *student;
@@ -2520,7 +2512,7 @@ int ncf_forward(const ncf_layout* lay, const float* params, const uint64_t* rows
 int64_t ncf_slab_stride(const ncf_layout* lay) { return lay ? lay->tower_len + 64 : -1; }
 
 int ncf_reduce_slab(const ncf_layout* lay, const void* workspace, float* grads, ncf_step_ctl* ctl, void* stream) {
-    if (!lay || !workspace || !grads || fa_applies(lay)) return NCF_E_ARG;
+    if (!lay || !workspace || !grads) return NCF_E_ARG;
     const float* slab = static_cast<const float*>(workspace);
     const int stride = (int)ncf_slab_stride(lay);
     const int lo = slab_lo(lay);
@@ -2562,8 +2554,7 @@ int ncf_adam_step_fact(const ncf_layout* lay, const void* workspace, float* para
                        float* exp_avg, float* exp_avg_sq, const int64_t* ranges, int nranges, int64_t shard_begin,
                        float* grads_local, int64_t grads_n, ncf_step_ctl* ctl, double lr, double beta1, double beta2,
                        double eps, int64_t loss_slot, float* loss_hist, int64_t hist_len, void* stream) {
-    if (!lay || !workspace || !params || !gshard || !exp_avg || !exp_avg_sq || !ranges || !ctl || nranges <= 0 ||
-        fa_applies(lay))
+    if (!lay || !workspace || !params || !gshard || !exp_avg || !exp_avg_sq || !ranges || !ctl || nranges <= 0)
         return NCF_E_ARG;
     if (grads_n < 0 || (grads_n & 3) || (grads_n > 0 && !grads_local)) return NCF_E_ARG;
     const int dm = fact_dm(lay);
@@ -2690,9 +2681,7 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
                          float* exp_avg_sq, const int64_t* ranges, int nranges, ncf_step_ctl* ctl, double lr,
                          double beta1, double beta2, double eps, float* loss_hist, int64_t hist_len, void* stream) {
     if (!lay || !workspace || !params || !grads || !exp_avg || !exp_avg_sq || !ranges || !ctl) return NCF_E_ARG;
-    if (fa_applies(lay))
-        return launch_fact_reduce_adam(lay, workspace, params, grads, exp_avg, exp_avg_sq, ranges, nranges, ctl, lr,
-                                       beta1, beta2, eps, loss_hist, hist_len, (hipStream_t)stream);
+    if (lay->flags & NCF_LAYOUT_RETIRED_0X20) return NCF_E_UNSUPPORTED;
     int err = 0;
     Ranges R = make_ranges(ranges, nranges, &err);
     if (err) return NCF_E_ARG;
@@ -2850,7 +2839,7 @@ int ncf_lazy_adam_step(const ncf_layout* lay, const void* workspace, float* para
                        const int32_t* touched, int64_t n_total, int64_t batch_global, int32_t* last_step,
                        float* step_scalars, int64_t ring, void* stream) {
     if (!lay || !workspace || !params || !grads || !exp_avg || !exp_avg_sq || !ranges || !ctl || !touched ||
-        !last_step || !step_scalars || n_total <= 0 || batch_global <= 0 || ring < LZ_WIN + 2 || fa_applies(lay))
+        !last_step || !step_scalars || n_total <= 0 || batch_global <= 0 || ring < LZ_WIN + 2)
         return NCF_E_ARG;
     int err = 0;
     Ranges R = make_ranges(ranges, nranges, &err);
@@ -2896,8 +2885,7 @@ int64_t ncf_touched_packed_floats(const ncf_layout* lay, const int64_t* ranges, 
 int ncf_touched_pack(const ncf_layout* lay, const void* workspace, float* grads, const int64_t* ranges, int nranges,
                      const int32_t* touched, int64_t n_total, int64_t batch_global, const ncf_step_ctl* ctl,
                      float* packed, void* stream) {
-    if (!lay || !workspace || !grads || !ranges || !touched || !ctl || !packed || n_total <= 0 || batch_global <= 0 ||
-        fa_applies(lay))
+    if (!lay || !workspace || !grads || !ranges || !touched || !ctl || !packed || n_total <= 0 || batch_global <= 0 )
         return NCF_E_ARG;
     LazyArgs a;
     const int rc = lazy_args(lay, nullptr, grads, nullptr, nullptr, ranges, nranges, nullptr, nullptr, 1, &a);
@@ -3101,5 +3089,3 @@ int ncf_hr_ndcg(const float* logits, const int32_t* items, int64_t n, int batch,
 // dp_mode "owner" (ABI 17): the owner-sharded sparse exchange
 #include "ncf_owner.inc"
 
-// NCF_LAYOUT_FACT_IN_ADAM (ABI 17): the factored expansion inside the optimizer launch
-#include "ncf_fact_adam.inc"

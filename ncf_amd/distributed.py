@@ -2,8 +2,8 @@
 
 The reference is single-device; the build adds one strategy:
 every rank computes the same global stream from the same seeds and takes a
-contiguous shard of each global batch.  The gradient exchange has two forms
-(``TrainEngine(dp_mode=...)``):
+contiguous shard of each global batch.  The gradient exchange forms
+(``TrainEngine(dp_mode=...)``; "touched" is engine-side, ncf_touched_pack):
 
 * ``"zero1"`` (default for world > 1): the flat gradient bucket (dense
   embedding tables + tower + predict, zero padded to world x shard floats) is
@@ -12,13 +12,6 @@ contiguous shard of each global batch.  The gradient exchange has two forms
   are all-gathered in place.  Same bytes on the wire as one all-reduce, 1/W
   of the optimizer's HBM traffic and moment memory per rank.
 * ``"allreduce"``: one all-reduce of the flat gradient bucket, replicated Adam.
-* ``"sparse"``: the zero1 shards and shard Adam, but the embedding gradients go
-  to their owners as buckets of (row id, gradient row) of the rows this rank's
-  batch shard touched (``sparse_exchange``: one all-to-all of the bucket sizes,
-  then an all-to-all of ids and rows per table), summed there into the local
-  gradient buffer; the small dense tower / predict tail is all-reduced.  The
-  parameter all-gather stays dense: dense Adam moves every row every step.
-
 * ``"owner"``: embedding row id owned by rank id % W; the touched rows' gradients go
   to their owners and the rows each rank's next batch reads come back, two
   fixed-size all-to-alls per step (device kernels ncf_owner_*, engine.py);
@@ -111,16 +104,6 @@ def _coll_ok(t, group):
     return dist.get_backend(group) != "gloo" or t.device.type == "cpu"
 
 
-def _all_to_all(out, inp, out_splits, in_splits, group):
-    if _coll_ok(inp, group):
-        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
-        return out
-    o = out.cpu()
-    dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
-    out.copy_(o)
-    return out
-
-
 def _all_reduce(t, group):
     if _coll_ok(t, group):
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
@@ -129,60 +112,6 @@ def _all_reduce(t, group):
     dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
     t.copy_(h)
     return t
-
-
-def sparse_exchange(grads, tables, tail, shard, rank, world, group=None):
-    """Sum every rank's gradient of the rows in this rank's shard into grads.
-
-    grads:  this rank's flat gradient buffer (all tables, dense layout); on return
-            grads[rank*shard : (rank+1)*shard] holds the summed gradient (the rest
-            keeps this rank's own contributions and what it received).
-    tables: [(offset, width, n_rows, ids)] -- an embedding table at flat offset
-            `offset` with rows of `width` floats, and the sorted unique row ids this
-            rank's batch shard touched (its only nonzero gradient rows).
-    tail:   (begin, end) -- the dense tower / predict / loss floats, all-reduced.
-
-    A row goes to every rank whose shard its floats intersect (a row may straddle
-    two shards), except this rank.  Returns the bytes this rank sent."""
-    sent = 0
-    b, e = tail
-    if e > b:
-        _all_reduce(grads[b:e], group)
-        sent += 4 * (e - b)
-    dev = grads.device
-    plans = []
-    counts = torch.zeros(world, len(tables), dtype=torch.int64, device=dev)
-    for k, (off, w, nrows, ids) in enumerate(tables):
-        ids = ids.to(device=dev, dtype=torch.int64)
-        first = torch.div(off + ids * w, shard, rounding_mode="floor")
-        last = torch.div(off + ids * w + w - 1, shard, rounding_mode="floor")
-        span = last - first + 1
-        rid = torch.repeat_interleave(ids, span)
-        base = torch.repeat_interleave(first, span)
-        step = torch.arange(rid.numel(), device=dev) - torch.repeat_interleave(torch.cumsum(span, 0) - span, span)
-        own = base + step
-        keep = own != rank
-        rid, own = rid[keep], own[keep]
-        order = torch.argsort(own, stable=True)
-        rid, own = rid[order], own[order]
-        counts[:, k] = torch.bincount(own, minlength=world)
-        plans.append((off, w, nrows, rid))
-    recv_counts = torch.empty_like(counts)
-    _all_to_all(recv_counts.view(-1), counts.view(-1), [len(tables)] * world, [len(tables)] * world, group)
-    send_c, recv_c = counts.cpu().tolist(), recv_counts.cpu().tolist()  # split sizes for the collectives
-    for k, (off, w, nrows, rid) in enumerate(plans):
-        in_s = [send_c[d][k] for d in range(world)]
-        out_s = [recv_c[d][k] for d in range(world)]
-        table = grads[off:off + nrows * w].view(nrows, w)
-        rows = table[rid]
-        r_ids = torch.empty(sum(out_s), dtype=torch.int64, device=dev)
-        r_rows = torch.empty(sum(out_s), w, dtype=grads.dtype, device=dev)
-        _all_to_all(r_ids, rid, out_s, in_s, group)
-        _all_to_all(r_rows.view(-1), rows.reshape(-1), [c * w for c in out_s], [c * w for c in in_s], group)
-        if r_ids.numel():
-            table.index_add_(0, r_ids, r_rows)
-        sent += (8 + 4 * w) * sum(in_s)
-    return sent
 
 
 def capturable(t: torch.Tensor, group) -> bool:

@@ -10,14 +10,12 @@ with the all-reduce issued between them, see ``_capture_collective``):
                          train_neumf.py:111-114); on the factored path it also
                          launches the expansion (per-user/item sums -> dUm, dIm, dW0)
   2. ``ncf_reduce_slab`` per-workgroup tower grads -> flat grad buffer
-  3. world > 1, dp_mode "zero1" (default): RCCL reduce-scatter of the flat grad
-     buffer; dp_mode "sparse": the touched embedding rows as (id, row) buckets to
-     their owners + all-reduce of the dense tower tail; dp_mode "allreduce":
-     RCCL all-reduce of the flat grad buffer
+  3. world > 1, dp_mode "zero1": RCCL reduce-scatter of the flat grad buffer;
+     dp_mode "allreduce": RCCL all-reduce of the flat grad buffer
   4. ``ncf_adam_step``   dense Adam over the active parameters (zero1: of this
                          rank's shard only) + grad zeroing + loss bookkeeping
                          (train_neumf.py:90,115)
-  5. zero1 / sparse: RCCL all-gather of the updated parameter shards (in place)
+  5. zero1: RCCL all-gather of the updated parameter shards (in place)
 
 dp_mode "owner" (ncf_owner_* in include/ncf_hip.h): embedding row id is owned by
 rank id % W; per step train + ncf_owner_pack (this rank's gradient rows bucketed by
@@ -175,7 +173,7 @@ class TrainEngine:
                 if self.world_size > 1 else "single"
         # an explicit exchange mode stands at world 1 (a one-rank group still runs the
         # real collectives: how the captured-collective graph is tested on one GPU)
-        if dp_mode not in ("single", "zero1", "allreduce", "sparse", "touched", "auto", "owner"):
+        if dp_mode not in ("single", "zero1", "allreduce", "touched", "auto", "owner"):
             raise ValueError(f"dp_mode {dp_mode!r}")
         if dp_mode in ("touched", "auto", "owner") and not touched_ok:
             raise ValueError(f"dp_mode {dp_mode!r} needs Adam, factor_num % 4 == 0 and tables of <= 2^19 rows")
@@ -184,7 +182,7 @@ class TrainEngine:
         self.dp_mode = dp_mode
         # flat buffers padded to world x shard floats where the exchange shards them
         # (rank r owns [r*S, (r+1)*S)); "auto" pads too when its fallback would be zero1
-        shards = dp_mode in ("zero1", "sparse") or (
+        shards = dp_mode == "zero1" or (
             dp_mode == "auto" and self.default_dp_mode(int(lay.total)) == "zero1")
         self.shard = None
         n = int(lay.total)
@@ -202,7 +200,7 @@ class TrainEngine:
         n = self.flat.numel()
         self.grads = torch.zeros(n, dtype=torch.float32, device=dev)
         self.optimizer = optimizer
-        n_opt = D.shard_floats(int(lay.total), self.world_size) if dp_mode in ("zero1", "sparse") else n
+        n_opt = D.shard_floats(int(lay.total), self.world_size) if dp_mode == "zero1" else n
         if optimizer == "adam":
             self.exp_avg = torch.zeros(n_opt, dtype=torch.float32, device=dev)
             self.exp_avg_sq = torch.zeros(n_opt, dtype=torch.float32, device=dev)
@@ -217,7 +215,7 @@ class TrainEngine:
         self._nranges = len(rng)
         self._loss_slot = int(self.lay.loss_slot)
         self._opt_ptrs = (self.flat.data_ptr(), self.grads.data_ptr())
-        if dp_mode in ("zero1", "sparse"):
+        if dp_mode == "zero1":
             self._init_shards()
         self.loss_hist = torch.zeros(max_batches, dtype=torch.float32, device=dev)
         self.rows = None
@@ -256,14 +254,13 @@ class TrainEngine:
                                        dtype=torch.float32, device=dev)  # resized per batch size
 
     def _init_shards(self):
-        """zero1 / sparse: this rank's shard of the flat buffers, its active ranges,
+        """zero1: this rank's shard of the flat buffers, its active ranges,
         the loss slot's owner and the optimizer's pointers."""
-        model, dm_ = self.model, self.dp_mode
         S = self.shard = D.shard_floats(int(self.lay.total), self.world_size)
         r = self.rank
         assert self.flat.numel() >= S * self.world_size
         rng = [[self._ranges[2 * k], self._ranges[2 * k + 1]] for k in range(self._nranges)]
-        self.gshard = torch.zeros(S if dm_ == "zero1" else 0, dtype=torch.float32, device=self.device)
+        self.gshard = torch.zeros(S, dtype=torch.float32, device=self.device)
         # an empty [0, 0) range when no active parameter falls in the shard: the
         # launch still records the loss if this rank owns the loss slot
         srng = D.shard_ranges(rng, self.world_size, r, S) or [[0, 0]]
@@ -273,18 +270,6 @@ class TrainEngine:
         self.loss_owner = slot // S
         self._loss_slot = slot - r * S
         self._opt_ptrs = (self.flat.data_ptr() + 4 * r * S, self.gshard.data_ptr())
-        if dm_ == "sparse":  # the owner's summed shard gradient sits in the local buffer
-            self._opt_ptrs = (self.flat.data_ptr() + 4 * r * S, self.grads.data_ptr() + 4 * r * S)
-            lay = self.lay
-            f, dm = model.factor_num, model.factor_num << (model.num_layers - 1)
-            act = ops.active_mask(model)[:4]
-            if self.distill is not None and self.distill.active_extra is not None:
-                act = [a or b for a, b in zip(act, self.distill.active_extra[:4])]
-            self._sparse_tables = [(int(off), w, nrows, side) for (off, w, nrows, side), a in zip(
-                [(lay.ug, f, model.user_num, 0), (lay.ig, f, model.item_num, 1),
-                 (lay.um, dm, model.user_num, 0), (lay.im, dm, model.item_num, 1)], act) if a]
-            self._sparse_tail = (int(lay.tower_begin), int(lay.total))
-            self.sparse_bytes_sent = 0
         self._ag_scratch = None
 
     # ------------------------------------------------------------------ data
@@ -322,7 +307,6 @@ class TrainEngine:
             if os.environ.get("NCF_FORCE_LAYERED", "0") == "1":  # A/B: the layered path for any shape
                 self.lay.flags |= L.LAYOUT_LAYERED
             self._set_fact_shard()
-            self._set_fact_in_adam()
             self.ws = ops.new_workspace(self.lay, per, self.device)
         self.batch_size = int(batch_size)
         if self.num_batches > self.loss_hist.numel():
@@ -374,7 +358,6 @@ class TrainEngine:
             L.check(L.hip().ncf_user_order(rows.data_ptr(), n, self.batch_size, self.world_size,
                                            self.model.user_num, self._order_buf(rows).data_ptr(),
                                            L.stream_ptr(self.device)), "ncf_user_order")
-        self._hb = 0  # host copy of the batch index (the sparse exchange needs the batch's rows)
         if self.distill is not None:
             # the frozen teacher's logit for every row of the epoch stream (one
             # forward launch per epoch instead of one no_grad forward per step)
@@ -601,25 +584,6 @@ class TrainEngine:
             return  # an emulated world on a smaller group (scripts/dp_modes.py): timing only
         D.owner_gather_rows(self.flat, self._owner_tables(), self.world_size, self.rank, self.group)
 
-    def _set_fact_in_adam(self):
-        """Single-process Adam on the factored fused path (dm 16..64, e.g. C3): with
-        NCF_FACT_IN_ADAM=1 the expansion of the per-entity sums (dUm, dIm, dW0) runs
-        inside the optimizer launch (NCF_LAYOUT_FACT_IN_ADAM) -- one launch fewer per
-        step, but its in-launch hand-off of the dW0 partials measured slower than the
-        launch boundary it replaces (C3 optimizer 36 us against 7.4 + 9.3 us for
-        fact_expand + reduce_adam): off by default (A/B)."""
-        lay, m = self.lay, self.model
-        dm = m.factor_num << (m.num_layers - 1)
-        on = bool(self._fused_optimizer and self.distill is None and os.environ.get("NCF_LAZY_ADAM", "0") == "0"
-                  and os.environ.get("NCF_FACT_IN_ADAM", "0") == "1"
-                  and not (lay.flags & L.LAYOUT_LAYERED) and lay.dropout == 0.0
-                  and L.supported(m.model_type, m.factor_num, m.num_layers) == L.PATH_FUSED
-                  and dm in (16, 32, 64) and L.hip().ncf_fact_mode(ctypes.byref(lay)) == 1)
-        if on:
-            lay.flags |= L.LAYOUT_FACT_IN_ADAM
-        else:
-            lay.flags &= ~L.LAYOUT_FACT_IN_ADAM
-
     def _order_buf(self, rows):
         """The user-order buffer that goes with epoch-stream buffer `rows`."""
         key = (rows.data_ptr(), rows.numel())
@@ -731,37 +695,16 @@ class TrainEngine:
             D.allreduce_flat_grads(self._packed, self.group)
         elif self.dp_mode == "zero1":
             D.reduce_scatter_flat(self.gshard, self.grads, self.rank, self.group)
-        elif self.dp_mode == "sparse":
-            self._sparse_exchange()
         else:
             D.allreduce_flat_grads(self.grads, self.group)
 
-    def _touched(self):
-        """Sorted unique user and item ids of this rank's shard of the current batch."""
-        b = self._hb % self.num_batches
-        b0 = b * self.batch_size
-        lo, hi = D.shard_range(min(self.batch_size, self.n_total - b0), self.world_size, self.rank)
-        seg = self.rows[b0 + lo:b0 + hi]
-        u = seg & 0xFFFFFFFF
-        keep = u != 0xFFFFFFFF  # padding rows (user ~0, item 0x7FFFFFFF) touch nothing
-        return torch.unique(u[keep]), torch.unique(((seg >> 32) & 0x7FFFFFFF)[keep])
-
-    def _sparse_exchange(self):
-        """dp_mode "sparse": the touched rows' gradients to their owners, the dense
-        tower / predict / loss tail all-reduced (ncf_amd.distributed.sparse_exchange)."""
-        ids = self._touched()
-        tables = [(off, w, nrows, ids[side]) for off, w, nrows, side in self._sparse_tables]
-        self.sparse_bytes_sent += D.sparse_exchange(self.grads, tables, self._sparse_tail, self.shard, self.rank,
-                                                    self.world_size, self.group)
-        self._hb += 1
-
     def _allgather(self):
-        """Launch 5 (zero1, sparse): every rank's updated parameter shard to every rank;
+        """Launch 5 (zero1): every rank's updated parameter shard to every rank;
         owner: the rows of every rank's next batch to it, then unpacked."""
         if self.dp_mode == "owner":
             self._owner_a2a(1)
             self._owner_unpack()
-        elif self.dp_mode in ("zero1", "sparse"):
+        elif self.dp_mode == "zero1":
             if self._ag_scratch is None and not D._native_ok(self.flat, self.group):
                 self._ag_scratch = torch.empty_like(self.flat)
             D.all_gather_flat(self.flat, self.rank, self.shard, self.group, self._ag_scratch)
@@ -786,8 +729,8 @@ class TrainEngine:
                                                   self.LAZY_RING, self._packed.data_ptr(), st),
                                                   "ncf_lazy_adam_step_packed")
             return
-        if self.dp_mode in ("zero1", "sparse"):
-            if self.dp_mode == "zero1" and not self._fact_shard:
+        if self.dp_mode == "zero1":
+            if not self._fact_shard:
                 # the shard gradient is in gshard: clear the local bucket now (the
                 # factored launch below clears it itself)
                 L.check(lib.ncf_zero_f32(self.grads.data_ptr(), self.grads.numel(), st), "ncf_zero_f32")
@@ -813,8 +756,6 @@ class TrainEngine:
             L.check(lib.ncf_sgd_step(p, g, ranges, nr,
                                      self.ctl.data_ptr(), self.lr, self._loss_slot,
                                      hist, hist_len, st), "ncf_sgd_step")
-        if self.dp_mode == "sparse":  # the local bucket (own rows of other shards, received rows) for the next step
-            L.check(lib.ncf_zero_f32(self.grads.data_ptr(), self.grads.numel(), st), "ncf_zero_f32")
 
     @property
     def _fused_optimizer(self):
@@ -947,7 +888,7 @@ class TrainEngine:
                      ("ncf_reduce_slab", lambda: L.check(L.hip().ncf_reduce_slab(
                          ctypes.byref(self.lay), self.ws.data_ptr(), self.grads.data_ptr(), self.ctl.data_ptr(),
                          L.stream_ptr(self.device)), "ncf_reduce_slab")),
-                     ({"zero1": "reduce_scatter", "sparse": "sparse_exchange"}.get(self.dp_mode, "allreduce"),
+                     ("reduce_scatter" if self.dp_mode == "zero1" else "allreduce",
                       self._allreduce),
                      ("optimizer", self._optimize)]
             if self.dp_mode == "owner":  # the pack is part of _compute
@@ -957,7 +898,7 @@ class TrainEngine:
             if self.dp_mode == "touched":  # the pack is part of _compute
                 parts = [("ncf_train_step+ncf_touched_pack", self._compute), ("allreduce", self._allreduce),
                          ("ncf_lazy_adam_step_packed", self._optimize)]
-            if self.dp_mode in ("zero1", "sparse"):
+            if self.dp_mode == "zero1":
                 parts.append(("all_gather", self._allgather))
         acc = {k: 0.0 for k, _ in parts}
         evs = []
@@ -1018,8 +959,6 @@ class TrainEngine:
         the process group beyond a plain all_reduce (any backend)."""
         if self.dp_mode == "single":
             return True
-        if self.dp_mode == "sparse":  # bucket sizes go through the host every step
-            return False
         if self.dp_mode == "owner":  # RCCL: both all-to-alls inside the step graph unless turned off
             if getattr(self, "_owner_capture_failed", False):
                 return False
@@ -1207,7 +1146,7 @@ class TrainEngine:
         """Per-batch mean BCE of the last epoch (host copy).  zero1: the rank owning
         the loss slot recorded it; it is broadcast to the others (a collective: every
         rank calls this)."""
-        if self.dp_mode in ("zero1", "sparse"):
+        if self.dp_mode == "zero1":
             import torch.distributed as dist
             h = self.loss_hist[: self.num_batches].clone()
             if D._native_ok(h, self.group):

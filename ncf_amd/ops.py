@@ -253,7 +253,6 @@ def new_workspace(lay, rows, dev):
     need = int(L.hip().ncf_workspace_bytes(L.ctypes.byref(lay), int(rows)))
     if need < 0:
         raise ValueError("ncf_workspace_bytes failed")
-    # zero-filled: NCF_LAYOUT_FACT_IN_ADAM keeps its launch counters here (left zero)
     return torch.zeros((need + 3) // 4, dtype=torch.float32, device=dev)
 
 

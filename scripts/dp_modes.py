@@ -36,9 +36,9 @@ def main():
     rows = pipe.next_epoch(peek_eval_draw=False)
     res = {}
     for mode in modes:
-        # zero1 / sparse at an emulated world over a one-rank group: the collectives in
+        # zero1 at an emulated world over a one-rank group: the collectives in
         # their exact all-reduce forms (ncf_amd.distributed, NCF_DP_EMULATE)
-        os.environ["NCF_DP_EMULATE"] = "1" if mode in ("zero1", "sparse") else "0"
+        os.environ["NCF_DP_EMULATE"] = "1" if mode == "zero1" else "0"
         torch.manual_seed(0)
         model, _ = bench.build_model(cfg, ds["user_num"], ds["item_num"], dev)
         eng = TrainEngine(model, lr=1e-3, world_size=world, rank=0, process_group=dist.group.WORLD, dp_mode=mode)

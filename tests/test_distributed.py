@@ -194,143 +194,6 @@ def test_gloo_zero1_matches_single_process_adam(world, emulate):
 
 
 # ---------------------------------------------------------------------------
-# sparse: zero1 shards, but embedding gradients travel as (row id, row) buckets to
-# their owners (ncf_amd.distributed.sparse_exchange; TrainEngine(dp_mode="sparse"))
-
-def _tables_of(sizes, widths, touched):
-    """[(offset, width, rows, ids)] of consecutive tables in a flat buffer."""
-    out, off = [], 0
-    for (n, w), ids in zip(zip(sizes, widths), touched):
-        out.append((off, w, n, torch.as_tensor(np.unique(ids), dtype=torch.int64)))
-        off += n * w
-    return out, off
-
-
-def _sparse_exact_worker(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    from ncf_amd.distributed import reduce_scatter_flat, shard_floats, sparse_exchange
-    rng = np.random.default_rng(100 + rank)
-    sizes, widths = [37, 53, 37, 53], [8, 8, 24, 24]       # ug, ig, um, im (rows straddle shards)
-    tail_n = 101
-    touched = [rng.integers(0, n, 20) for n in sizes[:2]]
-    touched = touched + touched  # the MLP tables share the GMF tables' rows (same users / items)
-    tables, emb = _tables_of(sizes, widths, touched)
-    n = emb + tail_n
-    S = shard_floats(n, world, align=4)
-    g = torch.zeros(S * world)
-    for off, w, rows, ids in tables:  # integer gradients on the touched rows only: sums are exact
-        g[off:off + rows * w].view(rows, w)[ids] = torch.as_tensor(rng.integers(-50, 50, (len(ids), w)),
-                                                                    dtype=torch.float32)
-    g[emb:n] = torch.as_tensor(rng.integers(-50, 50, tail_n), dtype=torch.float32)
-    dense = torch.zeros(S)
-    reduce_scatter_flat(dense, g.clone(), rank)
-    sent = sparse_exchange(g, tables, (emb, n), S, rank, world)
-    q.put((rank, dense.numpy(), g[rank * S:(rank + 1) * S].numpy().copy(), sent, 4 * S * world))
-    dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_sparse_exchange_equals_dense_reduce_scatter(world):
-    """Integer gradients on random touched rows (exact fp32 sums): every owner's
-    shard after the sparse exchange is bit-identical to the dense reduce-scatter,
-    and the exchange sends fewer bytes."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = 31500 + (os.getpid() % 1000) + 10 * world
-    procs = [ctx.Process(target=_sparse_exact_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=120) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    for rank, dense, sparse, sent, dense_bytes in res:
-        assert np.array_equal(dense, sparse), rank
-        assert sent < dense_bytes
-
-
-def _sparse_adam_worker(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    from oracle import ncf_oracle as O
-    from ncf_amd.distributed import all_gather_flat, shard_floats, shard_range, sparse_exchange
-    torch.manual_seed(5)
-    m = O.OracleNCF(40, 60, 8, 3, 0.0, "NeuMF-end")
-    params = list(m.parameters())
-    n = sum(p.numel() for p in params)
-    S = shard_floats(n, world)
-    flat = torch.zeros(S * world)
-    flat[:n] = torch.cat([p.detach().reshape(-1) for p in params])
-    shard = torch.nn.Parameter(flat[rank * S:(rank + 1) * S].clone())
-    opt = torch.optim.Adam([shard], lr=1e-2)
-    rng = np.random.default_rng(2)
-    B = 257
-    sizes = [40, 60, 40, 60]
-    widths = [8, 8, 32, 32]
-    emb = sum(a * b for a, b in zip(sizes, widths))
-    for _ in range(3):
-        u, i = rng.integers(0, 40, B), rng.integers(0, 60, B)
-        y = (rng.random(B) < 0.3).astype(np.float32)
-        off = 0
-        with torch.no_grad():
-            for p in params:
-                p.copy_(flat[off:off + p.numel()].view_as(p))
-                off += p.numel()
-        m.zero_grad()
-        lo, hi = shard_range(B, world, rank)
-        logit = m(torch.as_tensor(u[lo:hi]), torch.as_tensor(i[lo:hi]))
-        loss = torch.nn.functional.binary_cross_entropy_with_logits(logit, torch.as_tensor(y[lo:hi]),
-                                                                    reduction="sum") / B
-        loss.backward()
-        g = torch.zeros(S * world)
-        g[:n] = torch.cat([p.grad.reshape(-1) for p in params])
-        tables, _ = _tables_of(sizes, widths, [u[lo:hi], i[lo:hi], u[lo:hi], i[lo:hi]])
-        sparse_exchange(g, tables, (emb, n), S, rank, world)
-        shard.grad = g[rank * S:(rank + 1) * S].clone()
-        opt.step()
-        with torch.no_grad():
-            flat[rank * S:(rank + 1) * S].copy_(shard)
-        all_gather_flat(flat, rank, S)
-    q.put((rank, flat[:n].numpy().copy()))
-    dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_sparse_matches_single_process_adam(world):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = 32500 + (os.getpid() % 1000) + 10 * world
-    procs = [ctx.Process(target=_sparse_adam_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=120) for _ in procs], key=lambda t: t[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    for _, f in res[1:]:
-        assert np.array_equal(f, res[0][1]), "ranks hold different parameters after the all-gather"
-    from oracle import ncf_oracle as O
-    torch.manual_seed(5)
-    m = O.OracleNCF(40, 60, 8, 3, 0.0, "NeuMF-end")
-    opt = torch.optim.Adam(m.parameters(), lr=1e-2)
-    rng = np.random.default_rng(2)
-    B = 257
-    for _ in range(3):
-        u, i = rng.integers(0, 40, B), rng.integers(0, 60, B)
-        y = (rng.random(B) < 0.3).astype(np.float32)
-        opt.zero_grad()
-        loss = torch.nn.functional.binary_cross_entropy_with_logits(m(torch.as_tensor(u), torch.as_tensor(i)),
-                                                                    torch.as_tensor(y))
-        loss.backward()
-        opt.step()
-    ref = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).numpy()
-    np.testing.assert_allclose(res[0][1], ref, rtol=1e-4, atol=1e-6)
-
-
-# ---------------------------------------------------------------------------
 # owner: row id owned by rank id % W; gradient rows to their owners, the next batch's
 # rows back to their readers (TrainEngine(dp_mode="owner"), include/ncf_hip.h
 # ncf_owner_*).  The protocol on CPU tensors, with the lists of tests/owner_model.py.

@@ -108,9 +108,6 @@ def _free_port():
                                                        ("NeuMF-end", 32, 3, True, "touched"),
                                                        ("NeuMF-end", 16, 3, True, "auto"),
                                                        ("NeuMF-end", 16, 3, False, "allreduce"),
-                                                       ("NeuMF-end", 16, 3, True, "sparse"),
-                                                       ("NeuMF-end", 16, 3, False, "sparse"),
-                                                       ("GMF", 16, 3, True, "sparse"),
                                                        ("NeuMF-end", 32, 3, True, "zero1"),
                                                        ("GMF", 16, 3, True, "zero1"),
                                                        ("NeuMF-end", 16, 3, True, "auto-zero1"),

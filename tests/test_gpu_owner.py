@@ -72,27 +72,37 @@ def test_owner_lists_random_stream(W):
         _check(rows, n, B, W, me, U, I)
 
 
+_C4_HEAD = {}
+
+
+def _c4_head():
+    """The first 12 global batches of a C4 epoch stream (built once per session)."""
+    if not _C4_HEAD:
+        from ncf_amd import ops, synthetic
+        from ncf_amd.data import NCFData, epoch_permutation
+        ds = synthetic.make_dataset("ml-20m", seed=0)
+        U, I = ds["user_num"], ds["item_num"]
+        train = NCFData(np.stack([ds["train_users"], ds["train_items"]], 1), I, None, 4, True)
+        np.random.seed(0)
+        torch.manual_seed(0)
+        train.ng_sample()
+        u, i, y = train.arrays()
+        B = 65536
+        perm = epoch_permutation(len(u)).to(DEV)
+        d = torch.from_numpy(ops.pack_rows_host(u, i, y)).to(DEV)
+        stream = ops.EpochPrep(torch.device(DEV), canonical=True)(d, perm, B, int(I))
+        n = 12 * B
+        _C4_HEAD.update(rows=stream[:n].cpu().numpy().view(np.uint64), n=n, B=B, U=U, I=I)
+    return _C4_HEAD
+
+
 @pytest.mark.parametrize("W", [2, 8])
 def test_owner_lists_c4_stream(W):
     """The first 12 global batches of a C4 epoch stream (ml-20m ids, grouped by item,
     canonical) -- the bench's multi-GPU stress config."""
-    from ncf_amd import ops, synthetic
-    from ncf_amd.data import NCFData, epoch_permutation
-    ds = synthetic.make_dataset("ml-20m", seed=0)
-    U, I = ds["user_num"], ds["item_num"]
-    train = NCFData(np.stack([ds["train_users"], ds["train_items"]], 1), I, None, 4, True)
-    np.random.seed(0)
-    torch.manual_seed(0)
-    train.ng_sample()
-    u, i, y = train.arrays()
-    B = 65536
-    perm = epoch_permutation(len(u)).to(DEV)
-    d = torch.from_numpy(ops.pack_rows_host(u, i, y)).to(DEV)
-    stream = ops.EpochPrep(torch.device(DEV), canonical=True)(d, perm, B, int(I))
-    n = 12 * B
-    rows = stream[:n].cpu().numpy().view(np.uint64)
+    h = _c4_head()
     for me in (0, W - 1):
-        _check(rows, n, B, W, me, U, I)
+        _check(h["rows"], h["n"], h["B"], W, me, h["U"], h["I"])
 
 
 def test_owner_lists_truncate_and_report():
@@ -133,7 +143,7 @@ def test_one_rank_owner_engine_equals_single(mt, f, nl, use_graph):
     (p1, l1, m1), (p2, l2, m2) = out
     assert m1 == "single" and m2 == "owner"
     # the same dense Adam on one contribution per row; the single-process engine's
-    # factored expansion sums W0's block partials in another order (FACT_IN_ADAM) and the
+    # factored expansion sums W0's block partials in another order and the
     # step's float atomics vary in the last bits between runs
     np.testing.assert_allclose(l2, l1, rtol=1e-6)
     np.testing.assert_allclose(p2, p1, rtol=1e-4, atol=1e-6)
