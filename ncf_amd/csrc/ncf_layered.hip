@@ -1672,6 +1672,8 @@ __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float
     }
 }
 
+#include "ncf_chain_wide.inc"
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1764,6 +1766,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
     // gradients in one launch); D_0 in Da, D_1 .. D_{L-1} packed into Db
     ChainBufs cb;
     bool chained = false;
+    bool wide = false;  // the wide chain (dm 512): D_0 in row order, scatter0 does items / users / db_0
     if (fact && vec && !drop) {
         // H_L feeds nothing after the chain (the predict layer is in it): not stored
         for (int k = 0; k < 5; ++k) cb.H[k] = (k >= 1 && k < L) ? H[k] : nullptr;
@@ -1781,6 +1784,10 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
                 if (lyr_launch_proj(&lay, a.params, Pj, a.zero_p, 4 * a.zero_n4, st) != NCF_OK) return NCF_E_LAUNCH;
                 if (vec && !drop && launch_step_chain(a, Pj, cb, R, st)) {
                     chained = true;
+                    break;
+                }
+                if (vec && !drop && launch_wide_chain(a, Pj, cb, R, st)) {
+                    chained = wide = true;
                     break;
                 }
                 int64_t g0 = (R * (DM / 4) + GNT - 1) / GNT;
@@ -1823,7 +1830,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             bm.start[i + 1] = bm.start[i] + (int)(bm.gx[i] * bm.gy[i] * splits);
         }
         int walk = 0;
-        if (a.uorder) {  // the user-order walk of D_0 rides in the same launch
+        if (a.uorder && !wide) {  // the user-order walk of D_0 rides in the same launch
             const int64_t per_block = (int64_t)(GNT / DM) * SC_ROWS;
             walk = (int)((R + per_block - 1) / per_block);
             bm.D0u = cb.D[0];
@@ -1837,11 +1844,11 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
         // the full scatter
 #define NCF_L0(DD)                           \
     case DD:                                 \
-        if (!a.uorder)                       \
+        if (!a.uorder || wide)               \
             launch_scatter0<DD>(a, cb.D[0], R, st);  \
         break;
         switch (DM) {
-            NCF_L0(8) NCF_L0(16) NCF_L0(32) NCF_L0(64) NCF_L0(128)
+            NCF_L0(8) NCF_L0(16) NCF_L0(32) NCF_L0(64) NCF_L0(128) NCF_L0(256) NCF_L0(512)
             default: return NCF_E_UNSUPPORTED;
         }
 #undef NCF_L0
