@@ -1694,6 +1694,8 @@ int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train, in
         fl += rup64(fact_part_floats) + rup64(((int64_t)lay->user_num + lay->item_num) * DM);
     for (int k = 1; k <= lay->num_layers; ++k) fl += rup64(rows * ((2 * DM) >> k));
     if (train) fl += 2 * rup64(rows * DM);
+    if (train && fact_part_floats >= 0 && DM == wc::DM && lay->num_layers == wc::L)
+        fl += rup64((int64_t)wc::NCH * wc::CHUNK / 4);  // the wide chain's weight chunk images
     return fl;
 }
 
@@ -1751,6 +1753,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             Da = ws + off;
             off += rup64(R * DM);
             Db = ws + off;
+            off += rup64(R * DM);
         }
     }
     // the slab is cleared by the step's first kernel (the projection or the first
@@ -1786,7 +1789,8 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
                     chained = true;
                     break;
                 }
-                if (vec && !drop && launch_wide_chain(a, Pj, cb, R, st)) {
+                if (vec && !drop && DM == wc::DM && L == wc::L &&
+                    launch_wide_chain(a, Pj, cb, reinterpret_cast<char*>(ws + off), R, st)) {
                     chained = wide = true;
                     break;
                 }
