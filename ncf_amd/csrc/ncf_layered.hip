@@ -396,6 +396,104 @@ __device__ __forceinline__ void gemm_block_x6s(int64_t kbeg, int64_t kend, GA ga
     ep(acc, wm, wn, l);
 }
 
+// gemm_block_x6w: the split core on a 128 x 128 block tile, each of the 4 waves a 64 x 64
+// quadrant (4 x 4 MFMA tiles).  The x6s core's waves own 32 x 32 quadrants: per K step a
+// wave splits 4 fragments (three bf16 planes each, ~40 VALU per fragment) for 24 MFMAs,
+// and a wave64 VALU instruction occupies the SIMD 4 cycles -- ~960 VALU cycles against
+// 384 MFMA cycles, so the split sets the time (SQ: 10 VALU per MFMA instruction in the
+// weight-gradient launch, MFMA busy 0.21).  Here a wave splits 8 fragments for 96 MFMAs.
+// Same planes, products, product order and K order per output element as x6s (the
+// outputs are bitwise the same for the same K range).  LDS: 2 x (128 + 128) x 32 fp32
+// = 64 KB, dynamic (X6W_LDS bytes; launchers set the attribute).  The epilogue gets
+// acc[4][4] and the wave's quadrant origin (wm, wn) in {0, 64}.
+constexpr int X6W_TB = 128;
+constexpr int X6W_LDS = 2 * 2 * X6W_TB * XBK * 4;
+
+template <bool KC, int TB, class G>
+__device__ __forceinline__ void x6w_load(G g, int64_t k0, int t, f4 (&v)[TB / 32]) {
+#pragma unroll
+    for (int h = 0; h < TB / 32; ++h) {
+        const int q = t + 256 * h;
+        v[h] = KC ? g(q >> 3, k0 + 4 * (q & 7)) : g(4 * (q % (TB / 4)), k0 + q / (TB / 4));
+    }
+}
+// (A register-transposed form for !KC -- four consecutive k rows per thread stored as f4
+// along k -- removed the weight-gradient launch's 17M LDS bank-conflict cycles but ran
+// 164.5 -> 194.8 us: profiles/r06_evidence/gemm_tile_ab/.)
+template <bool KC, int TB>
+__device__ __forceinline__ void x6w_store(float* S, int t, const f4 (&v)[TB / 32]) {
+#pragma unroll
+    for (int h = 0; h < TB / 32; ++h) {
+        const int q = t + 256 * h;
+        if constexpr (KC) {
+            *reinterpret_cast<f4*>(S + x6s_addr(q >> 3, 4 * (q & 7))) = v[h];
+        } else {
+            const int k = q / (TB / 4), mn = 4 * (q % (TB / 4));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) S[x6s_addr(mn + i, k)] = lane_get(v[h], i);
+        }
+    }
+}
+
+template <bool AKC, bool BKC, class GA, class GB, class EP, class SA = NoHook>
+__device__ __forceinline__ void gemm_block_x6w(int64_t kbeg, int64_t kend, GA ga4, GB gb4, EP ep, SA sa = SA{}) {
+    constexpr int TB = X6W_TB, NH = TB / 32;
+    extern __shared__ __attribute__((aligned(16))) float x6w_sm[];
+    float* As = x6w_sm;                  // [2][TB * XBK]
+    float* Bs = x6w_sm + 2 * TB * XBK;   // [2][TB * XBK]
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+    const X6Swap<GB> gbs{gb4};
+    f4 ra[NH], rb[NH];
+    auto load = [&](int64_t k0) {
+        x6w_load<AKC, TB>(ga4, k0, t, ra);
+        x6w_load<BKC, TB>(gbs, k0, t, rb);
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int h = 0; h < NH; ++h) sa(ra[h]);
+        x6w_store<AKC, TB>(As + buf * TB * XBK, t, ra);
+        x6w_store<BKC, TB>(Bs + buf * TB * XBK, t, rb);
+    };
+    f4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    load(kbeg);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t k0 = kbeg; k0 < kend; k0 += XBK) {
+        const bool more = k0 + XBK < kend;
+        if (more) load(k0 + XBK);
+        const float* Ab = As + buf * TB * XBK;
+        const float* Bb = Bs + buf * TB * XBK;
+        bf16x8 fa[4][3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x6s_frag(Ab, wm + 16 * i + (l & 15), l, fa[i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            bf16x8 fb[3];
+            x6s_frag(Bb, wn + 16 * j + (l & 15), l, fb);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                f4 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[1], c, 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[0], c, 0, 0, 0);
+            }
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    ep(acc, wm, wn, l);
+}
+
 // The GEMM core of the layered kernels' 16-byte loader path: the bf16 split core, or
 // (-DNCF_GEMM_F32, the A/B library variant) the f32-MFMA core.  (A variant that split
 // once per block into three bf16 plane images in LDS -- 48 KB per block, 3 blocks per
@@ -407,6 +505,16 @@ __device__ __forceinline__ void gemm_block_vx(int64_t kbeg, int64_t kend, GA ga4
 #else
     gemm_block_x6s<AKC, BKC>(kbeg, kend, ga4, gb4, ep, sa);
 #endif
+}
+
+// TB = 64: gemm_block_vx; TB = X6W_TB: the 128 x 128 split core (dynamic LDS X6W_LDS)
+template <int TB, bool AKC, bool BKC, class GA, class GB, class EP, class SA = NoHook>
+__device__ __forceinline__ void gemm_tile(int64_t kbeg, int64_t kend, GA ga4, GB gb4, EP ep, SA sa = SA{}) {
+    static_assert(TB == 64 || TB == X6W_TB, "block tile");
+    if constexpr (TB == X6W_TB)
+        gemm_block_x6w<AKC, BKC>(kbeg, kend, ga4, gb4, ep, sa);
+    else
+        gemm_block_vx<AKC, BKC>(kbeg, kend, ga4, gb4, ep, sa);
 }
 
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
@@ -581,17 +689,19 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_data_kernel(LyrArgs a, int k, con
 //   db_k[j]    += sum_m dY_k[m][j]             (the extra column c = s_k of ones)
 // into the slab (tower partials, reduced by ncf_reduce_slab).
 // grid (ceil(J/64), ceil((s_k+1)/64), splits).
-template <bool FIRST, bool DROP, bool VEC>
+template <bool FIRST, bool DROP, bool VEC, int TB = 64>
 __device__ __forceinline__ void bwd_w_body(const LyrArgs& a, int k, const float* __restrict__ D,
                                            const float* __restrict__ Ain, int64_t R, int64_t chunk, int bx, int by,
                                            int bz) {
-    __shared__ int su[GBK * 64], si[GBK * 64];  // ids of up to 1024 rows of the chunk (FIRST)
+    static_assert(TB == 64 || (VEC && !FIRST), "the 128-tile core: 16-byte loaders, layers k >= 1");
+    constexpr int NT = TB / 32;
+    __shared__ int su[FIRST ? GBK * 64 : 1], si[FIRST ? GBK * 64 : 1];  // ids of up to 1024 rows of the chunk (FIRST)
     const Sel s = select_rows(a);
     const ncf_layout& lay = a.lay;
     const int DM = lay.factor_num << (lay.num_layers - 1);
     const int K = (2 * DM) >> k, J = K / 2;
-    const int j0 = bx * GBM;
-    const int c0 = by * GBN;
+    const int j0 = bx * TB;
+    const int c0 = by * TB;
     const int64_t r0 = (int64_t)bz * chunk;
     int64_t r1 = r0 + chunk;
     if (r1 > R) r1 = R;
@@ -618,11 +728,11 @@ __device__ __forceinline__ void bwd_w_body(const LyrArgs& a, int k, const float*
     auto sa1 = [&](const float& v) {
         if (dbt) db1 += v;
     };
-    auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
+    auto ep = [&](f4 (&acc)[NT][NT], int wm, int wn, int l) {
 #pragma unroll
-        for (int ti = 0; ti < 2; ++ti)
+        for (int ti = 0; ti < NT; ++ti)
 #pragma unroll
-            for (int tj = 0; tj < 2; ++tj) {
+            for (int tj = 0; tj < NT; ++tj) {
                 const int c = c0 + wn + 16 * tj + (l & 15);
                 if (c >= K) continue;
 #pragma unroll
@@ -706,27 +816,28 @@ __device__ __forceinline__ void bwd_w_body(const LyrArgs& a, int k, const float*
                 }
                 return v;
             };
-            gemm_block_vx<false, false>(r0, r1, ga4, gb4, ep, sa4);
+            gemm_tile<TB, false, false>(r0, r1, ga4, gb4, ep, sa4);
         } else {
-            gemm_block<false, false>(j0, c0, r0, r1, ga, gb, ep, sa1);
+            if constexpr (TB == 64) gemm_block<false, false>(j0, c0, r0, r1, ga, gb, ep, sa1);
         }
     }
     if (dbt) {  // db_k: per-thread column sums -> LDS -> one atomic per column per block
-        // A operand [16 rows of m][64 j]: VEC thread t holds j 4 (t % 16) .. + 3 of
-        // rows t / 16 (16 slots); scalar thread t holds j t % 64 of rows t / 64 (4 slots)
-        __shared__ float dred[16][GBM];
+        // A operand [TB / 4 rows of m][TB j] per load: VEC thread t holds j 4 (t % (TB / 4))
+        // .. + 3 (TB = 64: 16 slots, 128: 8); scalar thread t holds j t % 64 of rows t / 64
+        constexpr int NS = VEC ? 256 / (TB / 4) : 4;
+        __shared__ float dred[NS][TB];
         const int t = threadIdx.x;
         if constexpr (VEC) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) dred[t >> 4][4 * (t & 15) + i] = lane_get(db4, i);
+            for (int i = 0; i < 4; ++i) dred[t / (TB / 4)][4 * (t % (TB / 4)) + i] = lane_get(db4, i);
         } else {
             dred[t >> 6][t & 63] = db1;
         }
         __syncthreads();
-        if (t < GBM) {
+        if (t < TB) {
             float sum = 0.f;
 #pragma unroll
-            for (int q = 0; q < (VEC ? 16 : 4); ++q) sum += dred[q][t];
+            for (int q = 0; q < NS; ++q) sum += dred[q][t];
             const int j = j0 + t;
             if (j < J && sum != 0.f) atomicAdd(slab + (lay.b[k] - tb) + j, sum);
         }
@@ -766,6 +877,7 @@ struct BwMulti {
 };
 __device__ __forceinline__ void user_walk_body(const LyrArgs& a, const float* __restrict__ D0u, int64_t blk,
                                                int nt, int dm);
+template <int TB>
 __global__ __launch_bounds__(GNT) void lyr_bwd_w_multi_kernel(LyrArgs a, BwMulti m, int64_t R) {
     const int b = blockIdx.x;
     if (b >= m.start[m.n]) {  // block-uniform
@@ -778,7 +890,7 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_multi_kernel(LyrArgs a, BwMulti
         if (q < m.n && b >= m.start[q]) i = q;
     const int loc = b - m.start[i], per = m.gx[i] * m.gy[i];
     const int bz = loc / per, rem = loc - bz * per;
-    bwd_w_body<false, false, true>(a, m.k[i], m.D[i], m.A[i], R, m.chunk[i], rem % m.gx[i], rem / m.gx[i], bz);
+    bwd_w_body<false, false, true, TB>(a, m.k[i], m.D[i], m.A[i], R, m.chunk[i], rem % m.gx[i], rem / m.gx[i], bz);
 }
 
 // ---------------------------------------------------------------------------
@@ -788,23 +900,25 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_multi_kernel(LyrArgs a, BwMulti
 // through LDS over 64 rows (an LDS-free wave-per-16-rows variant re-read the 64 KB
 // W0 half per wave at dm 128: 15.5 against 9.4 us).  It is the step's first kernel
 // and also clears the slab (zp, zn4).
+template <int TB>
 __global__ __launch_bounds__(GNT) void lyr_proj_kernel(ncf_layout lay, const float* __restrict__ prm,
                                                        float* __restrict__ P, int nbu, float* __restrict__ zp,
                                                        int64_t zn4) {
     if (zp != nullptr) zero_share(zp, zn4);
+    constexpr int NT = TB / 32;  // 16 x 16 tiles per wave side
     const int DM = lay.factor_num << (lay.num_layers - 1);
     const bool user = (int)blockIdx.x < nbu;
     const int64_t nrows = user ? lay.user_num : lay.item_num;
-    const int64_t m0 = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * GBM;
-    const int n0 = blockIdx.y * GBN;
+    const int64_t m0 = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * TB;
+    const int n0 = blockIdx.y * TB;
     const float* X = prm + (user ? lay.um : lay.im);
     const float* W = prm + lay.w[0] + (user ? 0 : DM);  // row stride 2 DM
     float* Pout = P + (user ? 0 : (int64_t)lay.user_num * DM);
-    auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
+    auto ep = [&](f4 (&acc)[NT][NT], int wm, int wn, int l) {
 #pragma unroll
-        for (int ti = 0; ti < 2; ++ti)
+        for (int ti = 0; ti < NT; ++ti)
 #pragma unroll
-            for (int tj = 0; tj < 2; ++tj) {
+            for (int tj = 0; tj < NT; ++tj) {
                 const int n = n0 + wn + 16 * tj + (l & 15);
                 if (n >= DM) continue;
 #pragma unroll
@@ -822,7 +936,7 @@ __global__ __launch_bounds__(GNT) void lyr_proj_kernel(ncf_layout lay, const flo
         const int nn = n0 + n;
         return (nn < DM && c < DM) ? ld4(W + (int64_t)nn * 2 * DM + c) : zero4();
     };
-    gemm_block_vx<true, true>(0, DM, ga4, gb4, ep);  // factored path: dm in {8, ..., 128}
+    gemm_tile<TB, true, true>(0, DM, ga4, gb4, ep);  // factored path: dm in {8, ..., 512}
 }
 
 // H_1[m][n] = ReLU(P[u_m][n] + P[U + i_m][n] + b_0[n]), four outputs per thread
@@ -836,22 +950,24 @@ __global__ __launch_bounds__(GNT) void lyr_proj_kernel(ncf_layout lay, const flo
 //   lyr_fact_dw0_kernel  dW0[:, koff + c] += G^T X over row chunks of each table
 //                        (z < zu: users), into the slab's W0 columns (no partials at
 //                        dm > 128: the reductions read W0 from the slab)
+template <int TB>
 __global__ __launch_bounds__(GNT) void lyr_fact_dx_kernel(ncf_layout lay, const float* __restrict__ prm,
                                                           const float* __restrict__ grads, float* __restrict__ out,
                                                           int nbu) {
+    constexpr int NT = TB / 32;
     const int DM = lay.factor_num << (lay.num_layers - 1);
     const bool user = (int)blockIdx.x < nbu;
     const int64_t nrows = user ? lay.user_num : lay.item_num;
-    const int64_t m0 = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * GBM;
-    const int n0 = blockIdx.y * GBN;
+    const int64_t m0 = (int64_t)(user ? blockIdx.x : blockIdx.x - nbu) * TB;
+    const int n0 = blockIdx.y * TB;
     const float* G = grads + (user ? lay.um : lay.im);
     const float* W = prm + lay.w[0] + (user ? 0 : DM);  // W0[o][koff + i], row stride 2 DM
     float* O = out + (user ? 0 : (int64_t)lay.user_num * DM);
-    auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
+    auto ep = [&](f4 (&acc)[NT][NT], int wm, int wn, int l) {
 #pragma unroll
-        for (int ti = 0; ti < 2; ++ti)
+        for (int ti = 0; ti < NT; ++ti)
 #pragma unroll
-            for (int tj = 0; tj < 2; ++tj) {
+            for (int tj = 0; tj < NT; ++tj) {
                 const int n = n0 + wn + 16 * tj + (l & 15);
                 if (n >= DM) continue;
 #pragma unroll
@@ -869,10 +985,12 @@ __global__ __launch_bounds__(GNT) void lyr_fact_dx_kernel(ncf_layout lay, const 
         const int nn = n0 + n;
         return (k < DM && nn < DM) ? ld4(W + k * 2 * DM + nn) : zero4();
     };
-    gemm_block_vx<true, false>(0, DM, ga4, gb4, ep);
+    gemm_tile<TB, true, false>(0, DM, ga4, gb4, ep);
 }
 
+template <int TB>
 __global__ __launch_bounds__(GNT) void lyr_fact_dw0_kernel(LyrArgs a, int zu, int64_t chunk) {
+    constexpr int NT = TB / 32;
     const ncf_layout& lay = a.lay;
     const int DM = lay.factor_num << (lay.num_layers - 1);
     const bool user = (int)blockIdx.z < zu;
@@ -880,17 +998,17 @@ __global__ __launch_bounds__(GNT) void lyr_fact_dw0_kernel(LyrArgs a, int zu, in
     const int64_t r0 = (int64_t)(user ? blockIdx.z : blockIdx.z - zu) * chunk;
     const int64_t r1 = r0 + chunk < nrows ? r0 + chunk : nrows;
     if (r0 >= r1) return;  // block-uniform
-    const int o0 = blockIdx.x * GBM, c0 = blockIdx.y * GBN;
+    const int o0 = blockIdx.x * TB, c0 = blockIdx.y * TB;
     const float* G = a.grads + (user ? lay.um : lay.im);
     const float* X = a.params + (user ? lay.um : lay.im);
     const int koff = user ? 0 : DM;
     float* slab = a.slab + (int64_t)(blockIdx.z % lyr_slab_rows(&lay)) * (lay.tower_len + 64) +
                   (lay.w[0] - lay.tower_begin);
-    auto ep = [&](f4 (&acc)[2][2], int wm, int wn, int l) {
+    auto ep = [&](f4 (&acc)[NT][NT], int wm, int wn, int l) {
 #pragma unroll
-        for (int ti = 0; ti < 2; ++ti)
+        for (int ti = 0; ti < NT; ++ti)
 #pragma unroll
-            for (int tj = 0; tj < 2; ++tj) {
+            for (int tj = 0; tj < NT; ++tj) {
                 const int c = c0 + wn + 16 * tj + (l & 15);
                 if (c >= DM) continue;
 #pragma unroll
@@ -908,7 +1026,7 @@ __global__ __launch_bounds__(GNT) void lyr_fact_dw0_kernel(LyrArgs a, int zu, in
         const int c = c0 + cr;
         return (m < r1 && c < DM) ? ld4(X + m * DM + c) : zero4();
     };
-    gemm_block_vx<false, false>(r0, r1, ga4, gb4, ep);
+    gemm_tile<TB, false, false>(r0, r1, ga4, gb4, ep);
 }
 
 __global__ __launch_bounds__(GNT) void lyr_fwd0_fact_kernel(LyrArgs a, const float* __restrict__ P,
@@ -1674,15 +1792,63 @@ __global__ __launch_bounds__(GNT) void lyr_predict_kernel(LyrArgs a, const float
 
 #include "ncf_chain_wide.inc"
 
+// Block tile of the chained path's weight-gradient GEMMs (dm >= 256): X6W_TB, the 128 x
+// 128 core (stress: lyr_bwd_w_multi 230 -> 165 us per step), or 64 with NCF_GEMM_TILE=64
+// (A/B).  The projection and the factored expansion (K = dm = 512: 16 K steps) keep the
+// 64 x 64 core: with 128-tiles they ran at a quarter of the blocks and slower (proj 55 ->
+// 58, dX 56 -> 60, dW0 61 -> 68 us, profiles/r06_evidence/gemm_tile_ab/); NCF_PROJ_TILE=128
+// selects the 128 x 128 core for them (A/B).
+int lyr_gemm_tile() {
+    static int tb = -1;
+    if (tb < 0) {
+        const char* e = getenv("NCF_GEMM_TILE");
+        tb = (e != nullptr && atoi(e) == 64) ? 64 : X6W_TB;
+    }
+    return tb;
+}
+int lyr_proj_tile() {
+    static int tb = -1;
+    if (tb < 0) {
+        const char* e = getenv("NCF_PROJ_TILE");
+        tb = (e != nullptr && atoi(e) == X6W_TB) ? X6W_TB : 64;
+    }
+    return tb;
+}
+// dynamic LDS of a 128-tile kernel (set once per kernel)
+bool x6w_ready(const void* fn) {
+    static const void* done[8] = {};
+    for (const void* d : done)
+        if (d == fn) return true;
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, X6W_LDS) != hipSuccess) return false;
+    for (auto& d : done)
+        if (d == nullptr) {
+            d = fn;
+            break;
+        }
+    return true;
+}
+int64_t env_int(const char* name, int64_t dflt) {
+    const char* e = getenv(name);
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? (int64_t)v : dflt;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
 int lyr_launch_proj(const ncf_layout* lay, const float* params, float* P, float* zero, int64_t zero_floats,
                     hipStream_t st) {
     const int DM = lay->factor_num << (lay->num_layers - 1);
-    const int nbu = (int)((lay->user_num + GBM - 1) / GBM), nbi = (int)((lay->item_num + GBM - 1) / GBM);
-    hipLaunchKernelGGL(lyr_proj_kernel, dim3((unsigned)(nbu + nbi), (unsigned)((DM + GBN - 1) / GBN)), dim3(GNT), 0,
-                       st, *lay, params, P, nbu, zero, zero_floats / 4);
+    const int TB = DM >= 256 ? lyr_proj_tile() : 64;
+    const int nbu = (int)((lay->user_num + TB - 1) / TB), nbi = (int)((lay->item_num + TB - 1) / TB);
+    const dim3 grid((unsigned)(nbu + nbi), (unsigned)((DM + TB - 1) / TB));
+    if (TB == X6W_TB) {
+        if (!x6w_ready(reinterpret_cast<const void*>(&lyr_proj_kernel<X6W_TB>))) return NCF_E_LAUNCH;
+        hipLaunchKernelGGL(lyr_proj_kernel<X6W_TB>, grid, dim3(GNT), X6W_LDS, st, *lay, params, P, nbu, zero,
+                           zero_floats / 4);
+    } else {
+        hipLaunchKernelGGL(lyr_proj_kernel<64>, grid, dim3(GNT), 0, st, *lay, params, P, nbu, zero, zero_floats / 4);
+    }
     return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
 }
 
@@ -1706,14 +1872,24 @@ static int launch_gemm_expand(const LyrArgs& a, float* Pj, hipStream_t st) {
     const ncf_layout& lay = a.lay;
     const int DM = lay.factor_num << (lay.num_layers - 1);
     const int U = lay.user_num, I = lay.item_num;
-    const int nbu = (U + GBM - 1) / GBM, nbi = (I + GBM - 1) / GBM;
-    hipLaunchKernelGGL(lyr_fact_dx_kernel, dim3((unsigned)(nbu + nbi), (unsigned)((DM + GBN - 1) / GBN)), dim3(GNT),
-                       0, st, lay, a.params, a.grads, Pj, nbu);
-    const int64_t chunk = 256;
+    const int TB = lyr_proj_tile();
+    const int nbu = (U + TB - 1) / TB, nbi = (I + TB - 1) / TB;
+    const dim3 gx((unsigned)(nbu + nbi), (unsigned)((DM + TB - 1) / TB));
+    // dW0 row chunks: a 128 x 128 block does 4x the work per row of a 64 x 64 one, and
+    // each chunk adds its whole tile with float atomics (NCF_DW0_CHUNK: A/B)
+    const int64_t chunk = env_int("NCF_DW0_CHUNK", TB == X6W_TB ? 512 : 256);
     const int zu = (int)((U + chunk - 1) / chunk), zi = (int)((I + chunk - 1) / chunk);
-    hipLaunchKernelGGL(lyr_fact_dw0_kernel,
-                       dim3((unsigned)((DM + GBM - 1) / GBM), (unsigned)((DM + GBN - 1) / GBN), (unsigned)(zu + zi)),
-                       dim3(GNT), 0, st, a, zu, chunk);
+    const dim3 gw((unsigned)((DM + TB - 1) / TB), (unsigned)((DM + TB - 1) / TB), (unsigned)(zu + zi));
+    if (TB == X6W_TB) {
+        if (!x6w_ready(reinterpret_cast<const void*>(&lyr_fact_dx_kernel<X6W_TB>)) ||
+            !x6w_ready(reinterpret_cast<const void*>(&lyr_fact_dw0_kernel<X6W_TB>)))
+            return NCF_E_LAUNCH;
+        hipLaunchKernelGGL(lyr_fact_dx_kernel<X6W_TB>, gx, dim3(GNT), X6W_LDS, st, lay, a.params, a.grads, Pj, nbu);
+        hipLaunchKernelGGL(lyr_fact_dw0_kernel<X6W_TB>, gw, dim3(GNT), X6W_LDS, st, a, zu, chunk);
+    } else {
+        hipLaunchKernelGGL(lyr_fact_dx_kernel<64>, gx, dim3(GNT), 0, st, lay, a.params, a.grads, Pj, nbu);
+        hipLaunchKernelGGL(lyr_fact_dw0_kernel<64>, gw, dim3(GNT), 0, st, a, zu, chunk);
+    }
     if (hipMemcpyAsync(a.grads + lay.um, Pj, (size_t)U * DM * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
         hipMemcpyAsync(a.grads + lay.im, Pj + (int64_t)U * DM, (size_t)I * DM * 4, hipMemcpyDeviceToDevice, st) !=
             hipSuccess)
@@ -1814,10 +1990,16 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
     if (chained) {  // weight gradients of layers L-1 .. 1 (one launch), then the layer-0 scatter
         BwMulti bm;
         memset(&bm, 0, sizeof(bm));
-        for (int k = L - 1; k >= 1; --k) {
+        // blocks per layer (row splits x tiles): 1,024 64 x 64 blocks, or 256 of the 128
+        // x 128 core (4x the work per row each; the float atomics of the split partials
+        // stay at one dW per 2,048 rows of layer 1); layer 1 (the largest) first
+        const int TB = DM >= 256 ? lyr_gemm_tile() : 64;  // narrower towers: 64-row tiles fit
+        const int64_t bw_blocks = env_int("NCF_BW_BLOCKS", TB == X6W_TB ? 256 : 1024);
+        for (int kk = 1; kk <= L - 1; ++kk) {
+            const int k = TB == X6W_TB ? kk : L - kk;
             const int K = (2 * DM) >> k, J = K / 2;
-            const int64_t tiles = (int64_t)((J + GBM - 1) / GBM) * ((K + GBN - 1) / GBN);
-            int64_t splits = 1024 / tiles;
+            const int64_t tiles = (int64_t)((J + TB - 1) / TB) * ((K + TB - 1) / TB);
+            int64_t splits = bw_blocks / tiles;
             const int64_t max_splits = (R + 255) / 256;
             if (splits > max_splits) splits = max_splits;
             if (splits < 1) splits = 1;
@@ -1826,8 +2008,8 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             splits = (R + chunk - 1) / chunk;
             const int i = bm.n++;
             bm.k[i] = k;
-            bm.gx[i] = (J + GBM - 1) / GBM;
-            bm.gy[i] = (K + GBN - 1) / GBN;
+            bm.gx[i] = (J + TB - 1) / TB;
+            bm.gy[i] = (K + TB - 1) / TB;
             bm.D[i] = cb.D[k];
             bm.A[i] = H[k];
             bm.chunk[i] = chunk;
@@ -1840,9 +2022,15 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             bm.D0u = cb.D[0];
             bm.walk_dm = DM;
         }
-        if (bm.start[bm.n] + walk > 0)
-            hipLaunchKernelGGL(lyr_bwd_w_multi_kernel, dim3((unsigned)(bm.start[bm.n] + walk)), dim3(GNT), 0, st, a, bm,
-                               R);
+        if (bm.start[bm.n] + walk > 0) {
+            const dim3 grid((unsigned)(bm.start[bm.n] + walk));
+            if (TB == X6W_TB) {
+                if (!x6w_ready(reinterpret_cast<const void*>(&lyr_bwd_w_multi_kernel<X6W_TB>))) return NCF_E_LAUNCH;
+                hipLaunchKernelGGL(lyr_bwd_w_multi_kernel<X6W_TB>, grid, dim3(GNT), X6W_LDS, st, a, bm, R);
+            } else {
+                hipLaunchKernelGGL(lyr_bwd_w_multi_kernel<64>, grid, dim3(GNT), 0, st, a, bm, R);
+            }
+        }
         // with the user order the chain did the item runs and db_0 and left D_0 in user
         // order (the walk blocks of the launch above read it sequentially); without,
         // the full scatter

@@ -6,7 +6,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-ARGS="--steps 30 --warmup 5 --skip-cpu-baseline --skip-eval --kernel-steps 3"
+ARGS="--config ${CONFIG:-c3} --steps 30 --warmup 5 --skip-cpu-baseline --skip-eval --kernel-steps 3 --e2e-epochs 0"
+export FILTER="${FILTER:-ncf_step_kernel reduce_adam}"
 P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES"
 P2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_LDS"
 i=0
@@ -22,9 +23,10 @@ for f in glob.glob("gpurun_out/sq*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in acc.items():
-    if "ncf_step_kernel" not in k and "reduce_adam" not in k:
+    import os
+    if not any(f in k for f in os.environ["FILTER"].split()):
         continue
-    print(k[:60])
+    print(k.replace("(anonymous namespace)::", "")[:70])
     for c, v in sorted(d.items()):
         print(f"   {c:28s} {sum(v) / len(v):16.0f}  (n={len(v)})")
 PY
