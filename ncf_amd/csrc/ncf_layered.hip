@@ -494,6 +494,73 @@ __device__ __forceinline__ void gemm_block_x6w(int64_t kbeg, int64_t kend, GA ga
     ep(acc, wm, wn, l);
 }
 
+// gemm_block_x6b: the x6s core (64 x 64 block tile, 4 waves of 32 x 32) with the B
+// operand already split: bimg is the block's first 16-column group of a fragment-major
+// image (lyr_wc_prep_kernel's W0 images: per 16-column group ngs bytes, per K step of 32
+// three planes x 64 lanes x 16 B), read straight from memory (L2-resident, 1.5 MB per
+// image) one K step ahead.  Only A passes through LDS and the split, so a wave splits 2
+// fragments per 24 MFMAs instead of 4 (the weight operand is split once per step instead
+// of once per block).  Same planes, products and K order per element as x6s.
+template <bool AKC, class GA, class EP>
+__device__ __forceinline__ void gemm_block_x6b(int64_t kbeg, int64_t kend, GA ga4, const char* __restrict__ bimg,
+                                               int64_t ngs, EP ep) {
+    __shared__ __attribute__((aligned(16))) float As[2][64 * XBK];
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+    f4 ra[2];
+    bf16x8 fb[2][3], fn[2][3];
+    auto load_b = [&](int64_t k0, bf16x8 (&f)[2][3]) {
+        const char* p = bimg + (k0 / XBK) * 3072 + l * 16;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                f[j][q] = *reinterpret_cast<const bf16x8*>(p + (int64_t)(wn / 16 + j) * ngs + q * 1024);
+    };
+    f4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    x6s_load<AKC>(ga4, kbeg, t, ra);
+    load_b(kbeg, fb);
+    x6s_store<AKC>(As[0], t, ra);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t k0 = kbeg; k0 < kend; k0 += XBK) {
+        const bool more = k0 + XBK < kend;
+        if (more) {
+            x6s_load<AKC>(ga4, k0 + XBK, t, ra);
+            load_b(k0 + XBK, fn);
+        }
+        bf16x8 fa[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) x6s_frag(As[buf], wm + 16 * i + (l & 15), l, fa[i]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f4 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+            }
+        if (more) {
+            x6s_store<AKC>(As[buf ^ 1], t, ra);
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) fb[j][q] = fn[j][q];
+        }
+        __syncthreads();
+        buf ^= 1;
+    }
+    ep(acc, wm, wn, l);
+}
+
 // The GEMM core of the layered kernels' 16-byte loader path: the bf16 split core, or
 // (-DNCF_GEMM_F32, the A/B library variant) the f32-MFMA core.  (A variant that split
 // once per block into three bf16 plane images in LDS -- 48 KB per block, 3 blocks per
@@ -900,10 +967,12 @@ __global__ __launch_bounds__(GNT) void lyr_bwd_w_multi_kernel(LyrArgs a, BwMulti
 // through LDS over 64 rows (an LDS-free wave-per-16-rows variant re-read the 64 KB
 // W0 half per wave at dm 128: 15.5 against 9.4 us).  It is the step's first kernel
 // and also clears the slab (zp, zn4).
-template <int TB>
+// BPRE: W0 comes pre-split (bimg: the users' image, the items' one W0 image later;
+// lyr_wc_prep_kernel) through gemm_block_x6b
+template <int TB, bool BPRE = false>
 __global__ __launch_bounds__(GNT) void lyr_proj_kernel(ncf_layout lay, const float* __restrict__ prm,
                                                        float* __restrict__ P, int nbu, float* __restrict__ zp,
-                                                       int64_t zn4) {
+                                                       int64_t zn4, const char* __restrict__ bimg = nullptr) {
     if (zp != nullptr) zero_share(zp, zn4);
     constexpr int NT = TB / 32;  // 16 x 16 tiles per wave side
     const int DM = lay.factor_num << (lay.num_layers - 1);
@@ -936,7 +1005,13 @@ __global__ __launch_bounds__(GNT) void lyr_proj_kernel(ncf_layout lay, const flo
         const int nn = n0 + n;
         return (nn < DM && c < DM) ? ld4(W + (int64_t)nn * 2 * DM + c) : zero4();
     };
-    gemm_tile<TB, true, true>(0, DM, ga4, gb4, ep);  // factored path: dm in {8, ..., 512}
+    if constexpr (BPRE) {
+        static_assert(TB == 64, "pre-split B: the 64 x 64 core");
+        const int64_t ngs = (int64_t)(DM / 32) * 3072, img = (int64_t)(DM / 16) * ngs;
+        gemm_block_x6b<true>(0, DM, ga4, bimg + (user ? 0 : img) + (int64_t)(n0 / 16) * ngs, ngs, ep);
+    } else {
+        gemm_tile<TB, true, true>(0, DM, ga4, gb4, ep);  // factored path: dm in {8, ..., 512}
+    }
 }
 
 // H_1[m][n] = ReLU(P[u_m][n] + P[U + i_m][n] + b_0[n]), four outputs per thread
@@ -950,10 +1025,10 @@ __global__ __launch_bounds__(GNT) void lyr_proj_kernel(ncf_layout lay, const flo
 //   lyr_fact_dw0_kernel  dW0[:, koff + c] += G^T X over row chunks of each table
 //                        (z < zu: users), into the slab's W0 columns (no partials at
 //                        dm > 128: the reductions read W0 from the slab)
-template <int TB>
+template <int TB, bool BPRE = false>
 __global__ __launch_bounds__(GNT) void lyr_fact_dx_kernel(ncf_layout lay, const float* __restrict__ prm,
                                                           const float* __restrict__ grads, float* __restrict__ out,
-                                                          int nbu) {
+                                                          int nbu, const char* __restrict__ bimg = nullptr) {
     constexpr int NT = TB / 32;
     const int DM = lay.factor_num << (lay.num_layers - 1);
     const bool user = (int)blockIdx.x < nbu;
@@ -985,7 +1060,13 @@ __global__ __launch_bounds__(GNT) void lyr_fact_dx_kernel(ncf_layout lay, const 
         const int nn = n0 + n;
         return (k < DM && nn < DM) ? ld4(W + k * 2 * DM + nn) : zero4();
     };
-    gemm_tile<TB, true, false>(0, DM, ga4, gb4, ep);
+    if constexpr (BPRE) {
+        static_assert(TB == 64, "pre-split B: the 64 x 64 core");
+        const int64_t ngs = (int64_t)(DM / 32) * 3072, img = (int64_t)(DM / 16) * ngs;
+        gemm_block_x6b<true>(0, DM, ga4, bimg + (user ? 0 : img) + (int64_t)(n0 / 16) * ngs, ngs, ep);
+    } else {
+        gemm_tile<TB, true, false>(0, DM, ga4, gb4, ep);
+    }
 }
 
 template <int TB>
@@ -1806,6 +1887,15 @@ int lyr_gemm_tile() {
     }
     return tb;
 }
+// NCF_W0PRE=0: the wide chain's projection and dX split W0 per block (A/B)
+bool w0_pre_enabled() {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("NCF_W0PRE");
+        on = (e != nullptr && e[0] == '0') ? 0 : 1;
+    }
+    return on == 1;
+}
 int lyr_proj_tile() {
     static int tb = -1;
     if (tb < 0) {
@@ -1861,14 +1951,14 @@ int64_t lyr_workspace_floats(const ncf_layout* lay, int64_t rows, bool train, in
     for (int k = 1; k <= lay->num_layers; ++k) fl += rup64(rows * ((2 * DM) >> k));
     if (train) fl += 2 * rup64(rows * DM);
     if (train && fact_part_floats >= 0 && DM == wc::DM && lay->num_layers == wc::L)
-        fl += rup64((int64_t)wc::NCH * wc::CHUNK / 4);  // the wide chain's weight chunk images
+        fl += rup64((int64_t)wc::NCH * wc::CHUNK / 4 + 4 * wc::W0_IMG_BYTES / 4);  // the wide chain's weight images
     return fl;
 }
 
 // The factored expansion as GEMMs (dm > FACT_LDS_DM, after the layer-0 scatter): dX
 // into the dead projection buffer, dW0 into the slab's W0 columns (both read G), then
 // dX copied over G.
-static int launch_gemm_expand(const LyrArgs& a, float* Pj, hipStream_t st) {
+static int launch_gemm_expand(const LyrArgs& a, float* Pj, hipStream_t st, const char* w0img = nullptr) {
     const ncf_layout& lay = a.lay;
     const int DM = lay.factor_num << (lay.num_layers - 1);
     const int U = lay.user_num, I = lay.item_num;
@@ -1880,7 +1970,11 @@ static int launch_gemm_expand(const LyrArgs& a, float* Pj, hipStream_t st) {
     const int64_t chunk = env_int("NCF_DW0_CHUNK", TB == X6W_TB ? 512 : 256);
     const int zu = (int)((U + chunk - 1) / chunk), zi = (int)((I + chunk - 1) / chunk);
     const dim3 gw((unsigned)((DM + TB - 1) / TB), (unsigned)((DM + TB - 1) / TB), (unsigned)(zu + zi));
-    if (TB == X6W_TB) {
+    if (w0img != nullptr && TB == 64) {  // dX with W0 pre-split (images 2, 3 of lyr_wc_prep_kernel)
+        hipLaunchKernelGGL((lyr_fact_dx_kernel<64, true>), gx, dim3(GNT), 0, st, lay, a.params, a.grads, Pj, nbu,
+                           w0img + 2 * wc::W0_IMG_BYTES);
+        hipLaunchKernelGGL(lyr_fact_dw0_kernel<64>, gw, dim3(GNT), 0, st, a, zu, chunk);
+    } else if (TB == X6W_TB) {
         if (!x6w_ready(reinterpret_cast<const void*>(&lyr_fact_dx_kernel<X6W_TB>)) ||
             !x6w_ready(reinterpret_cast<const void*>(&lyr_fact_dw0_kernel<X6W_TB>)))
             return NCF_E_LAUNCH;
@@ -1941,6 +2035,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
         return NCF_E_LAUNCH;
     }
     const unsigned mt = (unsigned)((R + GBM - 1) / GBM);
+    char* w0img = nullptr;  // the pre-split W0 images of the wide chain's step (W0PRE)
     // factored training with f % 4 == 0: the step chain (forward, predict, data
     // gradients in one launch); D_0 in Da, D_1 .. D_{L-1} packed into Db
     ChainBufs cb;
@@ -1960,13 +2055,24 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             const int N = (2 * DM) >> (k + 1);
             const dim3 grid(mt, (unsigned)((N + GBN - 1) / GBN));
             if (k == 0 && fact) {
-                if (lyr_launch_proj(&lay, a.params, Pj, a.zero_p, 4 * a.zero_n4, st) != NCF_OK) return NCF_E_LAUNCH;
+                // the wide chain: its weight images (and W0's for the projection and the
+                // expansion, W0PRE) prepared first, in one launch
+                const bool wide_ok = vec && !drop && wide_chain_applies(lay);
+                char* wimg = reinterpret_cast<char*>(ws + off);
+                if (wide_ok && w0_pre_enabled()) {
+                    w0img = wimg + (int64_t)wc::NCH * wc::CHUNK;
+                    launch_wc_prep(a, wimg, w0img, st);
+                    const int nbu = (lay.user_num + 63) / 64, nbi = (lay.item_num + 63) / 64;
+                    hipLaunchKernelGGL((lyr_proj_kernel<64, true>), dim3((unsigned)(nbu + nbi), (unsigned)(DM / 64)),
+                                       dim3(GNT), 0, st, lay, a.params, Pj, nbu, a.zero_p, a.zero_n4, w0img);
+                } else if (lyr_launch_proj(&lay, a.params, Pj, a.zero_p, 4 * a.zero_n4, st) != NCF_OK) {
+                    return NCF_E_LAUNCH;
+                }
                 if (vec && !drop && launch_step_chain(a, Pj, cb, R, st)) {
                     chained = true;
                     break;
                 }
-                if (vec && !drop && DM == wc::DM && L == wc::L &&
-                    launch_wide_chain(a, Pj, cb, reinterpret_cast<char*>(ws + off), R, st)) {
+                if (wide_ok && launch_wide_chain(a, Pj, cb, wimg, R, st, w0img != nullptr)) {
                     chained = wide = true;
                     break;
                 }
@@ -2044,7 +2150,7 @@ int lyr_run(const LyrArgs& a0, float* ws, int64_t R, bool train, hipStream_t st)
             default: return NCF_E_UNSUPPORTED;
         }
 #undef NCF_L0
-        if (DM > FACT_LDS_DM && launch_gemm_expand(a, Pj, st) != NCF_OK) return NCF_E_LAUNCH;
+        if (DM > FACT_LDS_DM && launch_gemm_expand(a, Pj, st, w0img) != NCF_OK) return NCF_E_LAUNCH;
         return hipGetLastError() == hipSuccess ? NCF_OK : NCF_E_LAUNCH;
     }
     int G = 1;

@@ -72,8 +72,9 @@ def test_abi_version_and_layout():
     assert L.hip().ncf_fact_mode(ctypes.byref(lay)) == 1
     assert 1 <= rows <= 16 and L.hip().ncf_fact_partials_bytes(ctypes.byref(lay)) == 0
     proj = (6041 + 3707) * dm
-    # plus the wide step chain's weight chunk images (ncf_chain_wide.inc: 42 chunks of 48 KB)
-    wc = 42 * 48 * 1024 // 4
+    # plus the wide step chain's weight images (ncf_chain_wide.inc: 42 chunks of 48 KB and
+    # four pre-split W0 images of 1.5 MB)
+    wc = 42 * 48 * 1024 // 4 + 4 * 32 * 16 * 3072 // 4
     assert (acts + proj + wc) * 4 <= ws <= (acts + proj + wc + rows * (lay.tower_len + 64) + 64 * 10) * 4
     # NCF(32,3) at ml-1m: factored layer 0 on the layered path (ABI 10): the
     # workspace adds the dW0 partials and the two tables' projections
