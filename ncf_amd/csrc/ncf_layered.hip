@@ -1965,9 +1965,10 @@ static int launch_gemm_expand(const LyrArgs& a, float* Pj, hipStream_t st, const
     const int TB = lyr_proj_tile();
     const int nbu = (U + TB - 1) / TB, nbi = (I + TB - 1) / TB;
     const dim3 gx((unsigned)(nbu + nbi), (unsigned)((DM + TB - 1) / TB));
-    // dW0 row chunks: a 128 x 128 block does 4x the work per row of a 64 x 64 one, and
-    // each chunk adds its whole tile with float atomics (NCF_DW0_CHUNK: A/B)
-    const int64_t chunk = env_int("NCF_DW0_CHUNK", TB == X6W_TB ? 512 : 256);
+    // dW0 row chunks: each chunk adds its whole tile with float atomics; 512 rows (16 K
+    // steps per block) against 256 took the stress step 846 -> 832 us (NCF_DW0_CHUNK:
+    // A/B, profiles/r06_evidence/dw0_chunk_ab/)
+    const int64_t chunk = env_int("NCF_DW0_CHUNK", 512);
     const int zu = (int)((U + chunk - 1) / chunk), zi = (int)((I + chunk - 1) / chunk);
     const dim3 gw((unsigned)((DM + TB - 1) / TB), (unsigned)((DM + TB - 1) / TB), (unsigned)(zu + zi));
     if (w0img != nullptr && TB == 64) {  // dX with W0 pre-split (images 2, 3 of lyr_wc_prep_kernel)
