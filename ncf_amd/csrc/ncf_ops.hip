@@ -2711,7 +2711,15 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
     const int rows = reduce_rows(lay);
     const int64_t etotal = RE.prefix[RE.n];
     int64_t nB = (etotal + 255) / 256;
-    if (nB > 2048) nB = 2048;
+    // embedding-Adam blocks at most: one float4 per thread up to 2M float4 (C4's 3.3M
+    // float4: 8192 against 2048 blocks took the step 132.4 -> 129.8 us; 16384 / 65536 the
+    // same as 8192; profiles/r06_evidence/adam_blocks_ab/).  NCF_ADAM_MAXB: A/B
+    static const int64_t max_b = [] {
+        const char* e = getenv("NCF_ADAM_MAXB");
+        const long v = e ? atol(e) : 0;
+        return (int64_t)(v > 0 ? v : 8192);
+    }();
+    if (nB > max_b) nB = max_b;
     hipLaunchKernelGGL(reduce_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
                        static_cast<const float*>(workspace), lo, stride, rows, nA, lay->tower_begin, lay->tower_len,
                        params, grads, exp_avg, exp_avg_sq, R, RE, ctl, lr, beta1, beta2, (float)eps, loss_hist,
