@@ -77,19 +77,21 @@ def test_feature_plan_rejects_matched_tower_features():
 
 
 def _build_ml1m(strategy, seed=7):
-    from src.distillation import FeatureDistillation, ResponseDistillation
+    from src.distillation import AttentionDistillation, FeatureDistillation, ResponseDistillation
     from src.ncf.models import NCF
     torch.manual_seed(seed)
     teacher = NCF(6041, 3707, 16, 3, 0.0, "NeuMF-end")
     student = NCF(6041, 3707, 8, 2, 0.0, "MLP")
     if strategy == "response":
         d = ResponseDistillation(teacher, student, temperature=2.0, alpha=0.5)
+    elif strategy == "attention":
+        d = AttentionDistillation(teacher, student, temperature=2.0, alpha=0.5, gamma=0.2)
     else:
         d = FeatureDistillation(teacher, student, temperature=2.0, alpha=0.5, beta=0.3)
     return teacher, student, d
 
 
-@pytest.mark.parametrize("strategy", ["response", "feature"])
+@pytest.mark.parametrize("strategy", ["response", "feature", "attention"])
 def test_device_plan_at_c5_id_space_vs_cpu_modules(strategy):
     """C5's own shape (bench config c5: teacher NCF(16,3,'NeuMF-end') -> student
     NCF(8,2,'MLP') at the ml-1m id space, 256-row batches, Adam 1e-3): the device plan
