@@ -67,11 +67,15 @@ def test_roofline_traffic_sources_in_committed_profiles():
     import bench
     t, busy, src = bench.layered_profile("stress")
     assert src is not None and t > 1e9 and 0 < busy < 1, (t, busy, src)
-    # weights per step: the step's three forward GEMM launches count three times
+    # weights per step: one launch each per step of the projection (the step's first),
+    # the wide step chain and the weight-gradient launch (round 6; the per-layer GEMM
+    # launches of earlier profiles counted per layer)
     d = json.load(open(os.path.join(ROOT, src)))
     ks = {k["kernel"]: k for k in d["kernels"]}
-    fwd = ks["ncf::lyr_fwd_kernel<false, false, true>"]
-    assert fwd["calls"] == 3 * ks["ncf::lyr_proj_kernel"]["calls"]
+    proj = [k for n, k in ks.items() if n.startswith("ncf::lyr_proj_kernel")]
+    assert len(proj) == 1
+    for name in ("ncf::lyr_wide_chain_kernel", "ncf::lyr_bwd_w_multi_kernel<128>"):
+        assert ks[name]["calls"] == proj[0]["calls"], name
     assert bench.layered_profile("cli")[0] is not None
     tr, src3 = bench.pmc_traffic("c3", ["ncf::ncf_step_kernel<16, 3, 2, false, true, 8>",
                                         "ncf::fact_expand_kernel<64>"])
