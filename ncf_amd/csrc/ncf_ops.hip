@@ -283,20 +283,69 @@ __device__ __forceinline__ void tower_reduce_adam_block(const float* __restrict_
     }
 }
 
+// Tower block for slabs of at most 16 rows and no dW0 partials (the layered path: 1-16
+// rows; the fused small-batch steps: one row per workgroup): one float4 column per
+// thread, its rows summed in order (the same additions as the 16-row-group form: rows 0,
+// 1, ..., then the empty groups' zeros, folded into one + 0), then Adam -- every thread
+// updates, where the 16 x 16 form reduced through LDS with one thread in 16 updating
+// (a stress tower of 700K floats ran 11K such blocks).
+__device__ __forceinline__ void tower_col_adam(const float* __restrict__ slab, int lo, int stride, int rows,
+                                               int64_t tb, int64_t tower_len, float* __restrict__ p,
+                                               float* __restrict__ m, float* __restrict__ v, const Ranges& R,
+                                               int64_t t_step, int64_t b_step, double lr, double beta1,
+                                               double beta2, float eps, float* loss_hist, int64_t hist_len, float* sc,
+                                               const ScCache* scc) {
+#pragma clang fp contract(off)
+    const ScCache sce = sc_peek(scc, t_step);
+    const float w1 = (float)(1.0 - beta1), b2 = (float)beta2, omb2 = (float)(1.0 - beta2);
+    const int j = lo + ((int)blockIdx.x * 256 + (int)threadIdx.x) * 4;
+    const int64_t i = tb + j;
+    const bool upd = j < tower_len && in_ranges(R, i);
+    f4 pp, mm, vv;
+    if (upd) {
+        pp = *reinterpret_cast<const f4*>(p + i);
+        mm = *reinterpret_cast<const f4*>(m + i);
+        vv = *reinterpret_cast<const f4*>(v + i);
+    }
+    f4 x[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        x[r] = (r < rows && j < stride) ? *reinterpret_cast<const f4*>(slab + (int64_t)r * stride + j)
+                                        : f4{0.f, 0.f, 0.f, 0.f};
+    f4 gs = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if (r < rows) { gs.x += x[r].x; gs.y += x[r].y; gs.z += x[r].z; gs.w += x[r].w; }
+    if (rows < 16) { gs.x += 0.f; gs.y += 0.f; gs.z += 0.f; gs.w += 0.f; }
+    sc_resolve(sce, t_step, lr, beta1, beta2, sc);
+    __syncthreads();
+    if (j == tower_len) {
+        if (loss_hist != nullptr && hist_len > 0) loss_hist[((b_step % hist_len) + hist_len) % hist_len] = gs.x;
+    } else if (upd) {
+        adam_f4(pp, mm, vv, gs, w1, b2, omb2, sc[1], eps, sc[0]);
+        *reinterpret_cast<f4*>(m + i) = mm;
+        *reinterpret_cast<f4*>(v + i) = vv;
+        *reinterpret_cast<f4*>(p + i) = pp;
+    }
+}
+
 __global__ __launch_bounds__(256) void reduce_adam_kernel(const float* __restrict__ slab, int lo, int stride, int rows,
                                                           int nA, int64_t tb, int64_t tower_len, float* __restrict__ p,
                                                           float* __restrict__ g, float* __restrict__ m,
                                                           float* __restrict__ v, Ranges R, Ranges RE,
                                                           ncf_step_ctl* ctl, double lr, double beta1, double beta2,
                                                           float eps, float* loss_hist, int64_t hist_len, W0Part wp,
-                                                          ScCache* scc) {
+                                                          ScCache* scc, int colmode) {
 #pragma clang fp contract(off)
     __shared__ float sc[2];
     __shared__ f4 part[16][16];
     const int64_t t_step = ctl->snap_t;
     const int64_t b_step = ctl->snap_batch;
     step_scalars_ahead(scc, t_step, lr, beta1, beta2);
-    if ((int)blockIdx.x < nA) {
+    if ((int)blockIdx.x < nA && colmode) {
+        tower_col_adam(slab, lo, stride, rows, tb, tower_len, p, m, v, R, t_step, b_step, lr, beta1, beta2, eps,
+                       loss_hist, hist_len, sc, scc);
+    } else if ((int)blockIdx.x < nA) {
         tower_reduce_adam_block(slab, lo, stride, rows, tb, tower_len, p, m, v, R, t_step, b_step, lr, beta1, beta2,
                                 eps, loss_hist, hist_len, wp, sc, part, scc);
     } else {
@@ -2707,8 +2756,19 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
     }
     const int stride = (int)ncf_slab_stride(lay);
     const int lo = slab_lo(lay);
-    const int nA = (stride - lo + 63) / 64;
     const int rows = reduce_rows(lay);
+    const W0Part wp = w0_part(lay, workspace);
+    // tower blocks: one float4 column per thread on the layered path (slab of <= 16 rows,
+    // no dW0 partials): stress 857 -> 841 us/step; CLI unchanged; on the fused
+    // small-batch step (C2: 16 rows, a 6K-float tower, 6 such blocks) the 16 x 16 form
+    // stays, 18.6 against 19.7 us (profiles/r06_evidence/tower_col_ab/).  NCF_TOWER_COL=0:
+    // the 16 x 16 form everywhere (A/B)
+    static const bool col_ok = [] {
+        const char* e = getenv("NCF_TOWER_COL");
+        return !(e != nullptr && e[0] == '0');
+    }();
+    const int colmode = col_ok && rows <= 16 && wp.p == nullptr && train_fused(lay) == nullptr ? 1 : 0;
+    const int nA = colmode ? ((stride - lo) / 4 + 1 + 255) / 256 : (stride - lo + 63) / 64;
     const int64_t etotal = RE.prefix[RE.n];
     int64_t nB = (etotal + 255) / 256;
     // embedding-Adam blocks at most: one float4 per thread up to 2M float4 (C4's 3.3M
@@ -2723,7 +2783,7 @@ int ncf_reduce_adam_step(const ncf_layout* lay, const void* workspace, float* pa
     hipLaunchKernelGGL(reduce_adam_kernel, dim3((unsigned)(nA + nB)), dim3(256), 0, (hipStream_t)stream,
                        static_cast<const float*>(workspace), lo, stride, rows, nA, lay->tower_begin, lay->tower_len,
                        params, grads, exp_avg, exp_avg_sq, R, RE, ctl, lr, beta1, beta2, (float)eps, loss_hist,
-                       hist_len, w0_part(lay, workspace), sc_cache_for(ctl, stream));
+                       hist_len, wp, sc_cache_for(ctl, stream), colmode);
     return launch_status();
 }
 
